@@ -1,0 +1,223 @@
+"""Benchmark: device-resident XXH3-128 content hashing (the `oxen add` hash stage) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c4]
+
+One step = one batched K1 launch hashing every buffer of the rank's shard, already resident in HBM
+(plus, for N > 1, the single all-gather of the 16-B digest table over RCCL). Workload (weak
+scaling, per GPU): BASELINE.json configs[1] -- 100 000 x 64 KiB splitmix64 blobs (6.1 GiB).
+Prints ONE JSON line on rank 0 (the driver's contract), including:
+  roofline      achieved HBM read GB/s of the K1 kernel (algorithmic bytes = buffer lengths) vs the
+                8 TB/s MI355X peak; `traffic` = PMC-measured HBM bytes per launch when a matching
+                profiles/*traffic*.json exists (rocprofv3 FETCH_SIZE, gfx950 x2 correction).
+  cpu_baseline  the C oracle (oracle/, a restatement of the reference's XXH3-128) timed on the
+                host cores over a bounded sample of the same workload; the GPU digests of that
+                sample are checked bit-exact against it.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s hashed device-resident on `oxen add` (N files); digests bit-exact"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+WORKLOADS = {
+    # name: (items per GPU, bytes per item, BASELINE config)
+    "c2": (100_000, 65_536, "100 000 x 64 KiB random blobs, device-resident, 1 MI355X (BASELINE configs[1])"),
+    "c4": (125_000, 262_144, "1 000 000 x 256 KiB blobs / 8 GPUs = 125 000 x 256 KiB per GPU (BASELINE configs[3])"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(da, gpu_digests: np.ndarray, seed: int, budget_s: float = 10.0) -> dict:
+    """Oracle (C, multi-threaded) on a bounded sample regenerated on the host; checks GPU digests."""
+    from oracle import oracle
+    from oxen_amd.workloads import splitmix_bytes
+
+    oracle.build()
+    threads = min(16, os.cpu_count() or 1)
+    item_len = int(da.lens_host[0])
+    nsample = min(da.n, max(threads, (256 << 20) // max(item_len, 1)))
+    idx = np.linspace(0, da.n - 1, nsample).astype(np.int64)
+    host = np.empty(nsample * item_len, dtype=np.uint8)
+    for j, i in enumerate(idx):
+        host[j * item_len:(j + 1) * item_len] = splitmix_bytes(seed, int(da.offsets_host[i]), item_len)
+    offs = np.arange(nsample, dtype=np.uint64) * np.uint64(item_len)
+    lens = np.full(nsample, item_len, dtype=np.uint64)
+    want = oracle.batch(host, offs, lens, threads)  # warm + reference digests
+    exact = bool(np.array_equal(want, gpu_digests[idx]))
+    t0 = time.perf_counter()
+    passes = 0
+    while True:
+        oracle.batch(host, offs, lens, threads)
+        passes += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    gib = passes * nsample * item_len / 2**30
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(gib / dt, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{nsample} of {da.n} items x {item_len} B ({nsample * item_len / 2**20:.0f} MiB), "
+                      f"{passes} passes in {dt:.1f} s, oracle/xxh3_oracle.c scalar C, {threads} threads, {cpu_model}",
+            "digests_bit_exact_on_sample": exact}
+
+
+def load_traffic(workload: str):
+    """PMC-derived HBM bytes per K1 launch for this workload, if profiled (tools/pmc_traffic.py)."""
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json"))):
+        try:
+            d = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
+            best = d
+    return best
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--variant", type=int, default=0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+    dev = torch.device(f"cuda:{local_rank}")
+    torch.cuda.set_device(dev)
+
+    from oxen_amd import _capi
+    from oxen_amd import build as hb
+    from oxen_amd.device import DeviceArena, to_numpy_u64
+    from oxen_amd.shard import gather_digest_table
+
+    if rank == 0:
+        hb.build()
+    if world > 1:
+        dist.barrier()
+    _capi.lib().oxh_set_kernel_variant(args.variant)
+
+    n_items, item_len, desc = WORKLOADS[args.workload]
+    # weak scaling: every rank owns its own n_items (global item ids rank*n_items ...); the seed is
+    # offset per rank so shards differ
+    seed = args.seed + rank
+    lens = np.full(n_items, item_len, dtype=np.uint64)
+    da = DeviceArena.splitmix(lens, seed=seed, device=dev)
+    out = torch.empty((n_items, 2), dtype=torch.int64, device=dev)
+    counts = [n_items] * world
+    torch.cuda.synchronize()
+
+    def step():
+        da.hash(out)
+        if world > 1:
+            return gather_digest_table(out, counts)
+        return out
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        table = step()
+    ev1.record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    gpu_s = ev0.elapsed_time(ev1) / 1e3
+    # per-launch kernel time, from HIP events on the launch stream (no collective in this window)
+    kev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    kev[0].record()
+    kreps = max(5, args.steps)
+    for _ in range(kreps):
+        da.hash(out)
+    kev[1].record()
+    torch.cuda.synchronize()
+    kernel_s = kev[0].elapsed_time(kev[1]) / 1e3 / kreps
+
+    elapsed = max(wall, gpu_s)
+    t = torch.tensor([elapsed, kernel_s], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kernel_max = float(t[0]), float(t[1])
+
+    bytes_per_rank = int(lens.sum())
+    total_bytes = bytes_per_rank * world * args.steps
+    value = total_bytes / elapsed / 2**30
+
+    result = None
+    if rank == 0:
+        digests = to_numpy_u64(out).reshape(-1, 2)
+        if world > 1:
+            assert table.shape[0] == n_items * world
+            assert np.array_equal(to_numpy_u64(table[:n_items]).reshape(-1, 2), digests)
+        achieved = bytes_per_rank / kernel_s / 1e9
+        tr = load_traffic(args.workload)
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": (tr["hbm_bytes_per_launch"] if tr else None),
+                    "kernel": "xxh3_wave_kernel (K1)", "kernel_ms": round(kernel_s * 1e3, 4),
+                    "algorithmic_bytes_per_launch": bytes_per_rank}
+        if tr:
+            roofline["traffic_source"] = tr.get("source")
+        cpu = None
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(da, digests, seed, args.cpu_budget)
+        result = {
+            "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (splitmix64 byte stream, seed %d+rank), device-resident in HBM" % args.seed,
+            "config": {"workload": desc, "items_per_gpu": n_items, "item_bytes": item_len,
+                       "bytes_per_gpu": bytes_per_rank, "parallelism": f"files sharded x{world}, RCCL all-gather of digests" if world > 1 else "single GPU",
+                       "kernel_variant": args.variant},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,125 @@
+/*
+ * include/oxen_hash.h -- C ABI of the MI355X content-hashing stage for `oxen add` / commit.
+ *
+ * Drop-in boundary for liboxen's `util::hasher` module (crates/liboxen/src/util/hasher.rs) and the
+ * per-file hash call in the add loop (crates/liboxen/src/core/v_latest/add.rs:716-718,741-743).
+ * Every digest is XXH3-128 with seed 0 and the default secret -- bit-identical to
+ * `xxhash_rust::xxh3::xxh3_128` (xxhash-rust 0.8.15) -- returned as two u64 words per item:
+ * out[2*i] = low 64 bits, out[2*i+1] = high 64 bits, i.e. the Rust `u128` is
+ * `((hi as u128) << 64) | lo as u128` (MerkleHash, model/merkle_tree/merkle_hash.rs:16).
+ *
+ * Conventions:
+ *   - plain pointers and sizes only; no torch / Rust / HIP-runtime types in the signatures
+ *     (`stream` is an opaque hipStream_t, NULL = the context's own stream);
+ *   - every function returns an int status (OXH_OK == 0); batch calls also fill a per-item
+ *     `status[]` so one unreadable file never fails the batch (add.rs:533-544 logs and skips);
+ *   - the library never frees caller memory and retains no caller pointer after returning;
+ *   - all entry points are thread-safe; calls on one context are serialised internally;
+ *   - there is no CPU fallback: without a usable gfx950 device, calls fail with OXH_ERR_NODEVICE.
+ *
+ * The Rust-side `extern "C"` block that binds these is in INTEGRATION.md.
+ */
+#ifndef OXEN_HASH_H
+#define OXEN_HASH_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OXH_ABI_VERSION 1
+
+/* status codes (also used per item in status[]) */
+#define OXH_OK 0
+#define OXH_ERR_INVALID 1   /* bad argument */
+#define OXH_ERR_HIP 2       /* HIP runtime error */
+#define OXH_ERR_IO 3        /* file could not be opened/read (hasher.rs:137-145, 151-164) */
+#define OXH_ERR_NOMEM 4     /* host or device allocation failed */
+#define OXH_ERR_NODEVICE 5  /* no usable MI355X (gfx950) device */
+
+/* kernel selection for the device-resident batch */
+#define OXH_MODE_AUTO 0     /* one wave per buffer (K1), lane-per-item for short-only batches */
+#define OXH_MODE_WAVE 1     /* force K1: one 64-lane wave per buffer */
+#define OXH_MODE_LANE 2     /* force K1s: one lane per buffer (short items, parent-node streams) */
+
+typedef struct oxh_ctx oxh_ctx;
+
+/* ---------------------------------------------------------------- library / context */
+int oxh_abi_version(void);
+/* Thread-local text of the last error on this thread ("" if none). */
+const char* oxh_last_error(void);
+/* Number of visible HIP devices (0 on a host without a GPU). */
+int oxh_device_count(int* count);
+/* Create a hashing context on `device`: owns a compute stream, a copy stream, pinned host staging
+ * (`staging_bytes` per slot, 0 = default 256 MiB, 3 slots) and matching device slots. */
+int oxh_ctx_create(int device, uint64_t staging_bytes, oxh_ctx** out);
+int oxh_ctx_destroy(oxh_ctx* ctx);
+/* The context's compute stream (hipStream_t), for callers that want to order against it. */
+void* oxh_ctx_stream(oxh_ctx* ctx);
+
+/* ---------------------------------------------------------------- K1 / K1s: device-resident batch
+ * Replaces N calls of `hash_buffer_128bit(&[u8]) -> u128` (hasher.rs:28-30) over buffers that are
+ * already resident in HBM: item i is d_arena[d_offsets[i] .. d_offsets[i] + d_lens[i]).
+ * d_offsets / d_lens / d_out are device pointers; d_out receives 2*n u64. Asynchronous on `stream`.
+ * Buffers starting on a 16-byte boundary take the coalesced dwordx4 path; others stay correct. */
+int oxh_xxh3_128_batch_device(const void* d_arena, const uint64_t* d_offsets, const uint64_t* d_lens,
+                              uint64_t n, uint64_t* d_out, int mode, void* stream);
+
+/* Fixed-size chunk digests of one device-resident buffer (block-level dedup,
+ * experiments/block-level-dedup/src/chunker/fixedsize.rs:52-102): chunk i is
+ * d_buf[i*chunk .. min((i+1)*chunk, len)); d_out receives 2*ceil(len/chunk) u64. */
+int oxh_chunk_digests_device(const void* d_buf, uint64_t len, uint64_t chunk, uint64_t* d_out,
+                             void* stream);
+
+/* K1L: whole-buffer digest of one large device-resident buffer (files >= 1e9 B take the streamed
+ * branch in hasher.rs:150-174; the digest is the same XXH3-128). Block sums are computed in
+ * parallel across the chip, then the serial scramble chain runs on one wave. `d_out` gets 2 u64. */
+int oxh_xxh3_128_large_device(oxh_ctx* ctx, const void* d_buf, uint64_t len, uint64_t* d_out,
+                              void* stream);
+
+/* ---------------------------------------------------------------- host-resident entry points
+ * These block until the digests are in host memory. */
+
+/* hash_buffer_128bit x n over host buffers (pinned staging, H2D on a side stream, K1, D2H). */
+int oxh_hash_buffers(oxh_ctx* ctx, const uint8_t* const* bufs, const uint64_t* lens, uint64_t n,
+                     uint64_t* out);
+
+/* get_hash_given_metadata / u128_hash_file_contents x n (hasher.rs:56-65,102-112): reads each file
+ * whole (parallel readers straight into pinned staging), overlaps H2D with hashing, and returns
+ * digests, file sizes and a per-file status (OXH_OK or OXH_ERR_IO; digest 0 on error).
+ * `sizes` and `status` may be NULL. */
+int oxh_hash_files(oxh_ctx* ctx, const char* const* paths, uint64_t n, uint64_t* out,
+                   uint64_t* sizes, int32_t* status);
+
+/* ---------------------------------------------------------------- K2: merkle parent nodes */
+/* get_combined_hash (hasher.rs:67-80) x n on the device:
+ * XXH3-128(content.to_le_bytes() || metadata.to_le_bytes()), inputs as (lo, hi) pairs. */
+int oxh_combined_hash_device(const uint64_t* d_content, const uint64_t* d_metadata, uint64_t n,
+                             uint64_t* d_out, void* stream);
+/* Host-resident batch of caller-serialised parent streams (vnode ids, commit_writer.rs:686-720;
+ * dir hashes, commit_writer.rs:995-1147; metadata JSON, hasher.rs:95-100): item i is
+ * streams[offsets[i] .. offsets[i] + lens[i]). Blocks until `out` (2n u64) is filled. */
+int oxh_hash_streams(oxh_ctx* ctx, const uint8_t* streams, const uint64_t* offsets,
+                     const uint64_t* lens, uint64_t n, uint64_t* out);
+
+/* ---------------------------------------------------------------- formatting (host only) */
+/* MerkleHash Display (merkle_hash.rs:73-77): format!("{:x}") -- lowercase, NOT zero-padded.
+ * `out` must hold 33 bytes; returns the string length (1..32). */
+int oxh_format_hex(uint64_t lo, uint64_t hi, char* out);
+/* u128::to_string() -- the decimal chunk names of the dedup experiment (fixedsize.rs:78).
+ * `out` must hold 40 bytes; returns the string length. */
+int oxh_format_dec(uint64_t lo, uint64_t hi, char* out);
+
+/* ---------------------------------------------------------------- bench / test utilities */
+/* Fill d_buf[0..nbytes) with the counter-based splitmix64 byte stream of `seed` (byte j is byte
+ * j%8, little-endian, of splitmix64(seed + (j/8 + 1) * 0x9E3779B97F4A7C15)) so that a host can
+ * regenerate any item of a device-resident synthetic workload without copying it back. */
+int oxh_fill_splitmix(void* d_buf, uint64_t nbytes, uint64_t seed, void* stream);
+/* Diagnostic: select the long-path kernel variant (0 = default). Returns the previous value. */
+int oxh_set_kernel_variant(int variant);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OXEN_HASH_H */

@@ -1,0 +1,113 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes wrapper around the CPU oracle (oracle/xxh3_oracle.c).
+
+The oracle is a scalar C restatement of XXH3-128 (seed 0, default secret), the content hash of
+liboxen `util/hasher.rs:28-30`. It is pinned by tests/test_oracle.py against the reference's own
+known-answer digest (`repositories/data_frames/schemas.rs:131`) and against the golden vectors in
+tests/golden/ (libxxhash 0.8.2). Only tests/, `__graft_entry__.smoke()` and bench.py's
+`cpu_baseline` leg may import this module; the product path (oxen_amd) never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "liboxh_oracle.so")
+_lib = None
+
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+
+
+def build(force: bool = False) -> str:
+    """Compile the oracle with gcc (oracle/Makefile)."""
+    if force or not os.path.exists(LIB_PATH) or (
+        os.path.getmtime(LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "xxh3_oracle.c"))
+    ):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        L.oxo_xxh3_128.argtypes = [ctypes.c_void_p, ctypes.c_uint64, _u64p]
+        L.oxo_xxh3_128.restype = None
+        L.oxo_combined_hash.argtypes = [_u64p, _u64p, _u64p]
+        L.oxo_combined_hash.restype = None
+        L.oxo_xxh3_128_batch.argtypes = [ctypes.c_void_p, _u64p, _u64p, ctypes.c_uint64, _u64p, ctypes.c_int]
+        L.oxo_xxh3_128_batch.restype = None
+        L.oxo_hash_files.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_uint64, _u64p, _u64p, _i32p, ctypes.c_int]
+        L.oxo_hash_files.restype = None
+        L.oxo_chunk_digests.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, _u64p, ctypes.c_int]
+        L.oxo_chunk_digests.restype = None
+        L.oxo_format_hex.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_char_p]
+        L.oxo_format_hex.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray, t=_u64p):
+    return a.ctypes.data_as(t)
+
+
+def xxh3_128(data: bytes) -> tuple[int, int]:
+    """(low64, high64) of XXH3-128(data)."""
+    out = np.zeros(2, dtype=np.uint64)
+    buf = ctypes.create_string_buffer(bytes(data), len(data)) if len(data) else None
+    lib().oxo_xxh3_128(ctypes.cast(buf, ctypes.c_void_p) if buf is not None else None, len(data), _ptr(out))
+    return int(out[0]), int(out[1])
+
+
+def xxh3_128_int(data: bytes) -> int:
+    lo, hi = xxh3_128(data)
+    return (hi << 64) | lo
+
+
+def combined_hash(content: int, metadata: int) -> int:
+    c = np.array([content & (2**64 - 1), content >> 64], dtype=np.uint64)
+    m = np.array([metadata & (2**64 - 1), metadata >> 64], dtype=np.uint64)
+    out = np.zeros(2, dtype=np.uint64)
+    lib().oxo_combined_hash(_ptr(c), _ptr(m), _ptr(out))
+    return (int(out[1]) << 64) | int(out[0])
+
+
+def batch(arena: np.ndarray, offsets: np.ndarray, lens: np.ndarray, threads: int = 1) -> np.ndarray:
+    """Digests of arena[offsets[i] : offsets[i]+lens[i]] -> uint64 array (n, 2) = (lo, hi)."""
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint64)
+    n = len(lens)
+    out = np.zeros((n, 2), dtype=np.uint64)
+    lib().oxo_xxh3_128_batch(arena.ctypes.data, _ptr(offsets), _ptr(lens), n, _ptr(out), int(threads))
+    return out
+
+
+def hash_files(paths: list[str], threads: int = 1):
+    n = len(paths)
+    arr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
+    out = np.zeros((n, 2), dtype=np.uint64)
+    sizes = np.zeros(n, dtype=np.uint64)
+    status = np.zeros(n, dtype=np.int32)
+    lib().oxo_hash_files(arr, n, _ptr(out), _ptr(sizes), _ptr(status, _i32p), int(threads))
+    return out, sizes, status
+
+
+def chunk_digests(data: np.ndarray, chunk: int, threads: int = 1) -> np.ndarray:
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    n = (len(data) + chunk - 1) // chunk if chunk else 0
+    out = np.zeros((n, 2), dtype=np.uint64)
+    lib().oxo_chunk_digests(data.ctypes.data, len(data), chunk, _ptr(out), int(threads))
+    return out
+
+
+def format_hex(lo: int, hi: int) -> str:
+    buf = ctypes.create_string_buffer(40)
+    lib().oxo_format_hex(lo, hi, buf)
+    return buf.value.decode()

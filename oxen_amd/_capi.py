@@ -1,0 +1,125 @@
+"""ctypes binding of the C ABI in include/oxen_hash.h (oxen_amd/liboxen_hash.so).
+
+Loading never falls back to anything: if the library is missing the import of a hashing entry
+point raises, and on a host without a gfx950 device `Context()` raises `OxenError`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboxen_hash.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "oxen_hash.h")
+
+OXH_OK = 0
+OXH_ERR_INVALID = 1
+OXH_ERR_HIP = 2
+OXH_ERR_IO = 3
+OXH_ERR_NOMEM = 4
+OXH_ERR_NODEVICE = 5
+OXH_MODE_AUTO = 0
+OXH_MODE_WAVE = 1
+OXH_MODE_LANE = 2
+
+_u64 = ctypes.c_uint64
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_vp = ctypes.c_void_p
+_int = ctypes.c_int
+
+# name -> (restype, argtypes); must mirror include/oxen_hash.h exactly (tests/test_capi.py checks).
+SIGNATURES = {
+    "oxh_abi_version": (_int, []),
+    "oxh_last_error": (ctypes.c_char_p, []),
+    "oxh_device_count": (_int, [ctypes.POINTER(_int)]),
+    "oxh_ctx_create": (_int, [_int, _u64, ctypes.POINTER(_vp)]),
+    "oxh_ctx_destroy": (_int, [_vp]),
+    "oxh_ctx_stream": (_vp, [_vp]),
+    "oxh_xxh3_128_batch_device": (_int, [_vp, _vp, _vp, _u64, _vp, _int, _vp]),
+    "oxh_chunk_digests_device": (_int, [_vp, _u64, _u64, _vp, _vp]),
+    "oxh_xxh3_128_large_device": (_int, [_vp, _vp, _u64, _vp, _vp]),
+    "oxh_hash_buffers": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64p, _u64, _u64p]),
+    "oxh_hash_files": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64, _u64p, _u64p, _i32p]),
+    "oxh_combined_hash_device": (_int, [_vp, _vp, _u64, _vp, _vp]),
+    "oxh_hash_streams": (_int, [_vp, _vp, _u64p, _u64p, _u64, _u64p]),
+    "oxh_format_hex": (_int, [_u64, _u64, ctypes.c_char_p]),
+    "oxh_format_dec": (_int, [_u64, _u64, ctypes.c_char_p]),
+    "oxh_fill_splitmix": (_int, [_vp, _u64, _u64, _vp]),
+    "oxh_set_kernel_variant": (_int, [_int]),
+}
+
+_lib = None
+
+
+class OxenError(Exception):
+    """Mirror of liboxen's OxenError for this path (error/mod.rs); carries the C status code."""
+
+    def __init__(self, msg: str, code: int = OXH_ERR_INVALID):
+        super().__init__(msg)
+        self.code = code
+
+
+def header_symbols() -> list[str]:
+    """Every function the public header declares."""
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:[\w\*\s]+?)\b(oxh_\w+)\s*\(", text, flags=re.M)))
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OxenError(f"{LIB_PATH} is missing: run `python -m oxen_amd.build` (no CPU fallback exists)",
+                            OXH_ERR_NODEVICE)
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != OXH_OK:
+        msg = lib().oxh_last_error().decode(errors="replace")
+        raise OxenError(f"{what} failed (status {rc}): {msg}", rc)
+
+
+def device_count() -> int:
+    n = _int(0)
+    check(lib().oxh_device_count(ctypes.byref(n)), "oxh_device_count")
+    return n.value
+
+
+class Context:
+    """An oxh_ctx: streams + pinned staging on one device."""
+
+    def __init__(self, device: int = 0, staging_bytes: int = 0):
+        h = _vp()
+        check(lib().oxh_ctx_create(int(device), int(staging_bytes), ctypes.byref(h)), "oxh_ctx_create")
+        self.handle = h
+        self.device = device
+
+    @property
+    def stream(self) -> int:
+        return lib().oxh_ctx_stream(self.handle) or 0
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            lib().oxh_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()

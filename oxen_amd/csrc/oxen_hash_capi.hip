@@ -1,0 +1,616 @@
+// oxen_amd/csrc/oxen_hash_capi.hip -- host runtime + extern "C" boundary (include/oxen_hash.h).
+//
+// The runtime replaces the per-file hashing inside liboxen's add loop
+// (core/v_latest/add.rs:444-545 -> util/hasher.rs:56-65) with batched device work:
+//   * a context owns a compute stream, a copy stream and NSLOT pinned/device staging slots;
+//   * host-resident batches are packed into a slot at 256-B aligned offsets (file readers pread
+//     straight into pinned memory), copied H2D on the copy stream, hashed by K1 on the compute
+//     stream, and the 16-B digests come back D2H -- while the next slot is being filled;
+//   * device-resident batches go straight to the kernels.
+// There is no CPU hashing path here: every digest this library returns was computed on the GPU.
+#include <hip/hip_runtime.h>
+#include <fcntl.h>
+#include <stdint.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/oxen_hash.h"
+
+namespace oxh {
+template <bool DESC, int VARIANT>
+__global__ void xxh3_wave_kernel(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+__global__ void xxh3_lane_kernel(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t*);
+__global__ void xxh3_combined_kernel(const uint64_t*, const uint64_t*, uint64_t, uint64_t*);
+template <bool ALIGNED>
+__global__ void xxh3_blocksum_kernel(const uint8_t*, uint64_t, uint64_t*);
+template <bool ALIGNED>
+__global__ void xxh3_chain_kernel(const uint8_t*, uint64_t, const uint64_t*, uint64_t*);
+__global__ void fill_splitmix_kernel(uint64_t*, uint64_t, uint64_t);
+__global__ void fill_splitmix_tail_kernel(uint8_t*, uint64_t, uint64_t, uint64_t);
+}  // namespace oxh
+
+namespace {
+
+thread_local std::string g_err;
+std::atomic<int> g_variant{0};
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return fail(OXH_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));  \
+    } while (0)
+
+constexpr uint64_t kAlign = 256;
+constexpr int NSLOT = 3;
+inline uint64_t align_up(uint64_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
+
+int check_device(int device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(OXH_ERR_NODEVICE, "no HIP device visible");
+    if (device < 0 || device >= n) return fail(OXH_ERR_INVALID, "device index out of range");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return fail(OXH_ERR_NODEVICE, "hipGetDeviceProperties failed");
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(OXH_ERR_NODEVICE, std::string("device is ") + prop.gcnArchName + ", this library is built for gfx950");
+    return OXH_OK;
+}
+
+// ---------------------------------------------------------------- kernel launch helpers
+int launch_wave(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens, uint64_t n, uint64_t* out,
+                hipStream_t st) {
+    if (n == 0) return OXH_OK;
+    const uint64_t blocks = (n + 3) / 4;
+    if (g_variant.load() == 1)
+        hipLaunchKernelGGL((oxh::xxh3_wave_kernel<true, 1>), dim3((unsigned)blocks), dim3(256), 0, st, arena, offs, lens, n, 0, 0, out);
+    else
+        hipLaunchKernelGGL((oxh::xxh3_wave_kernel<true, 0>), dim3((unsigned)blocks), dim3(256), 0, st, arena, offs, lens, n, 0, 0, out);
+    HIP_TRY(hipGetLastError());
+    return OXH_OK;
+}
+
+int launch_lane(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens, uint64_t n, uint64_t* out,
+                hipStream_t st) {
+    if (n == 0) return OXH_OK;
+    hipLaunchKernelGGL(oxh::xxh3_lane_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, arena, offs, lens, n, out);
+    HIP_TRY(hipGetLastError());
+    return OXH_OK;
+}
+
+// ---------------------------------------------------------------- a small blocking thread pool
+class Pool {
+   public:
+    explicit Pool(int n) {
+        for (int i = 0; i < n; ++i) th_.emplace_back([this] { run(); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    int size() const { return (int)th_.size(); }
+    // Run fn(t) for t in [0, ntasks) across the pool; blocks until all are done.
+    void parallel_for(int ntasks, const std::function<void(int)>& fn) {
+        if (ntasks <= 0) return;
+        std::atomic<int> next{0}, done{0};
+        std::mutex dmu;
+        std::condition_variable dcv;
+        auto body = [&] {
+            for (;;) {
+                const int t = next.fetch_add(1);
+                if (t >= ntasks) break;
+                fn(t);
+                if (done.fetch_add(1) + 1 == ntasks) {
+                    std::lock_guard<std::mutex> g(dmu);
+                    dcv.notify_all();
+                }
+            }
+        };
+        const int nw = std::min(ntasks, size());
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            for (int i = 0; i < nw; ++i) q_.push_back(body);
+        }
+        cv_.notify_all();
+        std::unique_lock<std::mutex> lk(dmu);
+        dcv.wait(lk, [&] { return done.load() == ntasks; });
+        // the helpers may still be returning from `body`; wait until none holds a reference
+        std::unique_lock<std::mutex> g(mu_);
+        idle_cv_.wait(g, [&] { return busy_ == 0 && q_.empty(); });
+    }
+
+   private:
+    void run() {
+        for (;;) {
+            std::function<void()> job;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+                if (stop_ && q_.empty()) return;
+                job = std::move(q_.back());
+                q_.pop_back();
+                ++busy_;
+            }
+            job();
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                --busy_;
+            }
+            idle_cv_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::vector<std::function<void()>> q_;
+    std::mutex mu_;
+    std::condition_variable cv_, idle_cv_;
+    int busy_ = 0;
+    bool stop_ = false;
+};
+
+int default_threads() {
+    const char* e = getenv("OXH_NUM_THREADS");  // cf. OXEN_NUM_THREADS (util/concurrency.rs:1-45)
+    if (e && atoi(e) > 0) return atoi(e);
+    unsigned hc = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(hc ? hc : 4u, 16u));
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- context
+struct oxh_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr, copy_stream = nullptr;
+    uint64_t stage_bytes = 0, max_items = 0;
+    uint8_t* h_stage[NSLOT] = {};
+    uint8_t* d_stage[NSLOT] = {};
+    uint64_t* h_desc[NSLOT] = {};  // [offsets(max_items) | lens(max_items)]
+    uint64_t* d_desc[NSLOT] = {};
+    uint64_t* h_out[NSLOT] = {};
+    uint64_t* d_out[NSLOT] = {};
+    hipEvent_t ev_copied[NSLOT] = {}, ev_done[NSLOT] = {};
+    uint64_t* d_scratch = nullptr;
+    uint64_t scratch_bytes = 0;
+    Pool* pool = nullptr;
+    std::mutex mu;
+};
+
+namespace {
+
+int ctx_scratch(oxh_ctx* c, uint64_t bytes) {
+    if (c->scratch_bytes >= bytes) return OXH_OK;
+    if (c->d_scratch) {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(hipFree(c->d_scratch));
+        c->d_scratch = nullptr;
+        c->scratch_bytes = 0;
+    }
+    if (hipMalloc(&c->d_scratch, bytes) != hipSuccess) return fail(OXH_ERR_NOMEM, "scratch hipMalloc failed");
+    c->scratch_bytes = bytes;
+    return OXH_OK;
+}
+
+// K1L on a device buffer (block sums + chain); small buffers fall back to one K1 wave.
+int large_device(oxh_ctx* c, const uint8_t* d_buf, uint64_t len, uint64_t* d_out, hipStream_t st) {
+    const uint64_t nb = len > 0 ? (len - 1) >> 10 : 0;
+    if (nb < 1024) {
+        // one wave is faster than two launches below ~1 MiB; descriptors live in the scratch
+        int rc = ctx_scratch(c, 64);
+        if (rc) return rc;
+        uint64_t desc[2] = {0, len};
+        HIP_TRY(hipMemcpyAsync(c->d_scratch, desc, 16, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipStreamSynchronize(st));  // `desc` is a stack array
+        return launch_wave(d_buf, c->d_scratch, c->d_scratch + 1, 1, d_out, st);
+    }
+    int rc = ctx_scratch(c, nb * 64);
+    if (rc) return rc;
+    const bool aligned = (reinterpret_cast<uintptr_t>(d_buf) & 15) == 0;
+    const uint64_t nwaves = (nb + 3) / 4, blocks = (nwaves + 3) / 4;
+    if (aligned)
+        hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, d_buf, nb, c->d_scratch);
+    else
+        hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, d_buf, nb, c->d_scratch);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(oxh::xxh3_chain_kernel<true>, dim3(1), dim3(64), 0, st, d_buf, len, c->d_scratch, d_out);
+    HIP_TRY(hipGetLastError());
+    return OXH_OK;
+}
+
+// One staged batch: items [0, cnt) already in h_stage[s] at h_desc offsets; launch and queue D2H.
+int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_only) {
+    const uint64_t M = c->max_items;
+    HIP_TRY(hipMemcpyAsync(c->d_stage[s], c->h_stage[s], bytes, hipMemcpyHostToDevice, c->copy_stream));
+    HIP_TRY(hipMemcpyAsync(c->d_desc[s], c->h_desc[s], M * 16, hipMemcpyHostToDevice, c->copy_stream));
+    HIP_TRY(hipEventRecord(c->ev_copied[s], c->copy_stream));
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[s], 0));
+    int rc = any_short_only ? launch_lane(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->stream)
+                            : launch_wave(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->stream);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(c->h_out[s], c->d_out[s], cnt * 16, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipEventRecord(c->ev_done[s], c->stream));
+    return OXH_OK;
+}
+
+struct Pending {
+    bool busy = false;
+    std::vector<uint64_t> ids;  // caller indices of the staged items
+};
+
+int drain_slot(oxh_ctx* c, int s, Pending& p, uint64_t* out) {
+    if (!p.busy) return OXH_OK;
+    HIP_TRY(hipEventSynchronize(c->ev_done[s]));
+    for (size_t j = 0; j < p.ids.size(); ++j) {
+        out[2 * p.ids[j]] = c->h_out[s][2 * j];
+        out[2 * p.ids[j] + 1] = c->h_out[s][2 * j + 1];
+    }
+    p.busy = false;
+    p.ids.clear();
+    return OXH_OK;
+}
+
+// Hash one oversize host item (> a staging slot) through a temporary device buffer.
+int oversize_item(oxh_ctx* c, const uint8_t* src, uint64_t len, uint64_t* out2) {
+    uint8_t* d = nullptr;
+    if (hipMalloc(&d, len) != hipSuccess) return fail(OXH_ERR_NOMEM, "oversize hipMalloc failed");
+    int rc = OXH_OK;
+    // stream it through the pinned slot 0 in stage-sized pieces
+    for (uint64_t off = 0; off < len && rc == OXH_OK; off += c->stage_bytes) {
+        const uint64_t piece = std::min(c->stage_bytes, len - off);
+        memcpy(c->h_stage[0], src + off, piece);
+        if (hipMemcpy(d + off, c->h_stage[0], piece, hipMemcpyHostToDevice) != hipSuccess) rc = fail(OXH_ERR_HIP, "oversize H2D failed");
+    }
+    if (rc == OXH_OK) rc = large_device(c, d, len, c->d_out[0], c->stream);
+    if (rc == OXH_OK && hipMemcpyAsync(c->h_out[0], c->d_out[0], 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+        rc = fail(OXH_ERR_HIP, "oversize D2H failed");
+    if (rc == OXH_OK && hipStreamSynchronize(c->stream) != hipSuccess) rc = fail(OXH_ERR_HIP, "oversize sync failed");
+    if (rc == OXH_OK) {
+        out2[0] = c->h_out[0][0];
+        out2[1] = c->h_out[0][1];
+    }
+    (void)hipFree(d);
+    return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int oxh_abi_version(void) { return OXH_ABI_VERSION; }
+const char* oxh_last_error(void) { return g_err.c_str(); }
+
+int oxh_device_count(int* count) {
+    if (!count) return fail(OXH_ERR_INVALID, "count is NULL");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return OXH_OK;
+}
+
+int oxh_set_kernel_variant(int variant) { return g_variant.exchange(variant); }
+
+int oxh_ctx_create(int device, uint64_t staging_bytes, oxh_ctx** out) {
+    if (!out) return fail(OXH_ERR_INVALID, "out is NULL");
+    *out = nullptr;
+    int rc = check_device(device);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(device));
+    oxh_ctx* c = new oxh_ctx();
+    c->device = device;
+    c->stage_bytes = align_up(staging_bytes ? staging_bytes : (256ull << 20));
+    c->max_items = std::max<uint64_t>(1024, c->stage_bytes / 4096);
+    auto cleanup = [&](int code, const char* m) { oxh_ctx_destroy(c); return fail(code, m); };
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return cleanup(OXH_ERR_HIP, "stream");
+    if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) return cleanup(OXH_ERR_HIP, "copy stream");
+    for (int s = 0; s < NSLOT; ++s) {
+        if (hipHostMalloc(&c->h_stage[s], c->stage_bytes, hipHostMallocDefault) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "pinned staging");
+        if (hipMalloc(&c->d_stage[s], c->stage_bytes) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "device staging");
+        if (hipHostMalloc(&c->h_desc[s], c->max_items * 16, hipHostMallocDefault) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "pinned desc");
+        if (hipMalloc(&c->d_desc[s], c->max_items * 16) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "device desc");
+        if (hipHostMalloc(&c->h_out[s], c->max_items * 16, hipHostMallocDefault) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "pinned out");
+        if (hipMalloc(&c->d_out[s], c->max_items * 16) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "device out");
+        if (hipEventCreateWithFlags(&c->ev_copied[s], hipEventDisableTiming) != hipSuccess) return cleanup(OXH_ERR_HIP, "event");
+        if (hipEventCreateWithFlags(&c->ev_done[s], hipEventDisableTiming) != hipSuccess) return cleanup(OXH_ERR_HIP, "event");
+    }
+    c->pool = new Pool(default_threads());
+    *out = c;
+    return OXH_OK;
+}
+
+int oxh_ctx_destroy(oxh_ctx* c) {
+    if (!c) return OXH_OK;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+    for (int s = 0; s < NSLOT; ++s) {
+        if (c->h_stage[s]) (void)hipHostFree(c->h_stage[s]);
+        if (c->d_stage[s]) (void)hipFree(c->d_stage[s]);
+        if (c->h_desc[s]) (void)hipHostFree(c->h_desc[s]);
+        if (c->d_desc[s]) (void)hipFree(c->d_desc[s]);
+        if (c->h_out[s]) (void)hipHostFree(c->h_out[s]);
+        if (c->d_out[s]) (void)hipFree(c->d_out[s]);
+        if (c->ev_copied[s]) (void)hipEventDestroy(c->ev_copied[s]);
+        if (c->ev_done[s]) (void)hipEventDestroy(c->ev_done[s]);
+    }
+    if (c->d_scratch) (void)hipFree(c->d_scratch);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+    delete c->pool;
+    delete c;
+    return OXH_OK;
+}
+
+void* oxh_ctx_stream(oxh_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int oxh_xxh3_128_batch_device(const void* d_arena, const uint64_t* d_offsets, const uint64_t* d_lens, uint64_t n,
+                              uint64_t* d_out, int mode, void* stream) {
+    if (n == 0) return OXH_OK;
+    if (!d_arena || !d_offsets || !d_lens || !d_out) return fail(OXH_ERR_INVALID, "NULL device pointer");
+    hipStream_t st = (hipStream_t)stream;
+    const uint8_t* a = (const uint8_t*)d_arena;
+    if (mode == OXH_MODE_LANE) return launch_lane(a, d_offsets, d_lens, n, d_out, st);
+    if (mode == OXH_MODE_AUTO || mode == OXH_MODE_WAVE) return launch_wave(a, d_offsets, d_lens, n, d_out, st);
+    return fail(OXH_ERR_INVALID, "unknown mode");
+}
+
+int oxh_chunk_digests_device(const void* d_buf, uint64_t len, uint64_t chunk, uint64_t* d_out, void* stream) {
+    if (len == 0) return OXH_OK;
+    if (!d_buf || !d_out || chunk == 0) return fail(OXH_ERR_INVALID, "bad chunk arguments");
+    const uint64_t n = (len + chunk - 1) / chunk;
+    const uint64_t blocks = (n + 3) / 4;
+    if (g_variant.load() == 1)
+        hipLaunchKernelGGL((oxh::xxh3_wave_kernel<false, 1>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                           (const uint8_t*)d_buf, nullptr, nullptr, n, chunk, len, d_out);
+    else
+        hipLaunchKernelGGL((oxh::xxh3_wave_kernel<false, 0>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                           (const uint8_t*)d_buf, nullptr, nullptr, n, chunk, len, d_out);
+    HIP_TRY(hipGetLastError());
+    return OXH_OK;
+}
+
+int oxh_xxh3_128_large_device(oxh_ctx* c, const void* d_buf, uint64_t len, uint64_t* d_out, void* stream) {
+    if (!c || !d_out || (!d_buf && len)) return fail(OXH_ERR_INVALID, "bad large-buffer arguments");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    if (len == 0) {
+        // zero-length buffers still hash on the device (lane kernel, descriptors in scratch)
+        int rc = ctx_scratch(c, 64);
+        if (rc) return rc;
+        uint64_t desc[2] = {0, 0};
+        HIP_TRY(hipMemcpyAsync(c->d_scratch, desc, 16, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        return launch_lane((const uint8_t*)c->d_scratch, c->d_scratch, c->d_scratch + 1, 1, d_out, st);
+    }
+    return large_device(c, (const uint8_t*)d_buf, len, d_out, st);
+}
+
+int oxh_combined_hash_device(const uint64_t* d_content, const uint64_t* d_metadata, uint64_t n, uint64_t* d_out,
+                             void* stream) {
+    if (n == 0) return OXH_OK;
+    if (!d_content || !d_metadata || !d_out) return fail(OXH_ERR_INVALID, "NULL device pointer");
+    hipLaunchKernelGGL(oxh::xxh3_combined_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       d_content, d_metadata, n, d_out);
+    HIP_TRY(hipGetLastError());
+    return OXH_OK;
+}
+
+// Shared packer for host-resident items: item i's bytes come from `src(i)` (a pointer) or are read by
+// `reader(i, dst)` directly into the pinned slot; lens[i] is known up front.
+static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
+                           const std::function<int(uint64_t, uint8_t*)>& fill, uint64_t* out, int32_t* status,
+                           bool short_only_lane) {
+    Pending pend[NSLOT];
+    int slot = 0;
+    uint64_t i = 0;
+    std::vector<uint64_t> batch;
+    while (i < n) {
+        // gather the next batch (greedy, in order), routing oversize items individually
+        batch.clear();
+        uint64_t bytes = 0;
+        while (i < n && batch.size() < c->max_items) {
+            const uint64_t L = lens[i];
+            if (L > c->stage_bytes) {
+                if (!batch.empty()) break;
+                // oversize item: read it fully into a host buffer, then stream through slot 0
+                for (int s = 0; s < NSLOT; ++s) {
+                    int rc = drain_slot(c, s, pend[s], out);
+                    if (rc) return rc;
+                }
+                std::vector<uint8_t> tmp(L);
+                int st = fill(i, tmp.data());
+                if (status) status[i] = st;
+                if (st == OXH_OK) {
+                    int rc = oversize_item(c, tmp.data(), L, out + 2 * i);
+                    if (rc) return rc;
+                } else {
+                    out[2 * i] = out[2 * i + 1] = 0;
+                }
+                ++i;
+                continue;
+            }
+            if (align_up(bytes) + L > c->stage_bytes) break;
+            bytes = align_up(bytes) + L;
+            batch.push_back(i);
+            ++i;
+        }
+        if (batch.empty()) continue;
+        const int s = slot;
+        slot = (slot + 1) % NSLOT;
+        int rc = drain_slot(c, s, pend[s], out);
+        if (rc) return rc;
+        // lay out the slot
+        const uint64_t M = c->max_items;
+        uint64_t* hoff = c->h_desc[s];
+        uint64_t* hlen = c->h_desc[s] + M;
+        uint64_t off = 0;
+        bool all_short = true;
+        for (size_t j = 0; j < batch.size(); ++j) {
+            off = align_up(off);
+            hoff[j] = off;
+            hlen[j] = lens[batch[j]];
+            if (hlen[j] > 240) all_short = false;
+            off += hlen[j];
+        }
+        // fill it: parallel readers / copiers write straight into pinned memory
+        std::vector<int32_t> st(batch.size(), OXH_OK);
+        const int ntasks = (int)std::min<size_t>(batch.size(), (size_t)c->pool->size() * 4);
+        c->pool->parallel_for(ntasks, [&](int t) {
+            for (size_t j = (size_t)t; j < batch.size(); j += (size_t)ntasks)
+                st[j] = fill(batch[j], c->h_stage[s] + hoff[j]);
+        });
+        for (size_t j = 0; j < batch.size(); ++j) {
+            if (status) status[batch[j]] = st[j];
+            if (st[j] != OXH_OK) hlen[j] = 0;  // keep the batch alive; digest is zeroed below
+        }
+        rc = submit_slot(c, s, off, batch.size(), short_only_lane && all_short);
+        if (rc) return rc;
+        pend[s].busy = true;
+        pend[s].ids = batch;
+        if (status) {
+            // remember failures so their digests are zeroed after the drain
+            for (size_t j = 0; j < batch.size(); ++j)
+                if (st[j] != OXH_OK) pend[s].ids[j] = pend[s].ids[j];
+        }
+    }
+    for (int s = 0; s < NSLOT; ++s) {
+        int rc = drain_slot(c, s, pend[s], out);
+        if (rc) return rc;
+    }
+    if (status)
+        for (uint64_t k = 0; k < n; ++k)
+            if (status[k] != OXH_OK) out[2 * k] = out[2 * k + 1] = 0;
+    return OXH_OK;
+}
+
+int oxh_hash_buffers(oxh_ctx* c, const uint8_t* const* bufs, const uint64_t* lens, uint64_t n, uint64_t* out) {
+    if (!c || (n && (!bufs || !lens || !out))) return fail(OXH_ERR_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    return hash_host_items(c, n, lens, [&](uint64_t i, uint8_t* dst) {
+        if (lens[i]) memcpy(dst, bufs[i], lens[i]);
+        return OXH_OK;
+    }, out, nullptr, false);
+}
+
+int oxh_hash_streams(oxh_ctx* c, const uint8_t* streams, const uint64_t* offsets, const uint64_t* lens, uint64_t n,
+                     uint64_t* out) {
+    if (!c || (n && (!streams || !offsets || !lens || !out))) return fail(OXH_ERR_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    return hash_host_items(c, n, lens, [&](uint64_t i, uint8_t* dst) {
+        if (lens[i]) memcpy(dst, streams + offsets[i], lens[i]);
+        return OXH_OK;
+    }, out, nullptr, true);
+}
+
+static int read_whole(const char* path, uint8_t* dst, uint64_t len) {
+    int fd = open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return OXH_ERR_IO;
+    uint64_t got = 0;
+    while (got < len) {
+        ssize_t r = pread(fd, dst + got, len - got, (off_t)got);
+        if (r <= 0) {
+            close(fd);
+            return OXH_ERR_IO;
+        }
+        got += (uint64_t)r;
+    }
+    close(fd);
+    return OXH_OK;
+}
+
+int oxh_hash_files(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* sizes, int32_t* status) {
+    if (!c || (n && (!paths || !out))) return fail(OXH_ERR_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    // stat pass (util::fs::metadata in add.rs:716/741), parallel
+    std::vector<uint64_t> lens(n, 0);
+    std::vector<int32_t> st(n, OXH_OK);
+    const int ntasks = (int)std::min<uint64_t>(n, (uint64_t)c->pool->size() * 4);
+    c->pool->parallel_for(ntasks, [&](int t) {
+        for (uint64_t i = (uint64_t)t; i < n; i += (uint64_t)ntasks) {
+            struct stat sb;
+            if (!paths[i] || stat(paths[i], &sb) != 0 || !S_ISREG(sb.st_mode)) {
+                st[i] = OXH_ERR_IO;
+            } else {
+                lens[i] = (uint64_t)sb.st_size;
+            }
+        }
+    });
+    std::vector<int32_t> st2(n, OXH_OK);
+    int rc = hash_host_items(c, n, lens.data(), [&](uint64_t i, uint8_t* dst) {
+        if (st[i] != OXH_OK) return (int)st[i];
+        return read_whole(paths[i], dst, lens[i]);
+    }, out, st2.data(), false);
+    if (rc) return rc;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (sizes) sizes[i] = lens[i];
+        if (status) status[i] = st2[i];
+    }
+    return OXH_OK;
+}
+
+int oxh_fill_splitmix(void* d_buf, uint64_t nbytes, uint64_t seed, void* stream) {
+    if (!d_buf && nbytes) return fail(OXH_ERR_INVALID, "NULL buffer");
+    if ((reinterpret_cast<uintptr_t>(d_buf) & 7) != 0) return fail(OXH_ERR_INVALID, "buffer must be 8-byte aligned");
+    const uint64_t nwords = nbytes / 8;
+    if (nwords) {
+        const uint64_t blocks = std::min<uint64_t>((nwords + 255) / 256, 256ull * 64);
+        hipLaunchKernelGGL(oxh::fill_splitmix_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                           (uint64_t*)d_buf, nwords, seed);
+        HIP_TRY(hipGetLastError());
+    }
+    if (nbytes % 8) {
+        hipLaunchKernelGGL(oxh::fill_splitmix_tail_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream,
+                           (uint8_t*)d_buf + nwords * 8, nwords, nbytes % 8, seed);
+        HIP_TRY(hipGetLastError());
+    }
+    return OXH_OK;
+}
+
+int oxh_format_hex(uint64_t lo, uint64_t hi, char* out) {
+    if (!out) return 0;
+    unsigned __int128 v = ((unsigned __int128)hi << 64) | lo;
+    char tmp[33];
+    int n = 0;
+    do {
+        tmp[n++] = "0123456789abcdef"[(int)(v & 15)];
+        v >>= 4;
+    } while (v);
+    for (int i = 0; i < n; ++i) out[i] = tmp[n - 1 - i];
+    out[n] = 0;
+    return n;
+}
+
+int oxh_format_dec(uint64_t lo, uint64_t hi, char* out) {
+    if (!out) return 0;
+    unsigned __int128 v = ((unsigned __int128)hi << 64) | lo;
+    char tmp[40];
+    int n = 0;
+    do {
+        tmp[n++] = (char)('0' + (int)(v % 10));
+        v /= 10;
+    } while (v);
+    for (int i = 0; i < n; ++i) out[i] = tmp[n - 1 - i];
+    out[n] = 0;
+    return n;
+}
+
+}  // extern "C"

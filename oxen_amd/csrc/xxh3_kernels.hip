@@ -1,0 +1,401 @@
+// oxen_amd/csrc/xxh3_kernels.hip -- hand-written gfx950 kernels for the content-hash stage.
+//
+//   K1   xxh3_wave_kernel     one 64-lane wave per buffer; XXH3-128 long path in 4 KiB rounds.
+//   K1s  xxh3_lane_kernel     one lane per buffer (short items, parent-node streams).
+//   K1L  xxh3_blocksum_kernel + xxh3_chain_kernel: one huge buffer, block sums chip-wide, then the
+//        serial scramble chain on one wave.
+//   K2   xxh3_combined_kernel get_combined_hash (hasher.rs:67-80) on (content, metadata) pairs.
+//   util fill_splitmix_kernel synthetic, host-reproducible byte stream.
+//
+// Long-path data layout (K1): a "round" is 4 consecutive 1 KiB XXH3 blocks = 4 KiB. Lane l of the
+// wave owns row g = l/16 (block 4r+g of the round), stripe-in-quad q = (l/4)%4 and word pair
+// k = l%4. Load j (0..3) of a round reads 16 B at block_base + (4j+q)*64 + 16k, so each 16-lane row
+// reads 256 contiguous bytes per instruction (4 x 256 B = 8 full 128-B lines per wave-instruction,
+// the same line count as a flat 1 KiB load), and after the 4 loads lane l has summed stripes
+// {q, q+4, q+8, q+12} of its block for accumulators (2k, 2k+1). Two DPP row rotations (ror 4,
+// ror 8) finish the 16-stripe block sum inside each row; permlane16/32 swaps broadcast the four
+// block sums to every row, and every lane then runs the 4-step scramble chain for its 2 accumulators.
+// All of it is 32-bit VALU integer work -- no LDS traffic and no MFMA.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "xxh3_device.hpp"
+
+namespace oxh {
+
+static __constant__ uint64_t kInitW[8] = {acc_init(0), acc_init(1), acc_init(2), acc_init(3),
+                                          acc_init(4), acc_init(5), acc_init(6), acc_init(7)};
+// last-stripe keys: secret + 192 - 64 - 7 = 121
+static __constant__ uint64_t kLastW[8] = {S64(121), S64(129), S64(137), S64(145),
+                                          S64(153), S64(161), S64(169), S64(177)};
+// merge keys: low64 at secret + 11, high64 at secret + 192 - 64 - 11 = 117
+static __constant__ uint64_t kMrgLo[8] = {S64(11), S64(19), S64(27), S64(35),
+                                          S64(43), S64(51), S64(59), S64(67)};
+static __constant__ uint64_t kMrgHi[8] = {S64(117), S64(125), S64(133), S64(141),
+                                          S64(149), S64(157), S64(165), S64(173)};
+
+constexpr int DPP_ROW_ROR4 = 0x124;
+constexpr int DPP_ROW_ROR8 = 0x128;
+constexpr int DPP_QUAD_XOR1 = 0xB1;
+constexpr int DPP_QUAD_XOR2 = 0x4E;
+
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t x) {
+    const uint32_t lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)x, CTRL, 0xf, 0xf, false);
+    const uint32_t hi = __builtin_amdgcn_update_dpp(0u, (uint32_t)(x >> 32), CTRL, 0xf, 0xf, false);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Broadcast the value held by each 16-lane row r (x_r) so that every lane gets x_0..x_3.
+// VARIANT 0: v_permlane16_swap + v_permlane32_swap (gfx950 VALU cross-row moves).
+// VARIANT 1: ds_bpermute through __shfl (LDS crossbar) -- reference formulation for A/B.
+template <int VARIANT>
+__device__ __forceinline__ void bcast_rows32(uint32_t x, uint32_t& b0, uint32_t& b1, uint32_t& b2,
+                                             uint32_t& b3, int lane) {
+    if constexpr (VARIANT == 0) {
+        // permlane16_swap(a, b): swaps odd rows of a with even rows of b.
+        //   with a = b = x:  r[0] = (x0, x0, x2, x2), r[1] = (x1, x1, x3, x3)
+        // permlane32_swap(a, b): swaps the upper half of a with the lower half of b.
+        //   with a = b = y:  r[0] = (y_lo, y_lo),    r[1] = (y_hi, y_hi)
+        const auto p16 = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        const auto pa = __builtin_amdgcn_permlane32_swap(p16[0], p16[0], false, false);
+        const auto pb = __builtin_amdgcn_permlane32_swap(p16[1], p16[1], false, false);
+        b0 = pa[0];
+        b2 = pa[1];
+        b1 = pb[0];
+        b3 = pb[1];
+    } else {
+        const int c = lane & 15;
+        b0 = __shfl((int)x, c, 64);
+        b1 = __shfl((int)x, 16 + c, 64);
+        b2 = __shfl((int)x, 32 + c, 64);
+        b3 = __shfl((int)x, 48 + c, 64);
+    }
+}
+
+template <int VARIANT>
+__device__ __forceinline__ void bcast_rows64(uint64_t x, uint64_t t[4], int lane) {
+    uint32_t l0, l1, l2, l3, h0, h1, h2, h3;
+    bcast_rows32<VARIANT>((uint32_t)x, l0, l1, l2, l3, lane);
+    bcast_rows32<VARIANT>((uint32_t)(x >> 32), h0, h1, h2, h3, lane);
+    t[0] = ((uint64_t)h0 << 32) | l0;
+    t[1] = ((uint64_t)h1 << 32) | l1;
+    t[2] = ((uint64_t)h2 << 32) | l2;
+    t[3] = ((uint64_t)h3 << 32) | l3;
+}
+
+template <bool ALIGNED>
+__device__ __forceinline__ uint4 load16(const uint8_t* p) {
+    if constexpr (ALIGNED) {
+        return *reinterpret_cast<const uint4*>(p);
+    } else {
+        uint4 v;
+        __builtin_memcpy(&v, p, 16);
+        return v;
+    }
+}
+
+// One 16-byte piece of one stripe: words (2k, 2k+1) with keys (key0, key1).
+__device__ __forceinline__ void accum16(const uint4 d, uint64_t key0, uint64_t key1, uint64_t& s0,
+                                        uint64_t& s1) {
+    const uint64_t w0 = ((uint64_t)d.y << 32) | d.x;
+    const uint64_t w1 = ((uint64_t)d.w << 32) | d.z;
+    const uint64_t k0 = w0 ^ key0;
+    const uint64_t k1 = w1 ^ key1;
+    s0 += mul32x32(k0) + w1;  // acc[2k]   += lo*hi of its keyed word, plus word 2k+1 (the i^1 swap)
+    s1 += mul32x32(k1) + w0;  // acc[2k+1] += lo*hi of its keyed word, plus word 2k
+}
+
+// Fold a round: in-row stripe reduction, cross-row broadcast, 4 chain steps.
+// nfull: how many of the 4 blocks are full (scrambled); block nfull (if < 4) is the partial one.
+template <int VARIANT>
+__device__ __forceinline__ void fold_round(uint64_t s0, uint64_t s1, uint64_t& a0, uint64_t& a1,
+                                           uint64_t sk0, uint64_t sk1, int nfull, int lane) {
+    s0 += dpp64<DPP_ROW_ROR4>(s0);
+    s1 += dpp64<DPP_ROW_ROR4>(s1);
+    s0 += dpp64<DPP_ROW_ROR8>(s0);
+    s1 += dpp64<DPP_ROW_ROR8>(s1);
+    uint64_t t0[4], t1[4];
+    bcast_rows64<VARIANT>(s0, t0, lane);
+    bcast_rows64<VARIANT>(s1, t1, lane);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        if (g < nfull) {
+            a0 = scramble1(a0 + t0[g], sk0);
+            a1 = scramble1(a1 + t1[g], sk1);
+        } else if (g == nfull) {
+            a0 += t0[g];
+            a1 += t1[g];
+        }
+    }
+}
+
+// The long path (len > 240) for one buffer, executed by one full wave. Writes out[0..1] from lane 0.
+template <bool ALIGNED, int VARIANT>
+__device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_t len,
+                                          uint64_t* __restrict__ out, int lane) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, k = lane & 3;
+    uint64_t key0[4], key1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        key0[j] = kSecW[4 * j + q + 2 * k];
+        key1[j] = kSecW[4 * j + q + 2 * k + 1];
+    }
+    const uint64_t sk0 = kSecW[16 + 2 * k], sk1 = kSecW[16 + 2 * k + 1];
+    uint64_t a0 = kInitW[2 * k], a1 = kInitW[2 * k + 1];
+
+    const uint64_t nb = (len - 1) >> 10;  // blocks followed by a scramble
+    const uint64_t nr = nb >> 2;          // full rounds (4 scrambled blocks each)
+    const uint8_t* lp = p + (uint64_t)g * 1024 + (uint64_t)q * 64 + (uint64_t)k * 16;
+
+    if (nr > 0) {
+        // software pipeline: round r+1's four loads are in flight while round r is folded
+        uint4 cur[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cur[j] = load16<ALIGNED>(lp + j * 256);
+        for (uint64_t r = 0; r < nr; ++r) {
+            const uint64_t rn = (r + 1 < nr) ? r + 1 : r;
+            uint4 nxt[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) nxt[j] = load16<ALIGNED>(lp + rn * 4096 + j * 256);
+            uint64_t s0 = 0, s1 = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) accum16(cur[j], key0[j], key1[j], s0, s1);
+            fold_round<VARIANT>(s0, s1, a0, a1, sk0, sk1, 4, lane);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+        }
+    }
+    // final round: (nb - 4nr) full blocks, then the partial block with `ns` stripes
+    {
+        const uint64_t b = nr * 4 + g;
+        const uint64_t ns = ((len - 1) - (nb << 10)) >> 6;
+        uint64_t s0 = 0, s1 = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t s = 4 * j + q;
+            if (b < nb || (b == nb && s < ns)) {
+                const uint4 d = load16<ALIGNED>(lp + nr * 4096 + j * 256);
+                accum16(d, key0[j], key1[j], s0, s1);
+            }
+        }
+        fold_round<VARIANT>(s0, s1, a0, a1, sk0, sk1, (int)(nb - nr * 4), lane);
+    }
+    // last stripe, at len - 64, with the secret shifted to offset 121
+    {
+        const uint8_t* ls = p + len - 64 + 16 * k;
+        const uint64_t w0 = ld64u(ls), w1 = ld64u(ls + 8);
+        const uint64_t k0 = w0 ^ kLastW[2 * k], k1 = w1 ^ kLastW[2 * k + 1];
+        a0 += mul32x32(k0) + w1;
+        a1 += mul32x32(k1) + w0;
+    }
+    // merge: lane k contributes mix2Accs for accumulator pair k; sum over the quad
+    uint64_t mlo = mul_fold64(a0 ^ kMrgLo[2 * k], a1 ^ kMrgLo[2 * k + 1]);
+    uint64_t mhi = mul_fold64(a0 ^ kMrgHi[2 * k], a1 ^ kMrgHi[2 * k + 1]);
+    mlo += dpp64<DPP_QUAD_XOR1>(mlo);
+    mhi += dpp64<DPP_QUAD_XOR1>(mhi);
+    mlo += dpp64<DPP_QUAD_XOR2>(mlo);
+    mhi += dpp64<DPP_QUAD_XOR2>(mhi);
+    if (lane == 0) {
+        out[0] = avalanche_xxh3(len * P64_1 + mlo);
+        out[1] = avalanche_xxh3(~(len * P64_2) + mhi);
+    }
+}
+
+// K1: one wave per item. DESC = descriptor table (offsets/lens); otherwise fixed-size chunks.
+template <bool DESC, int VARIANT>
+__global__ __launch_bounds__(256) void xxh3_wave_kernel(const uint8_t* __restrict__ arena,
+                                                        const uint64_t* __restrict__ offsets,
+                                                        const uint64_t* __restrict__ lens, uint64_t n,
+                                                        uint64_t chunk, uint64_t total,
+                                                        uint64_t* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t item = (uint64_t)blockIdx.x * 4 + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (item >= n) return;
+    uint64_t off, len;
+    if constexpr (DESC) {
+        off = offsets[item];
+        len = lens[item];
+    } else {
+        off = item * chunk;
+        len = (total - off < chunk) ? total - off : chunk;
+    }
+    const uint8_t* p = arena + off;
+    uint64_t* o = out + 2 * item;
+    if (len <= 240) {
+        if (lane == 0) {
+            const U128 h = xxh3_lane_short(p, len);
+            o[0] = h.lo;
+            o[1] = h.hi;
+        }
+        return;
+    }
+    if ((reinterpret_cast<uintptr_t>(p) & 15) == 0)
+        wave_long<true, VARIANT>(p, len, o, lane);
+    else
+        wave_long<false, VARIANT>(p, len, o, lane);
+}
+
+// K1s: one lane per item (any length; intended for short items).
+__global__ __launch_bounds__(256) void xxh3_lane_kernel(const uint8_t* __restrict__ arena,
+                                                        const uint64_t* __restrict__ offsets,
+                                                        const uint64_t* __restrict__ lens, uint64_t n,
+                                                        uint64_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const U128 h = xxh3_lane_any(arena + offsets[i], lens[i]);
+    out[2 * i] = h.lo;
+    out[2 * i + 1] = h.hi;
+}
+
+// K2 helper: combined = XXH3-128(content LE16 || metadata LE16) -- the 17..128 path at len 32.
+__global__ __launch_bounds__(256) void xxh3_combined_kernel(const uint64_t* __restrict__ content,
+                                                            const uint64_t* __restrict__ meta, uint64_t n,
+                                                            uint64_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t c0 = content[2 * i], c1 = content[2 * i + 1];
+    const uint64_t m0 = meta[2 * i], m1 = meta[2 * i + 1];
+    // mix32B(acc, in, in + 16, secret): a = (c0, c1), b = (m0, m1)
+    uint64_t lo = 32 * P64_1, hi = 0;
+    lo += mul_fold64(c0 ^ S64(0), c1 ^ S64(8));
+    lo ^= m0 + m1;
+    hi += mul_fold64(m0 ^ S64(16), m1 ^ S64(24));
+    hi ^= c0 + c1;
+    const U128 h = finish_mid(lo, hi, 32);
+    out[2 * i] = h.lo;
+    out[2 * i + 1] = h.hi;
+}
+
+// K1L phase 1: block sums. Wave w folds blocks [4w, 4w+4) of the buffer (only blocks < nb, i.e.
+// those followed by a scramble) and writes each block's 8 accumulator sums (64 B) to `sums`.
+template <bool ALIGNED>
+__global__ __launch_bounds__(256) void xxh3_blocksum_kernel(const uint8_t* __restrict__ p, uint64_t nb,
+                                                            uint64_t* __restrict__ sums) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t w = (uint64_t)blockIdx.x * 4 + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nwaves = (nb + 3) >> 2;
+    if (w >= nwaves) return;
+    const int g = lane >> 4, q = (lane >> 2) & 3, k = lane & 3;
+    const uint64_t b = 4 * w + g;
+    uint64_t s0 = 0, s1 = 0;
+    if (b < nb) {
+        const uint8_t* lp = p + b * 1024 + (uint64_t)q * 64 + (uint64_t)k * 16;
+        uint4 d[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[j] = load16<ALIGNED>(lp + j * 256);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            accum16(d[j], kSecW[4 * j + q + 2 * k], kSecW[4 * j + q + 2 * k + 1], s0, s1);
+    }
+    s0 += dpp64<DPP_ROW_ROR4>(s0);
+    s1 += dpp64<DPP_ROW_ROR4>(s1);
+    s0 += dpp64<DPP_ROW_ROR8>(s0);
+    s1 += dpp64<DPP_ROW_ROR8>(s1);
+    if (b < nb && q == 0) {
+        // block b's sums: 8 u64, lane k stores (2k, 2k+1)
+        uint64_t* dst = sums + b * 8 + 2 * k;
+        dst[0] = s0;
+        dst[1] = s1;
+    }
+}
+
+// K1L phase 2: the serial chain over nb block sums on one wave, then the tail and the merge.
+// Lanes 0..7 each own one accumulator; the block sums stream in GROUP steps at a time, with the
+// next group's loads in flight while the current group is chained.
+template <bool ALIGNED>
+__global__ __launch_bounds__(64) void xxh3_chain_kernel(const uint8_t* __restrict__ p, uint64_t len,
+                                                        const uint64_t* __restrict__ sums,
+                                                        uint64_t* __restrict__ out) {
+    constexpr int GROUP = 16;
+    const int lane = threadIdx.x;
+    const int i = lane & 7;
+    const uint64_t nb = (len - 1) >> 10;
+    uint64_t acc = kInitW[i];
+    const uint64_t sk = kSecW[16 + i];
+    uint64_t b = 0;
+    if (nb >= GROUP) {
+        uint64_t cur[GROUP];
+#pragma unroll
+        for (int t = 0; t < GROUP; ++t) cur[t] = sums[(uint64_t)t * 8 + i];
+        const uint64_t ngroups = nb / GROUP;
+        for (uint64_t gi = 0; gi < ngroups; ++gi) {
+            const uint64_t gn = (gi + 1 < ngroups) ? gi + 1 : gi;
+            uint64_t nxt[GROUP];
+#pragma unroll
+            for (int t = 0; t < GROUP; ++t) nxt[t] = sums[(gn * GROUP + t) * 8 + i];
+#pragma unroll
+            for (int t = 0; t < GROUP; ++t) acc = scramble1(acc + cur[t], sk);
+#pragma unroll
+            for (int t = 0; t < GROUP; ++t) cur[t] = nxt[t];
+        }
+        b = ngroups * GROUP;
+    }
+    for (; b < nb; ++b) acc = scramble1(acc + sums[b * 8 + i], sk);
+    // partial block stripes + last stripe: lane i owns accumulator i here (scalar per lane)
+    const uint64_t ns = ((len - 1) - (nb << 10)) >> 6;
+    const uint8_t* pb = p + (nb << 10);
+    for (uint64_t s = 0; s < ns; ++s) {
+        const uint64_t v = ld64u(pb + s * 64 + 8 * i);
+        const uint64_t vs = ld64u(pb + s * 64 + 8 * (i ^ 1));
+        acc += mul32x32(v ^ kSecW[s + i]) + vs;
+    }
+    {
+        const uint8_t* ls = p + len - 64;
+        const uint64_t v = ld64u(ls + 8 * i);
+        const uint64_t vs = ld64u(ls + 8 * (i ^ 1));
+        acc += mul32x32(v ^ kLastW[i]) + vs;
+    }
+    // merge: pairs (2m, 2m+1) live in lanes (2m, 2m+1)
+    const uint64_t partner = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)acc, 1, 64)) |
+                             ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(acc >> 32), 1, 64) << 32);
+    uint64_t mlo = 0, mhi = 0;
+    if ((i & 1) == 0) {
+        mlo = mul_fold64(acc ^ kMrgLo[i], partner ^ kMrgLo[i + 1]);
+        mhi = mul_fold64(acc ^ kMrgHi[i], partner ^ kMrgHi[i + 1]);
+    }
+    // sum lanes 0,2,4,6
+#pragma unroll
+    for (int off = 1; off < 8; off <<= 1) {
+        const uint64_t ol = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)mlo, off, 64)) |
+                            ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(mlo >> 32), off, 64) << 32);
+        const uint64_t oh = ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)mhi, off, 64)) |
+                            ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(mhi >> 32), off, 64) << 32);
+        mlo += ol;
+        mhi += oh;
+    }
+    if (lane == 0) {
+        out[0] = avalanche_xxh3(len * P64_1 + mlo);
+        out[1] = avalanche_xxh3(~(len * P64_2) + mhi);
+    }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void fill_splitmix_kernel(uint64_t* __restrict__ dst, uint64_t nwords,
+                                                            uint64_t seed) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += stride)
+        dst[w] = splitmix64(seed + (w + 1) * 0x9E3779B97F4A7C15ULL);
+}
+
+__global__ void fill_splitmix_tail_kernel(uint8_t* __restrict__ dst, uint64_t word, uint64_t nbytes,
+                                          uint64_t seed) {
+    const uint64_t v = splitmix64(seed + (word + 1) * 0x9E3779B97F4A7C15ULL);
+    for (uint64_t j = 0; j < nbytes; ++j) dst[j] = (uint8_t)(v >> (8 * j));
+}
+
+// explicit instantiations used by the host runtime
+template __global__ void xxh3_wave_kernel<true, 0>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<true, 1>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<false, 0>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<false, 1>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_blocksum_kernel<true>(const uint8_t*, uint64_t, uint64_t*);
+template __global__ void xxh3_blocksum_kernel<false>(const uint8_t*, uint64_t, uint64_t*);
+template __global__ void xxh3_chain_kernel<true>(const uint8_t*, uint64_t, const uint64_t*, uint64_t*);
+
+}  // namespace oxh

@@ -1,0 +1,127 @@
+"""Device-resident entry points over torch-allocated HBM buffers.
+
+PyTorch is plumbing here (device memory, the current HIP stream, torch.distributed); the hashing is
+the C ABI (include/oxen_hash.h). Digest tables are int64 tensors of shape (n, 2) holding the raw
+u64 words (lo, hi); `to_u128_list` turns them into Python ints.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _capi
+from .workloads import packed_layout
+
+
+def _stream(stream) -> int:
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream
+    return int(getattr(stream, "cuda_stream", stream))
+
+
+def _require_cuda(*ts: torch.Tensor) -> None:
+    for t in ts:
+        if not t.is_cuda:
+            raise _capi.OxenError("device entry points take device-resident tensors", _capi.OXH_ERR_INVALID)
+
+
+def xxh3_128_batch_device(arena: torch.Tensor, offsets: torch.Tensor, lens: torch.Tensor,
+                          out: Optional[torch.Tensor] = None, mode: int = _capi.OXH_MODE_AUTO,
+                          stream=None) -> torch.Tensor:
+    """K1/K1s over arena[offsets[i] : offsets[i] + lens[i]] (all on the device)."""
+    _require_cuda(arena, offsets, lens)
+    n = lens.numel()
+    if offsets.numel() != n or offsets.element_size() != 8 or lens.element_size() != 8:
+        raise _capi.OxenError("offsets/lens must be 64-bit and the same length", _capi.OXH_ERR_INVALID)
+    if out is None:
+        out = torch.empty((n, 2), dtype=torch.int64, device=arena.device)
+    _capi.check(_capi.lib().oxh_xxh3_128_batch_device(arena.data_ptr(), offsets.data_ptr(), lens.data_ptr(), n,
+                                                      out.data_ptr(), int(mode), _stream(stream)),
+                "oxh_xxh3_128_batch_device")
+    return out
+
+
+def chunk_digests_device(buf: torch.Tensor, chunk: int, nbytes: Optional[int] = None,
+                         out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+    _require_cuda(buf)
+    nbytes = buf.numel() * buf.element_size() if nbytes is None else nbytes
+    n = (nbytes + chunk - 1) // chunk
+    if out is None:
+        out = torch.empty((n, 2), dtype=torch.int64, device=buf.device)
+    _capi.check(_capi.lib().oxh_chunk_digests_device(buf.data_ptr(), nbytes, chunk, out.data_ptr(), _stream(stream)),
+                "oxh_chunk_digests_device")
+    return out
+
+
+def large_digest_device(ctx: _capi.Context, buf: torch.Tensor, nbytes: Optional[int] = None,
+                        out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+    _require_cuda(buf)
+    nbytes = buf.numel() * buf.element_size() if nbytes is None else nbytes
+    if out is None:
+        out = torch.empty(2, dtype=torch.int64, device=buf.device)
+    _capi.check(_capi.lib().oxh_xxh3_128_large_device(ctx.handle, buf.data_ptr(), nbytes, out.data_ptr(),
+                                                      _stream(stream)), "oxh_xxh3_128_large_device")
+    return out
+
+
+def combined_hash_device(content: torch.Tensor, metadata: torch.Tensor, out: Optional[torch.Tensor] = None,
+                         stream=None) -> torch.Tensor:
+    _require_cuda(content, metadata)
+    n = content.shape[0]
+    if out is None:
+        out = torch.empty((n, 2), dtype=torch.int64, device=content.device)
+    _capi.check(_capi.lib().oxh_combined_hash_device(content.data_ptr(), metadata.data_ptr(), n, out.data_ptr(),
+                                                     _stream(stream)), "oxh_combined_hash_device")
+    return out
+
+
+def fill_splitmix(buf: torch.Tensor, seed: int, nbytes: Optional[int] = None, stream=None) -> None:
+    _require_cuda(buf)
+    nbytes = buf.numel() * buf.element_size() if nbytes is None else nbytes
+    _capi.check(_capi.lib().oxh_fill_splitmix(buf.data_ptr(), nbytes, int(seed), _stream(stream)), "oxh_fill_splitmix")
+
+
+def to_numpy_u64(t: torch.Tensor) -> np.ndarray:
+    return t.detach().cpu().numpy().view(np.uint64)
+
+
+def to_u128_list(t: torch.Tensor) -> list[int]:
+    a = to_numpy_u64(t).reshape(-1, 2)
+    return [(int(hi) << 64) | int(lo) for lo, hi in a]
+
+
+@dataclass
+class DeviceArena:
+    """A packed, device-resident batch of synthetic buffers (one HBM allocation + descriptors)."""
+
+    arena: torch.Tensor
+    offsets: torch.Tensor
+    lens: torch.Tensor
+    offsets_host: np.ndarray
+    lens_host: np.ndarray
+    seed: int
+
+    @property
+    def n(self) -> int:
+        return len(self.lens_host)
+
+    @property
+    def payload_bytes(self) -> int:
+        return int(self.lens_host.sum())
+
+    @classmethod
+    def splitmix(cls, lens, seed: int = 0, device="cuda", align: int = 256) -> "DeviceArena":
+        lens_h = np.asarray(lens, dtype=np.uint64)
+        offs_h, total = packed_layout(lens_h, align)
+        alloc = max(8, (total + 7) // 8 * 8)
+        arena = torch.empty(alloc, dtype=torch.uint8, device=device)
+        fill_splitmix(arena, seed, alloc)
+        offs = torch.from_numpy(offs_h.view(np.int64)).to(device)
+        ln = torch.from_numpy(lens_h.view(np.int64)).to(device)
+        return cls(arena, offs, ln, offs_h, lens_h, seed)
+
+    def hash(self, out: Optional[torch.Tensor] = None, mode: int = _capi.OXH_MODE_AUTO, stream=None) -> torch.Tensor:
+        return xxh3_128_batch_device(self.arena, self.offsets, self.lens, out, mode, stream)

@@ -1,0 +1,231 @@
+"""Host-side mirror of liboxen `util::hasher` (crates/liboxen/src/util/hasher.rs) over the GPU C ABI.
+
+Same function names, argument meaning and error behaviour as the Rust module; every digest is
+computed by the HIP kernels in oxen_amd/csrc through include/oxen_hash.h -- there is no CPU
+hashing fallback (a missing library or device raises `OxenError`). On top of the per-item
+functions, `hash_buffers_128bit` / `hash_files_128bit` expose the batched form the add loop would
+call once per batch of files (core/v_latest/add.rs:422-444).
+
+u128 digests are Python ints: ``(hi << 64) | lo``, exactly the Rust `u128` / `MerkleHash` value.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import threading
+import time
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+
+from . import _capi
+from ._capi import OxenError
+
+_ctx: Optional[_capi.Context] = None
+_ctx_lock = threading.Lock()
+
+
+def default_context() -> _capi.Context:
+    """Process-wide context on device $OXH_DEVICE (default 0), created on first use."""
+    global _ctx
+    with _ctx_lock:
+        if _ctx is None:
+            _ctx = _capi.Context(int(os.environ.get("OXH_DEVICE", "0")))
+        return _ctx
+
+
+def _to_u128(lo: int, hi: int) -> int:
+    return (int(hi) << 64) | int(lo)
+
+
+def format_hex(value: int) -> str:
+    """`format!("{:x}", u128)` -- lowercase, not zero-padded (merkle_hash.rs:73-77)."""
+    return format(value, "x")
+
+
+# ---------------------------------------------------------------------------- batch entry points
+def hash_buffers_128bit(buffers: Sequence[bytes], ctx: Optional[_capi.Context] = None) -> list[int]:
+    """`hash_buffer_128bit` over many host buffers in one batched GPU pass."""
+    ctx = ctx or default_context()
+    n = len(buffers)
+    if n == 0:
+        return []
+    keep = [bytes(b) for b in buffers]
+    ptrs = (ctypes.c_char_p * n)(*keep)
+    lens = np.array([len(b) for b in keep], dtype=np.uint64)
+    out = np.zeros((n, 2), dtype=np.uint64)
+    _capi.check(_capi.lib().oxh_hash_buffers(ctx.handle, ptrs, lens.ctypes.data_as(_capi._u64p), n,
+                                             out.ctypes.data_as(_capi._u64p)), "oxh_hash_buffers")
+    return [_to_u128(lo, hi) for lo, hi in out]
+
+
+def hash_streams_128bit(streams: Sequence[bytes], ctx: Optional[_capi.Context] = None) -> list[int]:
+    """K2: XXH3-128 of caller-serialised parent-node byte streams (one lane per short stream)."""
+    ctx = ctx or default_context()
+    n = len(streams)
+    if n == 0:
+        return []
+    lens = np.array([len(s) for s in streams], dtype=np.uint64)
+    offs = np.zeros(n, dtype=np.uint64)
+    if n > 1:
+        offs[1:] = np.cumsum(lens[:-1])
+    arena = np.frombuffer(b"".join(streams) or b"\0", dtype=np.uint8)
+    out = np.zeros((n, 2), dtype=np.uint64)
+    _capi.check(_capi.lib().oxh_hash_streams(ctx.handle, arena.ctypes.data, offs.ctypes.data_as(_capi._u64p),
+                                             lens.ctypes.data_as(_capi._u64p), n,
+                                             out.ctypes.data_as(_capi._u64p)), "oxh_hash_streams")
+    return [_to_u128(lo, hi) for lo, hi in out]
+
+
+def hash_files_128bit(paths: Sequence[str], ctx: Optional[_capi.Context] = None):
+    """`get_hash_given_metadata` over many files: returns (digests, sizes, status).
+
+    digests[i] is None where status[i] != 0 (the add loop logs and skips such files,
+    add.rs:533-544); sizes are the stat sizes used for the read.
+    """
+    ctx = ctx or default_context()
+    n = len(paths)
+    if n == 0:
+        return [], [], []
+    arr = (ctypes.c_char_p * n)(*[os.fsencode(str(p)) for p in paths])
+    out = np.zeros((n, 2), dtype=np.uint64)
+    sizes = np.zeros(n, dtype=np.uint64)
+    status = np.zeros(n, dtype=np.int32)
+    _capi.check(_capi.lib().oxh_hash_files(ctx.handle, arr, n, out.ctypes.data_as(_capi._u64p),
+                                           sizes.ctypes.data_as(_capi._u64p),
+                                           status.ctypes.data_as(_capi._i32p)), "oxh_hash_files")
+    digests = [(_to_u128(lo, hi) if st == 0 else None) for (lo, hi), st in zip(out, status)]
+    return digests, [int(s) for s in sizes], [int(s) for s in status]
+
+
+# ---------------------------------------------------------------------------- hasher.rs mirror
+def hash_buffer_128bit(buffer: bytes) -> int:
+    """hasher.rs:28-30."""
+    return hash_buffers_128bit([buffer])[0]
+
+
+def hash_buffer(buffer: bytes) -> str:
+    """hasher.rs:11-14: unpadded lowercase hex of the XXH3-128."""
+    return format_hex(hash_buffer_128bit(buffer))
+
+
+def hash_str(buffer: str) -> str:
+    """hasher.rs:16-19."""
+    return hash_buffer(buffer.encode("utf-8"))
+
+
+def _hash_one_file(path) -> int:
+    digests, _, status = hash_files_128bit([path])
+    if status[0] != 0:
+        if not os.path.exists(path):
+            raise OxenError(f"util::hasher::hash_file_contents Could not open file {str(path)!r}", _capi.OXH_ERR_IO)
+        raise OxenError("Could not read file for hashing", _capi.OXH_ERR_IO)
+    return digests[0]
+
+
+def get_hash_given_metadata(path, metadata: os.stat_result) -> int:
+    """hasher.rs:56-65. Both size branches (one-shot < 1e9 B, streamed otherwise) give the same
+    XXH3-128; here both go through the batched file path (K1 or, for files larger than a staging
+    slot, K1L)."""
+    del metadata  # the size decision only changes how the reference reads the file
+    return _hash_one_file(path)
+
+
+def u128_hash_file_contents(path) -> int:
+    """hasher.rs:102-112 (stats the file itself; a missing file is an error)."""
+    if not os.path.exists(path):
+        raise OxenError(f"Could not get metadata for {str(path)!r}", _capi.OXH_ERR_IO)
+    return _hash_one_file(path)
+
+
+def hash_file_contents(path) -> str:
+    """hasher.rs:114-124."""
+    return format_hex(u128_hash_file_contents(path))
+
+
+def hash_file_contents_with_retry(path, total_retries: int = 5, sleep=time.sleep) -> str:
+    """hasher.rs:32-54: exponential backoff (2, 4, 8 ... s), give up after `total_retries` retries."""
+    timeout, retries = 1, 0
+    while True:
+        try:
+            return hash_file_contents(path)
+        except OxenError:
+            retries += 1
+            timeout *= 2
+            sleep(timeout)
+            if retries > total_retries:
+                raise
+
+
+def metadata_json(oxen_metadata) -> str:
+    """serde_json::to_string of the (untagged) GenericMetadata, or "null" for None.
+
+    Dicts are serialised compactly in insertion order (= Rust struct field order); non-ASCII is
+    written as UTF-8 like serde_json."""
+    if hasattr(oxen_metadata, "to_json"):
+        return oxen_metadata.to_json()
+    return json.dumps(oxen_metadata, separators=(",", ":"), ensure_ascii=False)
+
+
+def get_metadata_hash(oxen_metadata) -> int:
+    """hasher.rs:95-100: XXH3-128 of serde_json(Option<GenericMetadata>) ("null" when None)."""
+    return hash_streams_128bit([metadata_json(oxen_metadata).encode("utf-8")])[0]
+
+
+def maybe_get_metadata_hash(oxen_metadata) -> Optional[int]:
+    """hasher.rs:82-93."""
+    if oxen_metadata is None:
+        return None
+    return get_metadata_hash(oxen_metadata)
+
+
+def get_combined_hash(oxen_metadata_hash: Optional[int], content_hash: int) -> int:
+    """hasher.rs:67-80: XXH3-128(content.to_le_bytes() || metadata.to_le_bytes()), or the content
+    hash unchanged when there is no metadata hash."""
+    if oxen_metadata_hash is None:
+        return content_hash
+    stream = int(content_hash).to_bytes(16, "little") + int(oxen_metadata_hash).to_bytes(16, "little")
+    return hash_streams_128bit([stream])[0]
+
+
+class HashingReader:
+    """hasher.rs:183-209: wraps a reader, feeds every byte read into the hash.
+
+    XXH3's streaming form equals its one-shot form, so the bytes are kept and hashed on the GPU when
+    `digest128()` is asked for."""
+
+    def __init__(self, inner):
+        self.inner = inner
+        self._buf = bytearray()
+
+    def read(self, n: int = -1) -> bytes:
+        b = self.inner.read(n)
+        if b:
+            self._buf += b
+        return b
+
+    def digest128(self) -> int:
+        return hash_buffer_128bit(bytes(self._buf))
+
+
+class HashingWriter:
+    """hasher.rs:214-244: wraps a writer, feeds every byte successfully written into the hash."""
+
+    def __init__(self, inner):
+        self.inner = inner
+        self._buf = bytearray()
+
+    def write(self, b: bytes) -> int:
+        n = self.inner.write(b)
+        if n is None:
+            n = len(b)
+        if n > 0:
+            self._buf += bytes(b[:n])
+        return n
+
+    def flush(self) -> None:
+        self.inner.flush()
+
+    def digest128(self) -> int:
+        return hash_buffer_128bit(bytes(self._buf))

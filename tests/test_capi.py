@@ -1,0 +1,60 @@
+"""The C-ABI library builds, loads and exports exactly what include/oxen_hash.h declares.
+
+No compute calls here: on a host without a GPU the library must refuse (no CPU fallback).
+"""
+import ctypes
+import subprocess
+
+import pytest
+
+from oxen_amd import _capi
+
+
+def test_header_declares_the_bound_symbols(built_lib):
+    declared = _capi.header_symbols()
+    assert declared == sorted(_capi.SIGNATURES), (set(declared) ^ set(_capi.SIGNATURES))
+
+
+def test_library_exports_every_declared_symbol(built_lib):
+    out = subprocess.run(["nm", "-D", "--defined-only", built_lib], capture_output=True, text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = [s for s in _capi.header_symbols() if s not in exported]
+    assert not missing, missing
+    L = _capi.lib()
+    for s in _capi.header_symbols():
+        assert getattr(L, s) is not None
+
+
+def test_built_for_gfx950(built_lib):
+    data = open(built_lib, "rb").read()
+    assert b".hip_fatbin" in data
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+
+
+def test_abi_version_and_format(built_lib):
+    L = _capi.lib()
+    assert L.oxh_abi_version() == 1
+    buf = ctypes.create_string_buffer(40)
+    # unpadded lowercase hex (merkle_hash.rs:73-77)
+    n = L.oxh_format_hex(0x688558138047f8a, 0x2da4b9c5a75caad3 >> 4, buf)
+    v = (0x2da4b9c5a75caad3 >> 4 << 64) | 0x688558138047f8a
+    assert buf.value.decode() == format(v, "x") and n == len(format(v, "x"))
+    for v in [0, 1, 15, 16, (1 << 128) - 1, 1 << 64, 0x393ba5849f5590fc5985c4bbcec0003f]:
+        L.oxh_format_hex(v & (2**64 - 1), v >> 64, buf)
+        assert buf.value.decode() == format(v, "x")
+        L.oxh_format_dec(v & (2**64 - 1), v >> 64, buf)
+        assert buf.value.decode() == str(v)  # dedup chunk names (fixedsize.rs:78)
+
+
+def test_no_cpu_fallback_without_device(built_lib):
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(_capi.OxenError) as e:
+        _capi.Context(0)
+    assert e.value.code in (_capi.OXH_ERR_NODEVICE, _capi.OXH_ERR_HIP)
+    from oxen_amd import hasher
+
+    with pytest.raises(_capi.OxenError):
+        hasher.hash_buffer(b"hello")
