@@ -10,7 +10,7 @@
  *
  * Conventions:
  *   - plain pointers and sizes only; no torch / Rust / HIP-runtime types in the signatures
- *     (`stream` is an opaque hipStream_t, NULL = the context's own stream);
+ *     (`stream` is an opaque hipStream_t; NULL = the null stream, as in HIP itself);
  *   - every function returns an int status (OXH_OK == 0); batch calls also fill a per-item
  *     `status[]` so one unreadable file never fails the batch (add.rs:533-544 logs and skips);
  *   - the library never frees caller memory and retains no caller pointer after returning;

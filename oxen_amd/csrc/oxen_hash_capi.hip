@@ -84,6 +84,18 @@ int launch_wave(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens
     return OXH_OK;
 }
 
+// Fixed-size chunks of one buffer (no descriptor table): chunk i = [i*chunk, min((i+1)*chunk, total)).
+int launch_chunks(const uint8_t* buf, uint64_t n, uint64_t chunk, uint64_t total, uint64_t* out, hipStream_t st) {
+    if (n == 0) return OXH_OK;
+    const uint64_t blocks = (n + 3) / 4;
+    if (g_variant.load() == 1)
+        hipLaunchKernelGGL((oxh::xxh3_wave_kernel<false, 1>), dim3((unsigned)blocks), dim3(256), 0, st, buf, nullptr, nullptr, n, chunk, total, out);
+    else
+        hipLaunchKernelGGL((oxh::xxh3_wave_kernel<false, 0>), dim3((unsigned)blocks), dim3(256), 0, st, buf, nullptr, nullptr, n, chunk, total, out);
+    HIP_TRY(hipGetLastError());
+    return OXH_OK;
+}
+
 int launch_lane(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens, uint64_t n, uint64_t* out,
                 hipStream_t st) {
     if (n == 0) return OXH_OK;
@@ -186,50 +198,29 @@ struct oxh_ctx {
     uint64_t* h_out[NSLOT] = {};
     uint64_t* d_out[NSLOT] = {};
     hipEvent_t ev_copied[NSLOT] = {}, ev_done[NSLOT] = {};
-    uint64_t* d_scratch = nullptr;
-    uint64_t scratch_bytes = 0;
     Pool* pool = nullptr;
     std::mutex mu;
 };
 
 namespace {
 
-int ctx_scratch(oxh_ctx* c, uint64_t bytes) {
-    if (c->scratch_bytes >= bytes) return OXH_OK;
-    if (c->d_scratch) {
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        HIP_TRY(hipFree(c->d_scratch));
-        c->d_scratch = nullptr;
-        c->scratch_bytes = 0;
-    }
-    if (hipMalloc(&c->d_scratch, bytes) != hipSuccess) return fail(OXH_ERR_NOMEM, "scratch hipMalloc failed");
-    c->scratch_bytes = bytes;
-    return OXH_OK;
-}
-
 // K1L on a device buffer (block sums + chain); small buffers fall back to one K1 wave.
 int large_device(oxh_ctx* c, const uint8_t* d_buf, uint64_t len, uint64_t* d_out, hipStream_t st) {
     const uint64_t nb = len > 0 ? (len - 1) >> 10 : 0;
-    if (nb < 1024) {
-        // one wave is faster than two launches below ~1 MiB; descriptors live in the scratch
-        int rc = ctx_scratch(c, 64);
-        if (rc) return rc;
-        uint64_t desc[2] = {0, len};
-        HIP_TRY(hipMemcpyAsync(c->d_scratch, desc, 16, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipStreamSynchronize(st));  // `desc` is a stack array
-        return launch_wave(d_buf, c->d_scratch, c->d_scratch + 1, 1, d_out, st);
-    }
-    int rc = ctx_scratch(c, nb * 64);
-    if (rc) return rc;
+    if (nb < 1024) return launch_chunks(d_buf, 1, len, len, d_out, st);  // one K1 wave below ~1 MiB
+    // block sums live in stream-ordered scratch, so concurrent calls on different streams never share it
+    uint64_t* sums = nullptr;
+    HIP_TRY(hipMallocAsync((void**)&sums, nb * 64, st));
     const bool aligned = (reinterpret_cast<uintptr_t>(d_buf) & 15) == 0;
     const uint64_t nwaves = (nb + 3) / 4, blocks = (nwaves + 3) / 4;
     if (aligned)
-        hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, d_buf, nb, c->d_scratch);
+        hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, d_buf, nb, sums);
     else
-        hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, d_buf, nb, c->d_scratch);
+        hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, d_buf, nb, sums);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(oxh::xxh3_chain_kernel<true>, dim3(1), dim3(64), 0, st, d_buf, len, c->d_scratch, d_out);
+    hipLaunchKernelGGL(oxh::xxh3_chain_kernel<true>, dim3(1), dim3(64), 0, st, d_buf, len, sums, d_out);
     HIP_TRY(hipGetLastError());
+    HIP_TRY(hipFreeAsync(sums, st));
     return OXH_OK;
 }
 
@@ -348,7 +339,6 @@ int oxh_ctx_destroy(oxh_ctx* c) {
         if (c->ev_copied[s]) (void)hipEventDestroy(c->ev_copied[s]);
         if (c->ev_done[s]) (void)hipEventDestroy(c->ev_done[s]);
     }
-    if (c->d_scratch) (void)hipFree(c->d_scratch);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     delete c->pool;
@@ -372,32 +362,14 @@ int oxh_xxh3_128_batch_device(const void* d_arena, const uint64_t* d_offsets, co
 int oxh_chunk_digests_device(const void* d_buf, uint64_t len, uint64_t chunk, uint64_t* d_out, void* stream) {
     if (len == 0) return OXH_OK;
     if (!d_buf || !d_out || chunk == 0) return fail(OXH_ERR_INVALID, "bad chunk arguments");
-    const uint64_t n = (len + chunk - 1) / chunk;
-    const uint64_t blocks = (n + 3) / 4;
-    if (g_variant.load() == 1)
-        hipLaunchKernelGGL((oxh::xxh3_wave_kernel<false, 1>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
-                           (const uint8_t*)d_buf, nullptr, nullptr, n, chunk, len, d_out);
-    else
-        hipLaunchKernelGGL((oxh::xxh3_wave_kernel<false, 0>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
-                           (const uint8_t*)d_buf, nullptr, nullptr, n, chunk, len, d_out);
-    HIP_TRY(hipGetLastError());
-    return OXH_OK;
+    return launch_chunks((const uint8_t*)d_buf, (len + chunk - 1) / chunk, chunk, len, d_out, (hipStream_t)stream);
 }
 
 int oxh_xxh3_128_large_device(oxh_ctx* c, const void* d_buf, uint64_t len, uint64_t* d_out, void* stream) {
     if (!c || !d_out || (!d_buf && len)) return fail(OXH_ERR_INVALID, "bad large-buffer arguments");
     std::lock_guard<std::mutex> g(c->mu);
     HIP_TRY(hipSetDevice(c->device));
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    if (len == 0) {
-        // zero-length buffers still hash on the device (lane kernel, descriptors in scratch)
-        int rc = ctx_scratch(c, 64);
-        if (rc) return rc;
-        uint64_t desc[2] = {0, 0};
-        HIP_TRY(hipMemcpyAsync(c->d_scratch, desc, 16, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipStreamSynchronize(st));
-        return launch_lane((const uint8_t*)c->d_scratch, c->d_scratch, c->d_scratch + 1, 1, d_out, st);
-    }
+    hipStream_t st = (hipStream_t)stream;  // NULL = the null stream, as for every device entry point
     return large_device(c, (const uint8_t*)d_buf, len, d_out, st);
 }
 
