@@ -1,0 +1,75 @@
+"""Measure attainable HBM read bandwidth on this GPU (diagnostic for the K1 roofline).
+
+    python tools/readbw.py [--gib 6.1]
+
+Prints one JSON line: best flat dwordx4 read stream, the K1 access pattern with the hash replaced
+by an xor, and the real K1 kernel on the same bytes (C2 shape), all timed with HIP events on the
+launch stream, interleaved in one process (median of rounds).
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import statistics
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+SO = os.path.join(ROOT, "tools", "libreadbw.so")
+
+
+def build():
+    src = os.path.join(ROOT, "tools", "readbw.hip")
+    if not os.path.exists(SO) or os.path.getmtime(SO) < os.path.getmtime(src):
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-shared", "-fPIC", "-o", SO, src],
+                       check=True)
+    L = ctypes.CDLL(SO)
+    L.readbw_flat.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    L.readbw_items.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+    return L
+
+
+def main():
+    import torch
+
+    from oxen_amd.device import DeviceArena
+
+    L = build()
+    n, item = 100_000, 65_536
+    da = DeviceArena.splitmix([item] * n, seed=1)
+    nbytes = n * item
+    sink = torch.zeros(1024, dtype=torch.int32, device="cuda")
+    out = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+
+    def timed(fn, reps=10):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / 1e3 / reps
+
+    variants = {}
+    for blocks in (2048, 4096, 8192, 16384):
+        for unroll in (1, 4, 8):
+            variants[f"flat_b{blocks}_u{unroll}"] = (lambda b=blocks, u=unroll:
+                                                      L.readbw_flat(da.arena.data_ptr(), nbytes, sink.data_ptr(), b, u, st))
+    variants["k1_pattern_xor"] = lambda: L.readbw_items(da.arena.data_ptr(), n, item, sink.data_ptr(), st)
+    variants["k1_xxh3"] = lambda: da.hash(out)
+    res = {k: [] for k in variants}
+    for _ in range(5):
+        for k, fn in variants.items():
+            res[k].append(nbytes / timed(fn) / 1e9)
+    med = {k: round(statistics.median(v), 1) for k, v in res.items()}
+    best_flat = max((v, k) for k, v in med.items() if k.startswith("flat"))
+    print(json.dumps({"unit": "GB/s", "bytes": nbytes, "median_of_5": med,
+                      "attainable_read_GBs": best_flat[0], "attainable_variant": best_flat[1]}))
+
+
+if __name__ == "__main__":
+    main()
