@@ -72,14 +72,28 @@ int check_device(int device) {
 }
 
 // ---------------------------------------------------------------- kernel launch helpers
+using WaveKernel = void (*)(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+
+template <bool DESC>
+WaveKernel wave_kernel_for(int variant) {
+    switch (variant) {
+        case 1: return oxh::xxh3_wave_kernel<DESC, 1>;
+        case 2: return oxh::xxh3_wave_kernel<DESC, 2>;
+        case 4: return oxh::xxh3_wave_kernel<DESC, 4>;
+        case 8: return oxh::xxh3_wave_kernel<DESC, 8>;
+        case 12: return oxh::xxh3_wave_kernel<DESC, 12>;
+        case 64: return oxh::xxh3_wave_kernel<DESC, 64>;
+        default: return oxh::xxh3_wave_kernel<DESC, 0>;
+    }
+}
+
+// K1 over a descriptor table: one 64-lane wave per item, 4 waves per 256-thread workgroup.
 int launch_wave(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens, uint64_t n, uint64_t* out,
                 hipStream_t st) {
     if (n == 0) return OXH_OK;
     const uint64_t blocks = (n + 3) / 4;
-    if (g_variant.load() == 1)
-        hipLaunchKernelGGL((oxh::xxh3_wave_kernel<true, 1>), dim3((unsigned)blocks), dim3(256), 0, st, arena, offs, lens, n, 0, 0, out);
-    else
-        hipLaunchKernelGGL((oxh::xxh3_wave_kernel<true, 0>), dim3((unsigned)blocks), dim3(256), 0, st, arena, offs, lens, n, 0, 0, out);
+    hipLaunchKernelGGL(wave_kernel_for<true>(g_variant.load()), dim3((unsigned)blocks), dim3(256), 0, st, arena, offs, lens, n,
+                       (uint64_t)0, (uint64_t)0, out);
     HIP_TRY(hipGetLastError());
     return OXH_OK;
 }
@@ -88,10 +102,8 @@ int launch_wave(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens
 int launch_chunks(const uint8_t* buf, uint64_t n, uint64_t chunk, uint64_t total, uint64_t* out, hipStream_t st) {
     if (n == 0) return OXH_OK;
     const uint64_t blocks = (n + 3) / 4;
-    if (g_variant.load() == 1)
-        hipLaunchKernelGGL((oxh::xxh3_wave_kernel<false, 1>), dim3((unsigned)blocks), dim3(256), 0, st, buf, nullptr, nullptr, n, chunk, total, out);
-    else
-        hipLaunchKernelGGL((oxh::xxh3_wave_kernel<false, 0>), dim3((unsigned)blocks), dim3(256), 0, st, buf, nullptr, nullptr, n, chunk, total, out);
+    hipLaunchKernelGGL(wave_kernel_for<false>(g_variant.load()), dim3((unsigned)blocks), dim3(256), 0, st, buf,
+                       (const uint64_t*)nullptr, (const uint64_t*)nullptr, n, chunk, total, out);
     HIP_TRY(hipGetLastError());
     return OXH_OK;
 }

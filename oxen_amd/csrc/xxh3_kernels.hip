@@ -84,9 +84,30 @@ __device__ __forceinline__ void bcast_rows64(uint64_t x, uint64_t t[4], int lane
     t[3] = ((uint64_t)h3 << 32) | l3;
 }
 
-template <bool ALIGNED>
+// Kernel variant knobs (diagnostic A/B through oxh_set_kernel_variant; 0 is the shipped path):
+//   bit 0     cross-row broadcast: 0 = permlane16/32 swaps, 1 = ds_bpermute (__shfl)
+//   bit 1     0 = non-temporal (nt) loads for the once-read input stream, 1 = default-policy loads
+//   bits 2-3  rounds in flight per wave (software pipeline depth): 0 -> 4, 1 -> 3, 2 -> 2, 3 -> 5
+//   bit 4     1 = stagger: waves of the first resident generation start 0..15 x ~1 us apart
+//   bit 6     1 = stripe keys read from an LDS copy of the secret at each use (fewer VGPRs)
+// Measured on MI355X (C2, tools/readbw.py, profiles/r01_readbw*.json): nt loads ~+11 % over
+// default-policy loads; 4 rounds in flight (2 waves/SIMD at 180 VGPRs) ~+4 % over 2 rounds (5 waves/SIMD).
+template <int V>
+struct Cfg {
+    static constexpr int BCAST = V & 1;
+    static constexpr bool NT = ((V >> 1) & 1) == 0;
+    static constexpr int DEPTH = ((V >> 2) & 3) == 0 ? 4 : ((V >> 2) & 3) == 1 ? 3 : ((V >> 2) & 3) == 2 ? 2 : 5;
+    static constexpr bool KEYS_LDS = ((V >> 6) & 1) != 0;
+    static constexpr bool STAGGER = ((V >> 4) & 1) != 0;
+};
+
+template <bool ALIGNED, bool NT = false>
 __device__ __forceinline__ uint4 load16(const uint8_t* p) {
-    if constexpr (ALIGNED) {
+    if constexpr (ALIGNED && NT) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else if constexpr (ALIGNED) {
         return *reinterpret_cast<const uint4*>(p);
     } else {
         uint4 v;
@@ -130,56 +151,116 @@ __device__ __forceinline__ void fold_round(uint64_t s0, uint64_t s1, uint64_t& a
     }
 }
 
+// Buffer resource over one item: loads at voffset >= num_records are dropped by the hardware range
+// check (no memory traffic, zeros returned), which lets the pipeline issue every prefetch
+// unconditionally -- no branch around a load, so the register ring never needs a phi/copy.
+constexpr uint32_t kOOB = 0xFFFFF000u;
+constexpr int kRsrcFlags = 0x00020000;  // gfx950 raw-buffer descriptor word 3
+
+template <bool NT>
+__device__ __forceinline__ uint4 bload16(__amdgpu_buffer_rsrc_t rsrc, uint32_t voff) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 0, NT ? 2 : 0);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 // The long path (len > 240) for one buffer, executed by one full wave. Writes out[0..1] from lane 0.
-template <bool ALIGNED, int VARIANT>
+// All input loads are raw buffer loads (gfx950 supports unaligned buffer access, so any start offset
+// is fine); the descriptor is re-based every 1 GiB so 32-bit offsets cover buffers of any length.
+template <int VARIANT>
 __device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_t len,
-                                          uint64_t* __restrict__ out, int lane) {
+                                          uint64_t* __restrict__ out, int lane, const uint64_t* lds_sec) {
     const int g = lane >> 4, q = (lane >> 2) & 3, k = lane & 3;
-    uint64_t key0[4], key1[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        key0[j] = kSecW[4 * j + q + 2 * k];
-        key1[j] = kSecW[4 * j + q + 2 * k + 1];
-    }
+    // stripe keys: secret words (4j + q + 2k, +1)
+    auto keys = [&](int j, uint64_t& k0, uint64_t& k1) {
+        int idx = 4 * j + q + 2 * k;
+        if constexpr (Cfg<VARIANT>::KEYS_LDS) {
+            asm volatile("" : "+v"(idx));  // opaque: keep the LDS reads inside the loop
+            k0 = lds_sec[idx];
+            k1 = lds_sec[idx + 1];
+        } else {
+            k0 = kSecW[idx];
+            k1 = kSecW[idx + 1];
+        }
+    };
     const uint64_t sk0 = kSecW[16 + 2 * k], sk1 = kSecW[16 + 2 * k + 1];
     uint64_t a0 = kInitW[2 * k], a1 = kInitW[2 * k + 1];
 
     const uint64_t nb = (len - 1) >> 10;  // blocks followed by a scramble
     const uint64_t nr = nb >> 2;          // full rounds (4 scrambled blocks each)
-    const uint8_t* lp = p + (uint64_t)g * 1024 + (uint64_t)q * 64 + (uint64_t)k * 16;
+    const uint32_t lane_off = (uint32_t)(g * 1024 + q * 64 + k * 16);
+    // round rr lives in 1 GiB window rr >> 18; descriptor over that window (wave-uniform, SALU work)
+    auto window_rsrc = [&](uint64_t rr) {
+        const uint64_t base = (rr >> 18) << 30;
+        const uint64_t rem = len - base;
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(p + base), (short)0,
+                                                 (int)(rem < 0x7FFFFFFFull ? rem : 0x7FFFFFFFull), kRsrcFlags);
+    };
+    auto load_round = [&](uint64_t rr, bool live, uint4 (&dst)[4]) {
+        const __amdgpu_buffer_rsrc_t rsrc = window_rsrc(rr);
+        const uint32_t vo = live ? (uint32_t)(rr & 0x3FFFF) * 4096u + lane_off : kOOB;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dst[j] = bload16<Cfg<VARIANT>::NT>(rsrc, vo + j * 256);
+    };
+    auto fold4 = [&](const uint4 (&src)[4], int nfull) {
+        uint64_t s0 = 0, s1 = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint64_t k0, k1;
+            keys(j, k0, k1);
+            accum16(src[j], k0, k1, s0, s1);
+        }
+        fold_round<Cfg<VARIANT>::BCAST>(s0, s1, a0, a1, sk0, sk1, nfull, lane);
+    };
 
     if (nr > 0) {
-        // software pipeline: round r+1's four loads are in flight while round r is folded
-        uint4 cur[4];
+        // Software pipeline with a static register ring: slot d holds round r + d; D rounds
+        // (4D dwordx4 per lane) are in flight when a round is folded.
+        constexpr int D = Cfg<VARIANT>::DEPTH;
+        uint4 ring[D][4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) cur[j] = load16<ALIGNED>(lp + j * 256);
-        for (uint64_t r = 0; r < nr; ++r) {
-            const uint64_t rn = (r + 1 < nr) ? r + 1 : r;
-            uint4 nxt[4];
+        for (int d = 0; d < D; ++d) load_round((uint64_t)d, (uint64_t)d < nr, ring[d]);
+        const uint64_t nmain = nr - nr % D;
+        for (uint64_t r = 0; r < nmain; r += D) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) nxt[j] = load16<ALIGNED>(lp + rn * 4096 + j * 256);
-            uint64_t s0 = 0, s1 = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) accum16(cur[j], key0[j], key1[j], s0, s1);
-            fold_round<VARIANT>(s0, s1, a0, a1, sk0, sk1, 4, lane);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+            for (int d = 0; d < D; ++d) {
+                fold4(ring[d], 4);
+                load_round(r + d + D, r + d + D < nr, ring[d]);
+                // keep slot d+1's arithmetic below this point: otherwise the scheduler hoists its
+                // data-only adds above the refill and hipcc has to drain every load (vmcnt(0))
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
+        // the last nr % D rounds are already in ring slots 0 .. nr % D - 1
+#pragma unroll
+        for (int d = 0; d < D - 1; ++d)
+            if (nmain + d < nr) fold4(ring[d], 4);
     }
-    // final round: (nb - 4nr) full blocks, then the partial block with `ns` stripes
+    // final round: (nb - 4nr) full blocks, then the partial block with `ns` stripes; lanes whose
+    // stripe lies past the data read nothing (offset out of the buffer's range)
     {
         const uint64_t b = nr * 4 + g;
         const uint64_t ns = ((len - 1) - (nb << 10)) >> 6;
+        const __amdgpu_buffer_rsrc_t rsrc = window_rsrc(nr);
+        uint4 d[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t s = 4 * j + q;
+            const bool live = b < nb || (b == nb && s < ns);
+            d[j] = bload16<false>(rsrc, live ? (uint32_t)(nr & 0x3FFFF) * 4096u + lane_off + j * 256 : kOOB);
+        }
+        // a dropped (zero) piece would still add mul(0 ^ key) -- mask the contribution instead
         uint64_t s0 = 0, s1 = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint64_t s = 4 * j + q;
             if (b < nb || (b == nb && s < ns)) {
-                const uint4 d = load16<ALIGNED>(lp + nr * 4096 + j * 256);
-                accum16(d, key0[j], key1[j], s0, s1);
+                uint64_t k0, k1;
+                keys(j, k0, k1);
+                accum16(d[j], k0, k1, s0, s1);
             }
         }
-        fold_round<VARIANT>(s0, s1, a0, a1, sk0, sk1, (int)(nb - nr * 4), lane);
+        fold_round<Cfg<VARIANT>::BCAST>(s0, s1, a0, a1, sk0, sk1, (int)(nb - nr * 4), lane);
     }
     // last stripe, at len - 64, with the secret shifted to offset 121
     {
@@ -209,9 +290,20 @@ __global__ __launch_bounds__(256) void xxh3_wave_kernel(const uint8_t* __restric
                                                         const uint64_t* __restrict__ lens, uint64_t n,
                                                         uint64_t chunk, uint64_t total,
                                                         uint64_t* __restrict__ out) {
+    __shared__ uint64_t lds_sec[24];
+    if constexpr (Cfg<VARIANT>::KEYS_LDS) {
+        if (threadIdx.x < 24) lds_sec[threadIdx.x] = kSecW[threadIdx.x];
+        __syncthreads();
+    }
     const int lane = threadIdx.x & 63;
     const uint64_t item = (uint64_t)blockIdx.x * 4 + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (item >= n) return;
+    if constexpr (Cfg<VARIANT>::STAGGER) {
+        if (blockIdx.x < 2048) {
+            const int steps = (int)(item & 15) * 40;  // s_sleep 1 ~ 64 clocks
+            for (int t = 0; t < steps; ++t) __builtin_amdgcn_s_sleep(1);
+        }
+    }
     uint64_t off, len;
     if constexpr (DESC) {
         off = offsets[item];
@@ -230,10 +322,7 @@ __global__ __launch_bounds__(256) void xxh3_wave_kernel(const uint8_t* __restric
         }
         return;
     }
-    if ((reinterpret_cast<uintptr_t>(p) & 15) == 0)
-        wave_long<true, VARIANT>(p, len, o, lane);
-    else
-        wave_long<false, VARIANT>(p, len, o, lane);
+    wave_long<VARIANT>(p, len, o, lane, lds_sec);
 }
 
 // K1s: one lane per item (any length; intended for short items).
@@ -389,11 +478,21 @@ __global__ void fill_splitmix_tail_kernel(uint8_t* __restrict__ dst, uint64_t wo
     for (uint64_t j = 0; j < nbytes; ++j) dst[j] = (uint8_t)(v >> (8 * j));
 }
 
-// explicit instantiations used by the host runtime
+// explicit instantiations used by the host runtime (variants: see Cfg)
 template __global__ void xxh3_wave_kernel<true, 0>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
-template __global__ void xxh3_wave_kernel<true, 1>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 template __global__ void xxh3_wave_kernel<false, 0>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<true, 1>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 template __global__ void xxh3_wave_kernel<false, 1>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<true, 2>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<false, 2>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<true, 4>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<false, 4>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<true, 8>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<false, 8>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<true, 12>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<false, 12>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<true, 64>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<false, 64>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 template __global__ void xxh3_blocksum_kernel<true>(const uint8_t*, uint64_t, uint64_t*);
 template __global__ void xxh3_blocksum_kernel<false>(const uint8_t*, uint64_t, uint64_t*);
 template __global__ void xxh3_chain_kernel<true>(const uint8_t*, uint64_t, const uint64_t*, uint64_t*);

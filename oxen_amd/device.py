@@ -113,9 +113,10 @@ class DeviceArena:
         return int(self.lens_host.sum())
 
     @classmethod
-    def splitmix(cls, lens, seed: int = 0, device="cuda", align: int = 256) -> "DeviceArena":
+    def splitmix(cls, lens, seed: int = 0, device="cuda", align: int = 256, pad: int = 0) -> "DeviceArena":
+        """Items packed back to back at `align`-byte boundaries (plus `pad` spare bytes after each)."""
         lens_h = np.asarray(lens, dtype=np.uint64)
-        offs_h, total = packed_layout(lens_h, align)
+        offs_h, total = packed_layout(lens_h + np.uint64(pad), align)
         alloc = max(8, (total + 7) // 8 * 8)
         arena = torch.empty(alloc, dtype=torch.uint8, device=device)
         fill_splitmix(arena, seed, alloc)

@@ -39,8 +39,11 @@ def _mismatch(got, want, lens):
     return [int(lens[i]) for i in bad[:20]]
 
 
+VARIANTS = [0, 1, 2, 4, 8, 12, 64]  # K1 variants (xxh3_kernels.hip Cfg); 0 is the shipped path
+
+
 @pytest.mark.parametrize("mode", [0, 1, 2])
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", VARIANTS)
 def test_every_length_unaligned(cuda, golden, mode, variant):
     """Every length 0..2048 + boundaries up to 1 MiB+1, at the golden (mostly unaligned) offsets."""
     import torch
@@ -59,7 +62,7 @@ def test_every_length_unaligned(cuda, golden, mode, variant):
     assert not _mismatch(got, want, lens)
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", VARIANTS)
 def test_every_length_aligned(cuda, golden, variant):
     """Same vectors re-packed at 256-B aligned offsets (the coalesced dwordx4 path)."""
     from oxen_amd import _capi

@@ -27,7 +27,7 @@ def build():
                        check=True)
     L = ctypes.CDLL(SO)
     L.readbw_flat.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
-    L.readbw_items.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+    L.readbw_items.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
     return L
 
 
@@ -56,15 +56,45 @@ def main():
 
     variants = {}
     for blocks in (2048, 4096, 8192, 16384):
-        for unroll in (1, 4, 8):
+        for unroll in (1, 4, 8, 108):
             variants[f"flat_b{blocks}_u{unroll}"] = (lambda b=blocks, u=unroll:
                                                       L.readbw_flat(da.arena.data_ptr(), nbytes, sink.data_ptr(), b, u, st))
-    variants["k1_pattern_xor"] = lambda: L.readbw_items(da.arena.data_ptr(), n, item, sink.data_ptr(), st)
-    variants["k1_xxh3"] = lambda: da.hash(out)
+    # memory-pattern-only kernels over a larger arena so item pitches can be skewed
+    big = torch.empty(n * (item + 4096), dtype=torch.uint8, device="cuda")
+    big.fill_(7)
+    for kind, kname in ((0, "rows"), (1, "flat1k"), (2, "rows_nt"), (3, "flat1k_nt")):
+        for pitch in (item, item + 256, item + 4096):
+            variants[f"items_{kname}_pitch{pitch}"] = (lambda k=kind, p=pitch:
+                                                       L.readbw_items(big.data_ptr(), n, item, p, k, sink.data_ptr(), st))
+    from oxen_amd import _capi
+
+    def k1(v):
+        def f():
+            _capi.lib().oxh_set_kernel_variant(v)
+            da.hash(out)
+        return f
+
+    ref = None
+    for v in (0, 1, 2, 4, 8, 12, 64):
+        variants[f"k1_xxh3_v{v}"] = k1(v)
+        k1(v)()
+        torch.cuda.synchronize()
+        d = out.cpu()
+        if ref is None:
+            ref = d
+        assert torch.equal(ref, d), f"variant {v} digests differ from variant 0"
+    # K1 (default variant) on skewed pitches and on a 4x larger batch (tail effect)
+    _capi.lib().oxh_set_kernel_variant(0)
+    for pad in (256, 4096):
+        dap = DeviceArena.splitmix([item] * n, seed=1, pad=pad)
+        variants[f"k1_xxh3_v0_pitch{item + pad}"] = (lambda d=dap: (_capi.lib().oxh_set_kernel_variant(0), d.hash(out)))
+    big4 = DeviceArena.splitmix([item] * (4 * n), seed=1)
+    out4 = torch.empty((4 * n, 2), dtype=torch.int64, device="cuda")
+    variants["k1_xxh3_v0_x4items_per_byte"] = lambda: (_capi.lib().oxh_set_kernel_variant(0), big4.hash(out4))
     res = {k: [] for k in variants}
     for _ in range(5):
         for k, fn in variants.items():
-            res[k].append(nbytes / timed(fn) / 1e9)
+            res[k].append((4 if "x4items" in k else 1) * nbytes / timed(fn) / 1e9)
     med = {k: round(statistics.median(v), 1) for k, v in res.items()}
     best_flat = max((v, k) for k, v in med.items() if k.startswith("flat"))
     print(json.dumps({"unit": "GB/s", "bytes": nbytes, "median_of_5": med,
