@@ -16,6 +16,8 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <atomic>
 #include <condition_variable>
 #include <functional>
@@ -240,7 +242,8 @@ int large_device(oxh_ctx* c, const uint8_t* d_buf, uint64_t len, uint64_t* d_out
 int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_only) {
     const uint64_t M = c->max_items;
     HIP_TRY(hipMemcpyAsync(c->d_stage[s], c->h_stage[s], bytes, hipMemcpyHostToDevice, c->copy_stream));
-    HIP_TRY(hipMemcpyAsync(c->d_desc[s], c->h_desc[s], M * 16, hipMemcpyHostToDevice, c->copy_stream));
+    HIP_TRY(hipMemcpyAsync(c->d_desc[s], c->h_desc[s], cnt * 8, hipMemcpyHostToDevice, c->copy_stream));
+    HIP_TRY(hipMemcpyAsync(c->d_desc[s] + M, c->h_desc[s] + M, cnt * 8, hipMemcpyHostToDevice, c->copy_stream));
     HIP_TRY(hipEventRecord(c->ev_copied[s], c->copy_stream));
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[s], 0));
     int rc = any_short_only ? launch_lane(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->stream)
@@ -250,6 +253,16 @@ int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_
     HIP_TRY(hipEventRecord(c->ev_done[s], c->stream));
     return OXH_OK;
 }
+
+// OXH_TRACE=1: per-call stage times on stderr (host-side wall clock)
+struct Trace {
+    bool on = getenv("OXH_TRACE") != nullptr;
+    double fill = 0, drain = 0, submit = 0, stat = 0;
+    int batches = 0;
+    static double now() {
+        return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
+};
 
 struct Pending {
     bool busy = false;
@@ -399,7 +412,9 @@ int oxh_combined_hash_device(const uint64_t* d_content, const uint64_t* d_metada
 // `reader(i, dst)` directly into the pinned slot; lens[i] is known up front.
 static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
                            const std::function<int(uint64_t, uint8_t*)>& fill, uint64_t* out, int32_t* status,
-                           bool short_only_lane) {
+                           bool short_only_lane, Trace* tr = nullptr) {
+    Trace local;
+    if (!tr) tr = &local;
     Pending pend[NSLOT];
     int slot = 0;
     uint64_t i = 0;
@@ -437,8 +452,11 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
         if (batch.empty()) continue;
         const int s = slot;
         slot = (slot + 1) % NSLOT;
+        double t0 = Trace::now();
         int rc = drain_slot(c, s, pend[s], out);
         if (rc) return rc;
+        double t1 = Trace::now();
+        tr->drain += t1 - t0;
         // lay out the slot
         const uint64_t M = c->max_items;
         uint64_t* hoff = c->h_desc[s];
@@ -463,20 +481,24 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
             if (status) status[batch[j]] = st[j];
             if (st[j] != OXH_OK) hlen[j] = 0;  // keep the batch alive; digest is zeroed below
         }
+        double t2 = Trace::now();
+        tr->fill += t2 - t1;
         rc = submit_slot(c, s, off, batch.size(), short_only_lane && all_short);
         if (rc) return rc;
+        tr->submit += Trace::now() - t2;
+        tr->batches++;
         pend[s].busy = true;
         pend[s].ids = batch;
-        if (status) {
-            // remember failures so their digests are zeroed after the drain
-            for (size_t j = 0; j < batch.size(); ++j)
-                if (st[j] != OXH_OK) pend[s].ids[j] = pend[s].ids[j];
-        }
     }
+    double t3 = Trace::now();
     for (int s = 0; s < NSLOT; ++s) {
         int rc = drain_slot(c, s, pend[s], out);
         if (rc) return rc;
     }
+    tr->drain += Trace::now() - t3;
+    if (tr->on)
+        fprintf(stderr, "[oxh] items=%llu batches=%d stat=%.3fs fill=%.3fs drain-wait=%.3fs submit=%.3fs threads=%d\n",
+                (unsigned long long)n, tr->batches, tr->stat, tr->fill, tr->drain, tr->submit, c->pool->size());
     if (status)
         for (uint64_t k = 0; k < n; ++k)
             if (status[k] != OXH_OK) out[2 * k] = out[2 * k + 1] = 0;
@@ -525,6 +547,8 @@ int oxh_hash_files(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* o
     std::lock_guard<std::mutex> g(c->mu);
     HIP_TRY(hipSetDevice(c->device));
     // stat pass (util::fs::metadata in add.rs:716/741), parallel
+    Trace tr;
+    const double ts = Trace::now();
     std::vector<uint64_t> lens(n, 0);
     std::vector<int32_t> st(n, OXH_OK);
     const int ntasks = (int)std::min<uint64_t>(n, (uint64_t)c->pool->size() * 4);
@@ -538,11 +562,12 @@ int oxh_hash_files(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* o
             }
         }
     });
+    tr.stat = Trace::now() - ts;
     std::vector<int32_t> st2(n, OXH_OK);
     int rc = hash_host_items(c, n, lens.data(), [&](uint64_t i, uint8_t* dst) {
         if (st[i] != OXH_OK) return (int)st[i];
         return read_whole(paths[i], dst, lens[i]);
-    }, out, st2.data(), false);
+    }, out, st2.data(), false, &tr);
     if (rc) return rc;
     for (uint64_t i = 0; i < n; ++i) {
         if (sizes) sizes[i] = lens[i];

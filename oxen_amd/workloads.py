@@ -86,6 +86,63 @@ def image_bytes(i: int, seed: int = 0, size=(128, 128)) -> bytes:
     return buf.getvalue()
 
 
+_TIFF_HEADER = {}
+
+
+def tiff_header(size=(128, 128)) -> bytes:
+    """The 140-byte header + IFD PIL writes for an uncompressed RGB TIFF of this size (pixels follow)."""
+    if size not in _TIFF_HEADER:
+        import io
+
+        from PIL import Image
+
+        buf = io.BytesIO()
+        Image.fromarray(np.zeros((size[0], size[1], 3), dtype=np.uint8)).save(buf, format="TIFF")
+        b = buf.getvalue()
+        _TIFF_HEADER[size] = b[: len(b) - size[0] * size[1] * 3]
+    return _TIFF_HEADER[size]
+
+
+def image_bytes_fast(i: int, seed: int = 0, size=(128, 128)) -> bytes:
+    """C3 image i: PIL's TIFF header + splitmix64 noise pixels (bytes [i*P, (i+1)*P) of the stream)."""
+    p = size[0] * size[1] * 3
+    return tiff_header(size) + splitmix_bytes(seed, i * p, p).tobytes()
+
+
+def write_image_repo_fast(root: str, num_images: int, num_dirs: int = 1000, seed: int = 0, size=(128, 128),
+                          threads: int = 16) -> list[str]:
+    """Config 3 at full scale in seconds: the same directory layout as generate_image_repo.py with
+    TIFF files whose pixel bytes come from the splitmix64 stream (valid TIFFs, see tests)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    images = os.path.join(root, "images")
+    for d in range(min(num_dirs, max(num_images, 1))):
+        os.makedirs(os.path.join(images, f"split_{d}"), exist_ok=True)
+    hdr = tiff_header(size)
+    p = size[0] * size[1] * 3
+    paths = [os.path.join(images, f"split_{i % num_dirs}", f"noise_image_{i}.tiff") for i in range(num_images)]
+    chunk = 2000
+
+    def work(c0):
+        c1 = min(num_images, c0 + chunk)
+        px = splitmix_bytes(seed, c0 * p, (c1 - c0) * p)
+        for i in range(c0, c1):
+            with open(paths[i], "wb") as f:
+                f.write(hdr)
+                f.write(px[(i - c0) * p:(i - c0 + 1) * p].tobytes())
+
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(work, range(0, num_images, chunk)))
+    labels = np.random.Generator(np.random.PCG64(seed)).choice(["cat", "dog"], size=num_images)
+    with open(os.path.join(root, "images.csv"), "w") as f:
+        f.write("images,labels\n")
+        for path, lab in zip(paths, labels):
+            f.write(f"{os.path.relpath(path, root)},{lab}\n")
+    with open(os.path.join(root, "README.md"), "w") as f:
+        f.write(f"# Sample Repo\n\nGenerated {num_images} images with {num_dirs} directories in {root}")
+    return paths + [os.path.join(root, "images.csv"), os.path.join(root, "README.md")]
+
+
 def write_image_repo(root: str, num_images: int, num_dirs: int = 1000, seed: int = 0, size=(128, 128)) -> list[str]:
     """generate_image_repo.py: images/split_{i % num_dirs}/noise_image_{i}.tiff (+ images.csv, README.md)."""
     images = os.path.join(root, "images")

@@ -1,0 +1,126 @@
+"""End-to-end `oxen add` hash stage from files on disk (config 3), recorded in DESIGN.md.
+
+    python tools/bench_e2e.py [--images 200000] [--dir /tmp/oxh_c3]
+
+Writes the C3 image repo (benchmark/generate_image_repo.py layout: 200 000 noise TIFFs of
+49 292 B in 1 000 dirs + images.csv + README.md), then times, on the same files:
+  gpu_e2e    oxh_hash_files: parallel pread into pinned staging -> H2D on a side stream (3-slot
+             ring, overlapped with K1 on the compute stream) -> D2H digests
+  cpu_ref    the reference's per-file loop restated in C (oracle/): stat, read whole file, one-shot
+             XXH3-128 (hasher.rs:126-148), one worker per host thread
+with the page cache warm, and cold (pages dropped with posix_fadvise DONTNEED). Also reports the
+pinned H2D copy rate. Every GPU digest is checked against the CPU one.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def drop_cache(paths):
+    os.sync()
+    for p in paths:
+        try:
+            fd = os.open(p, os.O_RDONLY)
+            os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+            os.close(fd)
+        except OSError:
+            pass
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--images", type=int, default=200_000)
+    ap.add_argument("--dir", default=os.path.join(os.environ.get("TMPDIR", "/tmp"), "oxh_c3"))
+    ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--keep", action="store_true")
+    a = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    from oracle import oracle
+    from oxen_amd import _capi, hasher
+    from oxen_amd.workloads import write_image_repo_fast
+
+    shutil.rmtree(a.dir, ignore_errors=True)
+    t0 = time.perf_counter()
+    paths = write_image_repo_fast(a.dir, a.images)
+    gen_s = time.perf_counter() - t0
+    nbytes = sum(os.path.getsize(p) for p in paths)
+    res = {"config": "C3: benchmark/generate_image_repo.py layout, %d TIFF 128x128x3 (49 292 B) in 1 000 dirs "
+                     "+ images.csv + README.md" % a.images,
+           "files": len(paths), "bytes": nbytes, "generate_s": round(gen_s, 1), "threads": a.threads}
+
+    os.environ.setdefault("OXH_NUM_THREADS", str(a.threads))
+    ctx = _capi.Context(0)
+    # pinned H2D rate for context
+    src = torch.empty(1 << 30, dtype=torch.uint8).pin_memory()
+    dst = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+    dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    res["h2d_pinned_GBs"] = round(5 * (1 << 30) / (time.perf_counter() - t0) / 1e9, 1)
+    del src, dst
+
+    oracle.build()
+    import ctypes
+
+    n = len(paths)
+    c_paths = (ctypes.c_char_p * n)(*[os.fsencode(p) for p in paths])  # built once, outside the timing
+    L, O = _capi.lib(), oracle.lib()
+
+    def gpu_call():
+        out = np.zeros((n, 2), dtype=np.uint64)
+        sizes = np.zeros(n, dtype=np.uint64)
+        st = np.zeros(n, dtype=np.int32)
+        t0 = time.perf_counter()
+        _capi.check(L.oxh_hash_files(ctx.handle, c_paths, n, out.ctypes.data_as(_capi._u64p),
+                                     sizes.ctypes.data_as(_capi._u64p), st.ctypes.data_as(_capi._i32p)),
+                    "oxh_hash_files")
+        return time.perf_counter() - t0, out, st
+
+    def cpu_call():
+        out = np.zeros((n, 2), dtype=np.uint64)
+        sizes = np.zeros(n, dtype=np.uint64)
+        st = np.zeros(n, dtype=np.int32)
+        t0 = time.perf_counter()
+        O.oxo_hash_files(c_paths, n, out.ctypes.data_as(oracle._u64p), sizes.ctypes.data_as(oracle._u64p),
+                         st.ctypes.data_as(oracle._i32p), a.threads)
+        return time.perf_counter() - t0, out, st
+
+    runs = {}
+    for cache in ("warm", "cold"):
+        for who in ("gpu_e2e", "cpu_ref"):
+            if cache == "cold":
+                drop_cache(paths)
+            else:  # warm: make sure everything is resident
+                oracle.hash_files(paths[: min(len(paths), 1000)], a.threads)
+            dt, out, st = gpu_call() if who == "gpu_e2e" else cpu_call()
+            runs[(who, cache)] = out
+            res[f"{who}_{cache}_s"] = round(dt, 3)
+            res[f"{who}_{cache}_GiBs"] = round(nbytes / dt / 2**30, 2)
+            assert (st == 0).all(), "file errors"
+    res["digests_bit_exact"] = all(np.array_equal(runs[("gpu_e2e", c)], runs[("cpu_ref", c)]) for c in ("warm", "cold"))
+    # the Python mirror (hasher.hash_files_128bit) on warm cache, for its wrapper overhead
+    t0 = time.perf_counter()
+    d, _, _ = hasher.hash_files_128bit(paths, ctx)
+    res["python_mirror_warm_s"] = round(time.perf_counter() - t0, 3)
+    print(json.dumps(res), flush=True)
+    ctx.close()
+    if not a.keep:
+        shutil.rmtree(a.dir, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()
