@@ -1,0 +1,71 @@
+"""N > 1 path on CPU: byte-balanced sharding and the single all-gather of the digest table (gloo)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oxen_amd.shard import gather_digest_table, shard_bounds
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_shard_bounds_cover_and_balance():
+    rng = np.random.default_rng(0)
+    for world in (1, 2, 3, 8):
+        for n in (0, 1, 7, 1000):
+            lens = rng.integers(0, 300_000, n)
+            b = shard_bounds(lens, world)
+            assert len(b) == world
+            assert b[0][0] == 0 and b[-1][1] == n
+            assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
+            if n >= 100 * world:
+                per = [lens[lo:hi].sum() for lo, hi in b]
+                assert max(per) <= lens.sum() / world + lens.max() + world
+
+
+def _worker(rank, world, port, lens, seed, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle
+        from oxen_amd.workloads import packed_layout, splitmix_bytes
+
+        offs, total = packed_layout(lens)
+        arena = splitmix_bytes(seed, 0, total)
+        lo, hi = shard_bounds(lens, world)[rank]
+        # this rank's shard (the oracle stands in for the device here -- test infrastructure)
+        local = oracle.batch(arena, offs[lo:hi], lens[lo:hi]).view(np.int64)
+        counts = [h - l for l, h in shard_bounds(lens, world)]
+        full = gather_digest_table(torch.from_numpy(local.copy()).reshape(-1, 2), counts)
+        if rank == 0:
+            want = oracle.batch(arena, offs, lens).view(np.int64)
+            q.put(bool(np.array_equal(full.numpy(), want)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_digest_table_gloo(world, oracle_lib):
+    rng = np.random.default_rng(world)
+    lens = rng.integers(0, 20_000, 101).astype(np.uint64)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, lens, 5, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert q.get(timeout=10) is True

@@ -1,0 +1,94 @@
+"""Host-side logic that needs no GPU: synthetic generators, layouts, merkle streams and formatting."""
+import io
+import os
+
+import numpy as np
+
+from oxen_amd import merkle, workloads
+
+
+def _splitmix_py(seed, i):
+    m = (1 << 64) - 1
+    z = (seed + (i + 1) * 0x9E3779B97F4A7C15) & m
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    return z ^ (z >> 31)
+
+
+def test_splitmix_bytes_matches_scalar_definition():
+    words = [_splitmix_py(7, i) for i in range(10)]
+    ref = b"".join(w.to_bytes(8, "little") for w in words)
+    assert workloads.splitmix_bytes(7, 0, 80).tobytes() == ref
+    assert workloads.splitmix_bytes(7, 3, 50).tobytes() == ref[3:53]
+    assert workloads.splitmix_bytes(7, 0, 0).size == 0
+
+
+def test_packed_layout_alignment():
+    offs, total = workloads.packed_layout([1, 300, 0, 256, 5], align=256)
+    assert list(offs) == [0, 256, 768, 768, 1024]
+    assert total == 1029
+    assert all(int(o) % 256 == 0 for o in offs)
+
+
+def test_text_repo_matches_generator():
+    files = workloads.text_repo_files(1000)
+    assert files[os.path.join("texts", "file_0.txt")] == b"File content 0"
+    assert files[os.path.join("texts", "file_999.txt")] == b"File content 999"
+    assert files["README.md"].startswith(b"# Sample Repo\n\nGenerated 1000 text files")
+    assert len(files) == 1001
+
+
+def test_image_repo_tiffs_are_valid(tmp_path):
+    from PIL import Image
+
+    b = workloads.image_bytes_fast(3)
+    assert len(b) == 49_292  # 128x128x3 TIFF written by PIL
+    im = Image.open(io.BytesIO(b))
+    assert im.size == (128, 128) and im.mode == "RGB"
+    assert np.array_equal(np.asarray(im).reshape(-1), workloads.splitmix_bytes(0, 3 * 49152, 49152))
+    paths = workloads.write_image_repo_fast(str(tmp_path), 25, num_dirs=10)
+    assert len(paths) == 27
+    assert os.path.exists(tmp_path / "images" / "split_4" / "noise_image_14.tiff")
+    assert open(paths[14], "rb").read() == workloads.image_bytes_fast(14)
+
+
+def test_merkle_hash_formatting():
+    h = merkle.MerkleHash.from_str("2da4b9c5a75caad3688558138047f8a")
+    assert str(h) == "2da4b9c5a75caad3688558138047f8a"  # unpadded (31 chars)
+    assert h.node_db_prefix() == "2da/4b9c5a75caad3688558138047f8a"
+    assert h.version_dir() == "2d/a4b9c5a75caad3688558138047f8a"
+    assert h.to_le_bytes() == h.value.to_bytes(16, "little")
+    assert merkle.MerkleHash(0).__str__() == "0"
+    rng = np.random.default_rng(1)
+    for _ in range(200):  # merkle_hash.rs:155-190 round trip
+        v = int.from_bytes(rng.bytes(16), "little")
+        assert merkle.MerkleHash.from_str(str(merkle.MerkleHash(v))).value == v
+
+
+def test_num_vnodes_f32_semantics():
+    assert merkle.num_vnodes(0, 10_000) == 0
+    assert merkle.num_vnodes(1, 10_000) == 1
+    assert merkle.num_vnodes(10_000, 10_000) == 1
+    assert merkle.num_vnodes(10_001, 10_000) == 2
+    assert merkle.num_vnodes(1000, 6) == 167
+
+
+def test_parent_streams_bytes(golden):
+    streams = {s["name"]: bytes.fromhex(s["bytes_hex"]) for s in golden("streams.json")["streams"]}
+    assert merkle.vnode_stream("", []) == b"vnode"
+    v = merkle.vnode_stream("texts", [1, 2])
+    assert v == b"vnodetexts" + (1).to_bytes(16, "little") + (2).to_bytes(16, "little")
+    assert streams["vnode_root_empty"] == b"vnode"
+    d = merkle.dir_stream("a", [(5, [("x", 7)])])
+    assert d == b"dira" + (5).to_bytes(16, "little") + b"x" + (7).to_bytes(16, "little")
+    c = merkle.commit_stream(["abc", "def"], "m", "a", "e", 1)
+    assert c == b'commit["abc", "def"]mae' + (1).to_bytes(8, "little")
+    assert streams["commit"] == merkle.commit_stream(["abc", "def"], "add files", "ox", "ox@oxen.ai", 1_700_000_000)
+
+
+def test_metadata_json_matches_serde(golden):
+    from oxen_amd.hasher import metadata_json
+
+    r0 = golden("text_repo.json")["files"][0]
+    assert metadata_json({"text": {"num_lines": 1, "num_chars": 14}}) == r0["metadata_json"]
+    assert metadata_json(None) == "null"
