@@ -113,6 +113,7 @@ def main() -> None:
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm); gloo only to rehearse N>1 on one GPU")
     args = ap.parse_args()
 
     import torch
@@ -121,12 +122,15 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = max(1, torch.cuda.device_count())
+    dev = torch.device(f"cuda:{local_rank % ndev}")
+    torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
-    dev = torch.device(f"cuda:{local_rank}")
-    torch.cuda.set_device(dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
 
     from oxen_amd import _capi
     from oxen_amd import build as hb
@@ -152,7 +156,9 @@ def main() -> None:
     def step():
         da.hash(out)
         if world > 1:
-            return gather_digest_table(out, counts)
+            if args.backend == "nccl":
+                return gather_digest_table(out, counts)
+            return gather_digest_table(out.cpu(), counts)  # gloo rehearsal: host tables
         return out
 
     for _ in range(args.warmup):
@@ -200,6 +206,14 @@ def main() -> None:
         if world > 1:
             assert table.shape[0] == n_items * world
             assert np.array_equal(to_numpy_u64(table[:n_items]).reshape(-1, 2), digests)
+            # every rank's shard digests arrived: rank r's first item is regenerated and checked
+            from oracle import oracle
+            from oxen_amd.workloads import splitmix_bytes
+
+            full = to_numpy_u64(table).reshape(-1, 2)
+            for r in range(world):
+                want = oracle.xxh3_128(splitmix_bytes(args.seed + r, int(da.offsets_host[0]), item_len).tobytes())
+                assert (int(full[r * n_items, 0]), int(full[r * n_items, 1])) == want, r
         achieved = bytes_per_rank / kernel_s / 1e9
         tr = load_traffic(args.workload)
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -42,6 +42,7 @@ extern "C" {
 #define OXH_MODE_AUTO 0     /* one wave per buffer (K1), lane-per-item for short-only batches */
 #define OXH_MODE_WAVE 1     /* force K1: one 64-lane wave per buffer */
 #define OXH_MODE_LANE 2     /* force K1s: one lane per buffer (short items, parent-node streams) */
+#define OXH_MODE_WAVE_SHORT 3 /* K1 shaped for items of <= ~16 KiB (more resident waves) */
 
 typedef struct oxh_ctx oxh_ctx;
 
@@ -77,6 +78,12 @@ int oxh_chunk_digests_device(const void* d_buf, uint64_t len, uint64_t chunk, ui
  * parallel across the chip, then the serial scramble chain runs on one wave. `d_out` gets 2 u64. */
 int oxh_xxh3_128_large_device(oxh_ctx* ctx, const void* d_buf, uint64_t len, uint64_t* d_out,
                               void* stream);
+
+/* K1L over n large device-resident buffers (e.g. the 16 x 8 GiB files of the dedup experiment):
+ * d_bufs and lens are HOST arrays of n device pointers / lengths; d_out (device) gets 2n u64.
+ * Block sums run chip-wide per buffer, then up to 32 serial chains run concurrently in one launch. */
+int oxh_xxh3_128_large_batch_device(const void* const* d_bufs, const uint64_t* lens, uint64_t n,
+                                    uint64_t* d_out, void* stream);
 
 /* ---------------------------------------------------------------- host-resident entry points
  * These block until the digests are in host memory. */

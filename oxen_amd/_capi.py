@@ -22,6 +22,7 @@ OXH_ERR_NODEVICE = 5
 OXH_MODE_AUTO = 0
 OXH_MODE_WAVE = 1
 OXH_MODE_LANE = 2
+OXH_MODE_WAVE_SHORT = 3
 
 _u64 = ctypes.c_uint64
 _u64p = ctypes.POINTER(ctypes.c_uint64)
@@ -40,6 +41,7 @@ SIGNATURES = {
     "oxh_xxh3_128_batch_device": (_int, [_vp, _vp, _vp, _u64, _vp, _int, _vp]),
     "oxh_chunk_digests_device": (_int, [_vp, _u64, _u64, _vp, _vp]),
     "oxh_xxh3_128_large_device": (_int, [_vp, _vp, _u64, _vp, _vp]),
+    "oxh_xxh3_128_large_batch_device": (_int, [ctypes.POINTER(_vp), _u64p, _u64, _vp, _vp]),
     "oxh_hash_buffers": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64p, _u64, _u64p]),
     "oxh_hash_files": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64, _u64p, _u64p, _i32p]),
     "oxh_combined_hash_device": (_int, [_vp, _vp, _u64, _vp, _vp]),

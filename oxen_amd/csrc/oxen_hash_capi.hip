@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "../../include/oxen_hash.h"
+#include "xxh3_device.hpp"
 
 namespace oxh {
 template <bool DESC, int VARIANT>
@@ -35,8 +36,7 @@ __global__ void xxh3_lane_kernel(const uint8_t*, const uint64_t*, const uint64_t
 __global__ void xxh3_combined_kernel(const uint64_t*, const uint64_t*, uint64_t, uint64_t*);
 template <bool ALIGNED>
 __global__ void xxh3_blocksum_kernel(const uint8_t*, uint64_t, uint64_t*);
-template <bool ALIGNED>
-__global__ void xxh3_chain_kernel(const uint8_t*, uint64_t, const uint64_t*, uint64_t*);
+__global__ void xxh3_chain_kernel(ChainBatch);
 __global__ void fill_splitmix_kernel(uint64_t*, uint64_t, uint64_t);
 __global__ void fill_splitmix_tail_kernel(uint8_t*, uint64_t, uint64_t, uint64_t);
 }  // namespace oxh
@@ -85,17 +85,31 @@ WaveKernel wave_kernel_for(int variant) {
         case 8: return oxh::xxh3_wave_kernel<DESC, 8>;
         case 12: return oxh::xxh3_wave_kernel<DESC, 12>;
         case 64: return oxh::xxh3_wave_kernel<DESC, 64>;
+        case 72: return oxh::xxh3_wave_kernel<DESC, 72>;
         default: return oxh::xxh3_wave_kernel<DESC, 0>;
     }
 }
 
+// K1 register/pipeline shape by item size (measured): items of a few KiB want many
+// resident waves (2-round ring, keys in LDS: 77 VGPRs, 6 waves/SIMD, every load issued up front);
+// large items want 4 rounds in flight per wave (201 VGPRs, 2 waves/SIMD). An explicit
+// oxh_set_kernel_variant() overrides the choice.
+constexpr uint64_t kShortItemBytes = 16384;
+constexpr int kVariantShort = 72;  // Cfg: depth 2, keys in LDS
+
+int pick_variant(bool short_items) {
+    const int v = g_variant.load();
+    if (v != 0) return v;
+    return short_items ? kVariantShort : 0;
+}
+
 // K1 over a descriptor table: one 64-lane wave per item, 4 waves per 256-thread workgroup.
 int launch_wave(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens, uint64_t n, uint64_t* out,
-                hipStream_t st) {
+                hipStream_t st, bool short_items = false) {
     if (n == 0) return OXH_OK;
     const uint64_t blocks = (n + 3) / 4;
-    hipLaunchKernelGGL(wave_kernel_for<true>(g_variant.load()), dim3((unsigned)blocks), dim3(256), 0, st, arena, offs, lens, n,
-                       (uint64_t)0, (uint64_t)0, out);
+    hipLaunchKernelGGL(wave_kernel_for<true>(pick_variant(short_items)), dim3((unsigned)blocks), dim3(256), 0, st, arena, offs,
+                       lens, n, (uint64_t)0, (uint64_t)0, out);
     HIP_TRY(hipGetLastError());
     return OXH_OK;
 }
@@ -104,7 +118,7 @@ int launch_wave(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens
 int launch_chunks(const uint8_t* buf, uint64_t n, uint64_t chunk, uint64_t total, uint64_t* out, hipStream_t st) {
     if (n == 0) return OXH_OK;
     const uint64_t blocks = (n + 3) / 4;
-    hipLaunchKernelGGL(wave_kernel_for<false>(g_variant.load()), dim3((unsigned)blocks), dim3(256), 0, st, buf,
+    hipLaunchKernelGGL(wave_kernel_for<false>(pick_variant(chunk <= kShortItemBytes)), dim3((unsigned)blocks), dim3(256), 0, st, buf,
                        (const uint64_t*)nullptr, (const uint64_t*)nullptr, n, chunk, total, out);
     HIP_TRY(hipGetLastError());
     return OXH_OK;
@@ -218,28 +232,57 @@ struct oxh_ctx {
 
 namespace {
 
-// K1L on a device buffer (block sums + chain); small buffers fall back to one K1 wave.
-int large_device(oxh_ctx* c, const uint8_t* d_buf, uint64_t len, uint64_t* d_out, hipStream_t st) {
-    const uint64_t nb = len > 0 ? (len - 1) >> 10 : 0;
-    if (nb < 1024) return launch_chunks(d_buf, 1, len, len, d_out, st);  // one K1 wave below ~1 MiB
-    // block sums live in stream-ordered scratch, so concurrent calls on different streams never share it
+// K1L over n device buffers: block sums chip-wide (one launch per buffer; each fills the chip),
+// then the serial chains of up to kChainJobs buffers in one launch, one wave each, so the chains of
+// many large files run concurrently. Buffers below ~1 MiB take one K1 wave instead.
+int large_batch_device(const uint8_t* const* bufs, const uint64_t* lens, uint64_t n, uint64_t* d_out, hipStream_t st) {
+    uint64_t total_nb = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t nb = lens[i] > 0 ? (lens[i] - 1) >> 10 : 0;
+        if (nb >= 1024) total_nb += nb;
+    }
     uint64_t* sums = nullptr;
-    HIP_TRY(hipMallocAsync((void**)&sums, nb * 64, st));
-    const bool aligned = (reinterpret_cast<uintptr_t>(d_buf) & 15) == 0;
-    const uint64_t nwaves = (nb + 3) / 4, blocks = (nwaves + 3) / 4;
-    if (aligned)
-        hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, d_buf, nb, sums);
-    else
-        hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, d_buf, nb, sums);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(oxh::xxh3_chain_kernel<true>, dim3(1), dim3(64), 0, st, d_buf, len, sums, d_out);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipFreeAsync(sums, st));
+    if (total_nb) HIP_TRY(hipMallocAsync((void**)&sums, total_nb * 64, st));  // stream-ordered scratch
+    oxh::ChainBatch batch;
+    int nj = 0;
+    uint64_t off = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t len = lens[i];
+        const uint64_t nb = len > 0 ? (len - 1) >> 10 : 0;
+        if (nb < 1024) {
+            int rc = launch_chunks(bufs[i], 1, len, len, d_out + 2 * i, st);
+            if (rc) return rc;
+            continue;
+        }
+        const bool aligned = (reinterpret_cast<uintptr_t>(bufs[i]) & 15) == 0;
+        const uint64_t nwaves = (nb + 3) / 4, blocks = (nwaves + 3) / 4;
+        if (aligned)
+            hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, bufs[i], nb, sums + off);
+        else
+            hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, bufs[i], nb, sums + off);
+        HIP_TRY(hipGetLastError());
+        batch.job[nj++] = {bufs[i], len, sums + off, d_out + 2 * i};
+        off += nb * 8;
+        if (nj == oxh::kChainJobs) {
+            hipLaunchKernelGGL(oxh::xxh3_chain_kernel, dim3(nj), dim3(64), 0, st, batch);
+            HIP_TRY(hipGetLastError());
+            nj = 0;
+        }
+    }
+    if (nj) {
+        hipLaunchKernelGGL(oxh::xxh3_chain_kernel, dim3(nj), dim3(64), 0, st, batch);
+        HIP_TRY(hipGetLastError());
+    }
+    if (sums) HIP_TRY(hipFreeAsync(sums, st));
     return OXH_OK;
 }
 
+int large_device(oxh_ctx*, const uint8_t* d_buf, uint64_t len, uint64_t* d_out, hipStream_t st) {
+    return large_batch_device(&d_buf, &len, 1, d_out, st);
+}
+
 // One staged batch: items [0, cnt) already in h_stage[s] at h_desc offsets; launch and queue D2H.
-int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_only) {
+int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_only, bool short_items) {
     const uint64_t M = c->max_items;
     HIP_TRY(hipMemcpyAsync(c->d_stage[s], c->h_stage[s], bytes, hipMemcpyHostToDevice, c->copy_stream));
     HIP_TRY(hipMemcpyAsync(c->d_desc[s], c->h_desc[s], cnt * 8, hipMemcpyHostToDevice, c->copy_stream));
@@ -247,7 +290,8 @@ int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_
     HIP_TRY(hipEventRecord(c->ev_copied[s], c->copy_stream));
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[s], 0));
     int rc = any_short_only ? launch_lane(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->stream)
-                            : launch_wave(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->stream);
+                            : launch_wave(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->stream,
+                                          short_items);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(c->h_out[s], c->d_out[s], cnt * 16, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipEventRecord(c->ev_done[s], c->stream));
@@ -381,6 +425,7 @@ int oxh_xxh3_128_batch_device(const void* d_arena, const uint64_t* d_offsets, co
     const uint8_t* a = (const uint8_t*)d_arena;
     if (mode == OXH_MODE_LANE) return launch_lane(a, d_offsets, d_lens, n, d_out, st);
     if (mode == OXH_MODE_AUTO || mode == OXH_MODE_WAVE) return launch_wave(a, d_offsets, d_lens, n, d_out, st);
+    if (mode == OXH_MODE_WAVE_SHORT) return launch_wave(a, d_offsets, d_lens, n, d_out, st, true);
     return fail(OXH_ERR_INVALID, "unknown mode");
 }
 
@@ -396,6 +441,15 @@ int oxh_xxh3_128_large_device(oxh_ctx* c, const void* d_buf, uint64_t len, uint6
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t st = (hipStream_t)stream;  // NULL = the null stream, as for every device entry point
     return large_device(c, (const uint8_t*)d_buf, len, d_out, st);
+}
+
+int oxh_xxh3_128_large_batch_device(const void* const* d_bufs, const uint64_t* lens, uint64_t n, uint64_t* d_out,
+                                    void* stream) {
+    if (n == 0) return OXH_OK;
+    if (!d_bufs || !lens || !d_out) return fail(OXH_ERR_INVALID, "bad large-batch arguments");
+    for (uint64_t i = 0; i < n; ++i)
+        if (!d_bufs[i] && lens[i]) return fail(OXH_ERR_INVALID, "NULL buffer with nonzero length");
+    return large_batch_device((const uint8_t* const*)d_bufs, lens, n, d_out, (hipStream_t)stream);
 }
 
 int oxh_combined_hash_device(const uint64_t* d_content, const uint64_t* d_metadata, uint64_t n, uint64_t* d_out,
@@ -483,7 +537,8 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
         }
         double t2 = Trace::now();
         tr->fill += t2 - t1;
-        rc = submit_slot(c, s, off, batch.size(), short_only_lane && all_short);
+        rc = submit_slot(c, s, off, batch.size(), short_only_lane && all_short,
+                         off / std::max<uint64_t>(1, batch.size()) <= kShortItemBytes);
         if (rc) return rc;
         tr->submit += Trace::now() - t2;
         tr->batches++;

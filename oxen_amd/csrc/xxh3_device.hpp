@@ -80,6 +80,18 @@ __device__ __forceinline__ uint32_t ld32u(const uint8_t* p) { uint32_t v; __buil
 
 struct U128 { uint64_t lo, hi; };
 
+// K1L chain launch: one job (one large buffer) per wave, passed by value as kernel arguments.
+struct ChainJob {
+    const uint8_t* p;
+    uint64_t len;
+    const uint64_t* sums;  // 8 u64 block sums per scrambled block
+    uint64_t* out;         // 2 u64 (lo, hi)
+};
+constexpr int kChainJobs = 32;
+struct ChainBatch {
+    ChainJob job[kChainJobs];
+};
+
 // The 24 aligned secret words, for lane-dependent (runtime) indexing on the device.
 static __constant__ uint64_t kSecW[24] = {
     S64(0), S64(8), S64(16), S64(24), S64(32), S64(40), S64(48), S64(56),

@@ -196,76 +196,68 @@ __device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_
         return __builtin_amdgcn_make_buffer_rsrc((void*)(p + base), (short)0,
                                                  (int)(rem < 0x7FFFFFFFull ? rem : 0x7FFFFFFFull), kRsrcFlags);
     };
-    auto load_round = [&](uint64_t rr, bool live, uint4 (&dst)[4]) {
-        const __amdgpu_buffer_rsrc_t rsrc = window_rsrc(rr);
-        const uint32_t vo = live ? (uint32_t)(rr & 0x3FFFF) * 4096u + lane_off : kOOB;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) dst[j] = bload16<Cfg<VARIANT>::NT>(rsrc, vo + j * 256);
+    // Rounds 0 .. nr-1 are full (4 scrambled blocks); round nr is the partial final round: blocks
+    // 4nr .. nb-1 full, block nb with `ns` stripes. Stripe s = 4j + q of row g is live in round rr
+    // if rr < nr, or rr == nr and (b < nb or (b == nb and s < ns)) with b = 4nr + g.
+    const uint64_t ns = ((len - 1) - (nb << 10)) >> 6;
+    const uint64_t bfin = nr * 4 + g;
+    // branch-free (bitwise) so that no load ends up inside control flow
+    const bool fin_row_full = bfin < nb;
+    const bool fin_row_part = bfin == nb;
+    auto live_j = [&](uint64_t rr, int j) -> bool {
+        const bool in_part = fin_row_full | (fin_row_part & ((uint64_t)(4 * j + q) < ns));
+        return (rr < nr) | ((rr == nr) & in_part);
     };
-    auto fold4 = [&](const uint4 (&src)[4], int nfull) {
+    auto load_round = [&](uint64_t rr, uint4 (&dst)[4]) {
+        const __amdgpu_buffer_rsrc_t rsrc = window_rsrc(rr);
+        const uint32_t vo = (uint32_t)(rr & 0x3FFFF) * 4096u + lane_off;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dst[j] = bload16<Cfg<VARIANT>::NT>(rsrc, live_j(rr, j) ? vo + j * 256 : kOOB);
+    };
+    auto fold4 = [&](const uint4 (&src)[4], uint64_t rr, bool partial) {
         uint64_t s0 = 0, s1 = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             uint64_t k0, k1;
             keys(j, k0, k1);
-            accum16(src[j], k0, k1, s0, s1);
+            if (!partial || live_j(rr, j)) accum16(src[j], k0, k1, s0, s1);
         }
-        fold_round<Cfg<VARIANT>::BCAST>(s0, s1, a0, a1, sk0, sk1, nfull, lane);
+        fold_round<Cfg<VARIANT>::BCAST>(s0, s1, a0, a1, sk0, sk1, partial ? (int)(nb - nr * 4) : 4, lane);
     };
+    // the last stripe (at len - 64, secret offset 121) is fetched up front with the first rounds
+    const __amdgpu_buffer_rsrc_t rsrc_last =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(p + len - 64), (short)0, 64, kRsrcFlags);
+    const uint4 last = bload16<false>(rsrc_last, 16u * (uint32_t)k);
 
-    if (nr > 0) {
-        // Software pipeline with a static register ring: slot d holds round r + d; D rounds
-        // (4D dwordx4 per lane) are in flight when a round is folded.
+    {
+        // Software pipeline with a static register ring: slot d holds round r + d; the D rounds
+        // (4D dwordx4 per lane) and the last stripe are all issued before the first fold, so a
+        // short item (an 8 KiB chunk is 2 rounds) costs one memory round trip.
         constexpr int D = Cfg<VARIANT>::DEPTH;
         uint4 ring[D][4];
 #pragma unroll
-        for (int d = 0; d < D; ++d) load_round((uint64_t)d, (uint64_t)d < nr, ring[d]);
-        const uint64_t nmain = nr - nr % D;
-        for (uint64_t r = 0; r < nmain; r += D) {
+        for (int d = 0; d < D; ++d) load_round((uint64_t)d, ring[d]);
+        uint64_t r = 0;
+        for (; r + D <= nr; r += D) {  // every slot holds a full round
 #pragma unroll
             for (int d = 0; d < D; ++d) {
-                fold4(ring[d], 4);
-                load_round(r + d + D, r + d + D < nr, ring[d]);
+                fold4(ring[d], r + d, false);
+                load_round(r + d + D, ring[d]);
                 // keep slot d+1's arithmetic below this point: otherwise the scheduler hoists its
                 // data-only adds above the refill and hipcc has to drain every load (vmcnt(0))
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
-        // the last nr % D rounds are already in ring slots 0 .. nr % D - 1
+        // rounds r .. nr (at most D, the last one partial) are already in slots 0 .. nr - r
 #pragma unroll
-        for (int d = 0; d < D - 1; ++d)
-            if (nmain + d < nr) fold4(ring[d], 4);
-    }
-    // final round: (nb - 4nr) full blocks, then the partial block with `ns` stripes; lanes whose
-    // stripe lies past the data read nothing (offset out of the buffer's range)
-    {
-        const uint64_t b = nr * 4 + g;
-        const uint64_t ns = ((len - 1) - (nb << 10)) >> 6;
-        const __amdgpu_buffer_rsrc_t rsrc = window_rsrc(nr);
-        uint4 d[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint64_t s = 4 * j + q;
-            const bool live = b < nb || (b == nb && s < ns);
-            d[j] = bload16<false>(rsrc, live ? (uint32_t)(nr & 0x3FFFF) * 4096u + lane_off + j * 256 : kOOB);
+        for (int d = 0; d < D; ++d) {
+            if (r + d < nr) fold4(ring[d], r + d, false);
+            else if (r + d == nr) fold4(ring[d], r + d, true);
         }
-        // a dropped (zero) piece would still add mul(0 ^ key) -- mask the contribution instead
-        uint64_t s0 = 0, s1 = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint64_t s = 4 * j + q;
-            if (b < nb || (b == nb && s < ns)) {
-                uint64_t k0, k1;
-                keys(j, k0, k1);
-                accum16(d[j], k0, k1, s0, s1);
-            }
-        }
-        fold_round<Cfg<VARIANT>::BCAST>(s0, s1, a0, a1, sk0, sk1, (int)(nb - nr * 4), lane);
     }
     // last stripe, at len - 64, with the secret shifted to offset 121
     {
-        const uint8_t* ls = p + len - 64 + 16 * k;
-        const uint64_t w0 = ld64u(ls), w1 = ld64u(ls + 8);
+        const uint64_t w0 = ((uint64_t)last.y << 32) | last.x, w1 = ((uint64_t)last.w << 32) | last.z;
         const uint64_t k0 = w0 ^ kLastW[2 * k], k1 = w1 ^ kLastW[2 * k + 1];
         a0 += mul32x32(k0) + w1;
         a1 += mul32x32(k1) + w0;
@@ -389,14 +381,16 @@ __global__ __launch_bounds__(256) void xxh3_blocksum_kernel(const uint8_t* __res
     }
 }
 
-// K1L phase 2: the serial chain over nb block sums on one wave, then the tail and the merge.
-// Lanes 0..7 each own one accumulator; the block sums stream in GROUP steps at a time, with the
-// next group's loads in flight while the current group is chained.
-template <bool ALIGNED>
-__global__ __launch_bounds__(64) void xxh3_chain_kernel(const uint8_t* __restrict__ p, uint64_t len,
-                                                        const uint64_t* __restrict__ sums,
-                                                        uint64_t* __restrict__ out) {
+// K1L phase 2: the serial chain over nb block sums, then the tail and the merge -- one wave per
+// buffer, up to kChainJobs buffers per launch (so the chains of many large files run concurrently on
+// different CUs). Lanes 0..7 each own one accumulator; block sums stream in GROUP steps at a time
+// with the next group's loads in flight while the current group is chained.
+__global__ __launch_bounds__(64) void xxh3_chain_kernel(ChainBatch batch) {
     constexpr int GROUP = 16;
+    const ChainJob job = batch.job[blockIdx.x];
+    const uint8_t* __restrict__ p = job.p;
+    const uint64_t len = job.len;
+    const uint64_t* __restrict__ sums = job.sums;
     const int lane = threadIdx.x;
     const int i = lane & 7;
     const uint64_t nb = (len - 1) >> 10;
@@ -454,8 +448,8 @@ __global__ __launch_bounds__(64) void xxh3_chain_kernel(const uint8_t* __restric
         mhi += oh;
     }
     if (lane == 0) {
-        out[0] = avalanche_xxh3(len * P64_1 + mlo);
-        out[1] = avalanche_xxh3(~(len * P64_2) + mhi);
+        job.out[0] = avalanche_xxh3(len * P64_1 + mlo);
+        job.out[1] = avalanche_xxh3(~(len * P64_2) + mhi);
     }
 }
 
@@ -493,8 +487,9 @@ template __global__ void xxh3_wave_kernel<true, 12>(const uint8_t*, const uint64
 template __global__ void xxh3_wave_kernel<false, 12>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 template __global__ void xxh3_wave_kernel<true, 64>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 template __global__ void xxh3_wave_kernel<false, 64>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<true, 72>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<false, 72>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 template __global__ void xxh3_blocksum_kernel<true>(const uint8_t*, uint64_t, uint64_t*);
 template __global__ void xxh3_blocksum_kernel<false>(const uint8_t*, uint64_t, uint64_t*);
-template __global__ void xxh3_chain_kernel<true>(const uint8_t*, uint64_t, const uint64_t*, uint64_t*);
 
 }  // namespace oxh

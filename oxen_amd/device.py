@@ -67,6 +67,23 @@ def large_digest_device(ctx: _capi.Context, buf: torch.Tensor, nbytes: Optional[
     return out
 
 
+def large_digests_device(bufs: list, nbytes: Optional[list] = None, out: Optional[torch.Tensor] = None,
+                         stream=None) -> torch.Tensor:
+    """K1L whole-buffer digests of several large device buffers (chains run concurrently)."""
+    import ctypes
+
+    _require_cuda(*bufs)
+    n = len(bufs)
+    nbytes = [b.numel() * b.element_size() for b in bufs] if nbytes is None else list(nbytes)
+    if out is None:
+        out = torch.empty((n, 2), dtype=torch.int64, device=bufs[0].device)
+    ptrs = (ctypes.c_void_p * n)(*[b.data_ptr() for b in bufs])
+    lens = np.array(nbytes, dtype=np.uint64)
+    _capi.check(_capi.lib().oxh_xxh3_128_large_batch_device(ptrs, lens.ctypes.data_as(_capi._u64p), n, out.data_ptr(),
+                                                            _stream(stream)), "oxh_xxh3_128_large_batch_device")
+    return out
+
+
 def combined_hash_device(content: torch.Tensor, metadata: torch.Tensor, out: Optional[torch.Tensor] = None,
                          stream=None) -> torch.Tensor:
     _require_cuda(content, metadata)

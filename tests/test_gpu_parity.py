@@ -39,10 +39,10 @@ def _mismatch(got, want, lens):
     return [int(lens[i]) for i in bad[:20]]
 
 
-VARIANTS = [0, 1, 2, 4, 8, 12, 64]  # K1 variants (xxh3_kernels.hip Cfg); 0 is the shipped path
+VARIANTS = [0, 1, 2, 4, 8, 12, 64, 72]  # K1 variants (xxh3_kernels.hip Cfg); 0 is the shipped path
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
 @pytest.mark.parametrize("variant", VARIANTS)
 def test_every_length_unaligned(cuda, golden, mode, variant):
     """Every length 0..2048 + boundaries up to 1 MiB+1, at the golden (mostly unaligned) offsets."""
@@ -189,6 +189,24 @@ def test_large_single_buffer_k1l(cuda, ctx, oracle_lib, n):
         torch.cuda.synchronize()
         want = oracle_lib.xxh3_128(view.cpu().numpy().tobytes())
         assert (int(got[0, 0]), int(got[0, 1])) == want, (n, start)
+
+
+def test_large_batch_k1l(cuda, oracle_lib):
+    """Several large buffers in one call (concurrent chains), mixed with small and misaligned ones."""
+    import torch
+
+    from oxen_amd.device import fill_splitmix, large_digests_device
+
+    sizes = [(3 << 20) + 5, 1000, (1 << 20) + 64, 0, (9 << 20) + 1, 300, (2 << 20) - 1]
+    bufs = []
+    for i, n in enumerate(sizes):
+        b = torch.empty(n + 16, dtype=torch.uint8, device=cuda)
+        fill_splitmix(b, 77 + i)
+        bufs.append(b[i % 3:i % 3 + n])  # misaligned starts for some
+    got = _u64(large_digests_device(bufs, sizes))
+    torch.cuda.synchronize()
+    for i, (b, n) in enumerate(zip(bufs, sizes)):
+        assert (int(got[i, 0]), int(got[i, 1])) == oracle_lib.xxh3_128(b.cpu().numpy().tobytes()), i
 
 
 def test_combined_hash_device(cuda, golden):

@@ -75,7 +75,7 @@ def main():
         return f
 
     ref = None
-    for v in (0, 1, 2, 4, 8, 12, 64):
+    for v in (0, 1, 2, 4, 8, 12, 64, 72):
         variants[f"k1_xxh3_v{v}"] = k1(v)
         k1(v)()
         torch.cuda.synchronize()
