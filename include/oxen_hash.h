@@ -99,6 +99,17 @@ int oxh_hash_buffers(oxh_ctx* ctx, const uint8_t* const* bufs, const uint64_t* l
 int oxh_hash_files(oxh_ctx* ctx, const char* const* paths, uint64_t n, uint64_t* out,
                    uint64_t* sizes, int32_t* status);
 
+/* Text-metadata fusion (K1T): the same digests as oxh_hash_files plus, per file, the counts liboxen's
+ * text metadata reads in a second full pass (repositories/metadata/text.rs:11-20 ->
+ * util/fs.rs:217-263): counts[2i] = num_lines (1 + number of b'\n'), counts[2i+1] = num_chars
+ * (bytes that are not UTF-8 continuation bytes, bytecount::num_chars). Computed in the hash's
+ * HBM pass; the caller uses them only for files it classifies as text. */
+int oxh_hash_files_text(oxh_ctx* ctx, const char* const* paths, uint64_t n, uint64_t* out,
+                        uint64_t* sizes, int32_t* status, uint64_t* counts);
+/* Device-resident K1T: as oxh_xxh3_128_batch_device plus d_counts (2n u64: num_lines, num_chars). */
+int oxh_xxh3_128_text_batch_device(const void* d_arena, const uint64_t* d_offsets, const uint64_t* d_lens,
+                                   uint64_t n, uint64_t* d_out, uint64_t* d_counts, void* stream);
+
 /* ---------------------------------------------------------------- K2: merkle parent nodes */
 /* get_combined_hash (hasher.rs:67-80) x n on the device:
  * XXH3-128(content.to_le_bytes() || metadata.to_le_bytes()), inputs as (lo, hi) pairs. */

@@ -38,6 +38,9 @@ template <bool ALIGNED>
 __global__ void xxh3_blocksum_kernel(const uint8_t*, uint64_t, uint64_t*);
 __global__ void xxh3_chain_kernel(ChainBatch);
 __global__ void fill_splitmix_kernel(uint64_t*, uint64_t, uint64_t);
+template <int VARIANT>
+__global__ void xxh3_text_wave_kernel(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t*, uint64_t*);
+__global__ void text_count_kernel(const uint8_t*, uint64_t, unsigned long long*);
 __global__ void fill_splitmix_tail_kernel(uint8_t*, uint64_t, uint64_t, uint64_t);
 }  // namespace oxh
 
@@ -110,6 +113,21 @@ int launch_wave(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens
     const uint64_t blocks = (n + 3) / 4;
     hipLaunchKernelGGL(wave_kernel_for<true>(pick_variant(short_items)), dim3((unsigned)blocks), dim3(256), 0, st, arena, offs,
                        lens, n, (uint64_t)0, (uint64_t)0, out);
+    HIP_TRY(hipGetLastError());
+    return OXH_OK;
+}
+
+// K1T: K1 plus text counts in the same pass.
+int launch_text(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens, uint64_t n, uint64_t* out,
+                uint64_t* counts, hipStream_t st, bool short_items = false) {
+    if (n == 0) return OXH_OK;
+    const uint64_t blocks = (n + 3) / 4;
+    if (pick_variant(short_items) == kVariantShort)
+        hipLaunchKernelGGL(oxh::xxh3_text_wave_kernel<kVariantShort>, dim3((unsigned)blocks), dim3(256), 0, st, arena, offs, lens,
+                           n, out, counts);
+    else
+        hipLaunchKernelGGL(oxh::xxh3_text_wave_kernel<0>, dim3((unsigned)blocks), dim3(256), 0, st, arena, offs, lens, n, out,
+                           counts);
     HIP_TRY(hipGetLastError());
     return OXH_OK;
 }
@@ -225,6 +243,8 @@ struct oxh_ctx {
     uint64_t* d_desc[NSLOT] = {};
     uint64_t* h_out[NSLOT] = {};
     uint64_t* d_out[NSLOT] = {};
+    uint64_t* h_cnt[NSLOT] = {};  // text counts (num_lines, num_chars) per item, K1T
+    uint64_t* d_cnt[NSLOT] = {};
     hipEvent_t ev_copied[NSLOT] = {}, ev_done[NSLOT] = {};
     Pool* pool = nullptr;
     std::mutex mu;
@@ -282,18 +302,21 @@ int large_device(oxh_ctx*, const uint8_t* d_buf, uint64_t len, uint64_t* d_out, 
 }
 
 // One staged batch: items [0, cnt) already in h_stage[s] at h_desc offsets; launch and queue D2H.
-int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_only, bool short_items) {
+int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_only, bool short_items, bool text) {
     const uint64_t M = c->max_items;
     HIP_TRY(hipMemcpyAsync(c->d_stage[s], c->h_stage[s], bytes, hipMemcpyHostToDevice, c->copy_stream));
     HIP_TRY(hipMemcpyAsync(c->d_desc[s], c->h_desc[s], cnt * 8, hipMemcpyHostToDevice, c->copy_stream));
     HIP_TRY(hipMemcpyAsync(c->d_desc[s] + M, c->h_desc[s] + M, cnt * 8, hipMemcpyHostToDevice, c->copy_stream));
     HIP_TRY(hipEventRecord(c->ev_copied[s], c->copy_stream));
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[s], 0));
-    int rc = any_short_only ? launch_lane(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->stream)
-                            : launch_wave(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->stream,
-                                          short_items);
+    int rc = text ? launch_text(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->d_cnt[s], c->stream,
+                                short_items)
+             : any_short_only ? launch_lane(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->stream)
+                              : launch_wave(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->stream,
+                                            short_items);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(c->h_out[s], c->d_out[s], cnt * 16, hipMemcpyDeviceToHost, c->stream));
+    if (text) HIP_TRY(hipMemcpyAsync(c->h_cnt[s], c->d_cnt[s], cnt * 16, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipEventRecord(c->ev_done[s], c->stream));
     return OXH_OK;
 }
@@ -313,20 +336,26 @@ struct Pending {
     std::vector<uint64_t> ids;  // caller indices of the staged items
 };
 
-int drain_slot(oxh_ctx* c, int s, Pending& p, uint64_t* out) {
+int drain_slot(oxh_ctx* c, int s, Pending& p, uint64_t* out, uint64_t* counts = nullptr) {
     if (!p.busy) return OXH_OK;
     HIP_TRY(hipEventSynchronize(c->ev_done[s]));
     for (size_t j = 0; j < p.ids.size(); ++j) {
         out[2 * p.ids[j]] = c->h_out[s][2 * j];
         out[2 * p.ids[j] + 1] = c->h_out[s][2 * j + 1];
     }
+    if (counts)
+        for (size_t j = 0; j < p.ids.size(); ++j) {
+            counts[2 * p.ids[j]] = c->h_cnt[s][2 * j];
+            counts[2 * p.ids[j] + 1] = c->h_cnt[s][2 * j + 1];
+        }
     p.busy = false;
     p.ids.clear();
     return OXH_OK;
 }
 
-// Hash one oversize host item (> a staging slot) through a temporary device buffer.
-int oversize_item(oxh_ctx* c, const uint8_t* src, uint64_t len, uint64_t* out2) {
+// Hash one oversize host item (> a staging slot) through a temporary device buffer; with `cnt2`,
+// also its text counts (num_lines, num_chars).
+int oversize_item(oxh_ctx* c, const uint8_t* src, uint64_t len, uint64_t* out2, uint64_t* cnt2 = nullptr) {
     uint8_t* d = nullptr;
     if (hipMalloc(&d, len) != hipSuccess) return fail(OXH_ERR_NOMEM, "oversize hipMalloc failed");
     int rc = OXH_OK;
@@ -337,12 +366,26 @@ int oversize_item(oxh_ctx* c, const uint8_t* src, uint64_t len, uint64_t* out2) 
         if (hipMemcpy(d + off, c->h_stage[0], piece, hipMemcpyHostToDevice) != hipSuccess) rc = fail(OXH_ERR_HIP, "oversize H2D failed");
     }
     if (rc == OXH_OK) rc = large_device(c, d, len, c->d_out[0], c->stream);
+    if (rc == OXH_OK && cnt2) {
+        if (hipMemsetAsync(c->d_cnt[0], 0, 16, c->stream) != hipSuccess) rc = fail(OXH_ERR_HIP, "memset counts");
+        if (rc == OXH_OK) {
+            hipLaunchKernelGGL(oxh::text_count_kernel, dim3(2048), dim3(256), 0, c->stream, d, len,
+                               (unsigned long long*)c->d_cnt[0]);
+            if (hipGetLastError() != hipSuccess) rc = fail(OXH_ERR_HIP, "text_count_kernel launch");
+        }
+        if (rc == OXH_OK && hipMemcpyAsync(c->h_cnt[0], c->d_cnt[0], 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+            rc = fail(OXH_ERR_HIP, "oversize counts D2H failed");
+    }
     if (rc == OXH_OK && hipMemcpyAsync(c->h_out[0], c->d_out[0], 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
         rc = fail(OXH_ERR_HIP, "oversize D2H failed");
     if (rc == OXH_OK && hipStreamSynchronize(c->stream) != hipSuccess) rc = fail(OXH_ERR_HIP, "oversize sync failed");
     if (rc == OXH_OK) {
         out2[0] = c->h_out[0][0];
         out2[1] = c->h_out[0][1];
+        if (cnt2) {
+            cnt2[0] = 1 + c->h_cnt[0][0];
+            cnt2[1] = len - c->h_cnt[0][1];
+        }
     }
     (void)hipFree(d);
     return rc;
@@ -385,6 +428,8 @@ int oxh_ctx_create(int device, uint64_t staging_bytes, oxh_ctx** out) {
         if (hipMalloc(&c->d_desc[s], c->max_items * 16) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "device desc");
         if (hipHostMalloc(&c->h_out[s], c->max_items * 16, hipHostMallocDefault) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "pinned out");
         if (hipMalloc(&c->d_out[s], c->max_items * 16) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "device out");
+        if (hipHostMalloc(&c->h_cnt[s], c->max_items * 16, hipHostMallocDefault) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "pinned counts");
+        if (hipMalloc(&c->d_cnt[s], c->max_items * 16) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "device counts");
         if (hipEventCreateWithFlags(&c->ev_copied[s], hipEventDisableTiming) != hipSuccess) return cleanup(OXH_ERR_HIP, "event");
         if (hipEventCreateWithFlags(&c->ev_done[s], hipEventDisableTiming) != hipSuccess) return cleanup(OXH_ERR_HIP, "event");
     }
@@ -405,6 +450,8 @@ int oxh_ctx_destroy(oxh_ctx* c) {
         if (c->d_desc[s]) (void)hipFree(c->d_desc[s]);
         if (c->h_out[s]) (void)hipHostFree(c->h_out[s]);
         if (c->d_out[s]) (void)hipFree(c->d_out[s]);
+        if (c->h_cnt[s]) (void)hipHostFree(c->h_cnt[s]);
+        if (c->d_cnt[s]) (void)hipFree(c->d_cnt[s]);
         if (c->ev_copied[s]) (void)hipEventDestroy(c->ev_copied[s]);
         if (c->ev_done[s]) (void)hipEventDestroy(c->ev_done[s]);
     }
@@ -466,7 +513,7 @@ int oxh_combined_hash_device(const uint64_t* d_content, const uint64_t* d_metada
 // `reader(i, dst)` directly into the pinned slot; lens[i] is known up front.
 static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
                            const std::function<int(uint64_t, uint8_t*)>& fill, uint64_t* out, int32_t* status,
-                           bool short_only_lane, Trace* tr = nullptr) {
+                           bool short_only_lane, Trace* tr = nullptr, uint64_t* counts = nullptr) {
     Trace local;
     if (!tr) tr = &local;
     Pending pend[NSLOT];
@@ -483,14 +530,14 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
                 if (!batch.empty()) break;
                 // oversize item: read it fully into a host buffer, then stream through slot 0
                 for (int s = 0; s < NSLOT; ++s) {
-                    int rc = drain_slot(c, s, pend[s], out);
+                    int rc = drain_slot(c, s, pend[s], out, counts);
                     if (rc) return rc;
                 }
                 std::vector<uint8_t> tmp(L);
                 int st = fill(i, tmp.data());
                 if (status) status[i] = st;
                 if (st == OXH_OK) {
-                    int rc = oversize_item(c, tmp.data(), L, out + 2 * i);
+                    int rc = oversize_item(c, tmp.data(), L, out + 2 * i, counts ? counts + 2 * i : nullptr);
                     if (rc) return rc;
                 } else {
                     out[2 * i] = out[2 * i + 1] = 0;
@@ -507,7 +554,7 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
         const int s = slot;
         slot = (slot + 1) % NSLOT;
         double t0 = Trace::now();
-        int rc = drain_slot(c, s, pend[s], out);
+        int rc = drain_slot(c, s, pend[s], out, counts);
         if (rc) return rc;
         double t1 = Trace::now();
         tr->drain += t1 - t0;
@@ -538,7 +585,7 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
         double t2 = Trace::now();
         tr->fill += t2 - t1;
         rc = submit_slot(c, s, off, batch.size(), short_only_lane && all_short,
-                         off / std::max<uint64_t>(1, batch.size()) <= kShortItemBytes);
+                         off / std::max<uint64_t>(1, batch.size()) <= kShortItemBytes, counts != nullptr);
         if (rc) return rc;
         tr->submit += Trace::now() - t2;
         tr->batches++;
@@ -547,7 +594,7 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
     }
     double t3 = Trace::now();
     for (int s = 0; s < NSLOT; ++s) {
-        int rc = drain_slot(c, s, pend[s], out);
+        int rc = drain_slot(c, s, pend[s], out, counts);
         if (rc) return rc;
     }
     tr->drain += Trace::now() - t3;
@@ -556,7 +603,10 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
                 (unsigned long long)n, tr->batches, tr->stat, tr->fill, tr->drain, tr->submit, c->pool->size());
     if (status)
         for (uint64_t k = 0; k < n; ++k)
-            if (status[k] != OXH_OK) out[2 * k] = out[2 * k + 1] = 0;
+            if (status[k] != OXH_OK) {
+                out[2 * k] = out[2 * k + 1] = 0;
+                if (counts) counts[2 * k] = counts[2 * k + 1] = 0;
+            }
     return OXH_OK;
 }
 
@@ -597,7 +647,8 @@ static int read_whole(const char* path, uint8_t* dst, uint64_t len) {
     return OXH_OK;
 }
 
-int oxh_hash_files(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* sizes, int32_t* status) {
+static int hash_files_impl(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* sizes, int32_t* status,
+                           uint64_t* counts) {
     if (!c || (n && (!paths || !out))) return fail(OXH_ERR_INVALID, "bad arguments");
     std::lock_guard<std::mutex> g(c->mu);
     HIP_TRY(hipSetDevice(c->device));
@@ -622,13 +673,30 @@ int oxh_hash_files(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* o
     int rc = hash_host_items(c, n, lens.data(), [&](uint64_t i, uint8_t* dst) {
         if (st[i] != OXH_OK) return (int)st[i];
         return read_whole(paths[i], dst, lens[i]);
-    }, out, st2.data(), false, &tr);
+    }, out, st2.data(), false, &tr, counts);
     if (rc) return rc;
     for (uint64_t i = 0; i < n; ++i) {
         if (sizes) sizes[i] = lens[i];
         if (status) status[i] = st2[i];
     }
     return OXH_OK;
+}
+
+int oxh_hash_files(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* sizes, int32_t* status) {
+    return hash_files_impl(c, paths, n, out, sizes, status, nullptr);
+}
+
+int oxh_hash_files_text(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* sizes, int32_t* status,
+                        uint64_t* counts) {
+    if (n && !counts) return fail(OXH_ERR_INVALID, "counts is NULL");
+    return hash_files_impl(c, paths, n, out, sizes, status, counts);
+}
+
+int oxh_xxh3_128_text_batch_device(const void* d_arena, const uint64_t* d_offsets, const uint64_t* d_lens, uint64_t n,
+                                   uint64_t* d_out, uint64_t* d_counts, void* stream) {
+    if (n == 0) return OXH_OK;
+    if (!d_arena || !d_offsets || !d_lens || !d_out || !d_counts) return fail(OXH_ERR_INVALID, "NULL device pointer");
+    return launch_text((const uint8_t*)d_arena, d_offsets, d_lens, n, d_out, d_counts, (hipStream_t)stream);
 }
 
 int oxh_fill_splitmix(void* d_buf, uint64_t nbytes, uint64_t seed, void* stream) {

@@ -127,6 +127,22 @@ __device__ __forceinline__ void accum16(const uint4 d, uint64_t key0, uint64_t k
     s1 += mul32x32(k1) + w0;  // acc[2k+1] += lo*hi of its keyed word, plus word 2k
 }
 
+// Text metadata counts fused into the hash pass (repositories/metadata/text.rs:11-20 ->
+// util/fs.rs:217-263): newlines (num_lines = 1 + count) and UTF-8 continuation bytes
+// (num_chars = len - count, bytecount::num_chars). SWAR over each dword.
+__device__ __forceinline__ uint32_t count_nl32(uint32_t w) {
+    const uint32_t x = w ^ 0x0A0A0A0Au;                                // newline bytes become 0
+    const uint32_t t = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;          // bit 7 set in non-zero bytes
+    return (uint32_t)__builtin_popcount(~t & 0x80808080u);
+}
+__device__ __forceinline__ uint32_t count_cont32(uint32_t w) {
+    return (uint32_t)__builtin_popcount(w & ~(w << 1) & 0x80808080u);  // bytes 10xxxxxx
+}
+__device__ __forceinline__ void count16(const uint4 d, uint32_t& nl, uint32_t& cont) {
+    nl += count_nl32(d.x) + count_nl32(d.y) + count_nl32(d.z) + count_nl32(d.w);
+    cont += count_cont32(d.x) + count_cont32(d.y) + count_cont32(d.z) + count_cont32(d.w);
+}
+
 // Fold a round: in-row stripe reduction, cross-row broadcast, 4 chain steps.
 // nfull: how many of the 4 blocks are full (scrambled); block nfull (if < 4) is the partial one.
 template <int VARIANT>
@@ -167,10 +183,12 @@ __device__ __forceinline__ uint4 bload16(__amdgpu_buffer_rsrc_t rsrc, uint32_t v
 // The long path (len > 240) for one buffer, executed by one full wave. Writes out[0..1] from lane 0.
 // All input loads are raw buffer loads (gfx950 supports unaligned buffer access, so any start offset
 // is fine); the descriptor is re-based every 1 GiB so 32-bit offsets cover buffers of any length.
-template <int VARIANT>
+template <int VARIANT, bool TEXT>
 __device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_t len,
-                                          uint64_t* __restrict__ out, int lane, const uint64_t* lds_sec) {
+                                          uint64_t* __restrict__ out, int lane, const uint64_t* lds_sec,
+                                          uint64_t* __restrict__ counts) {
     const int g = lane >> 4, q = (lane >> 2) & 3, k = lane & 3;
+    uint32_t n_nl = 0, n_cont = 0;  // TEXT only
     // stripe keys: secret words (4j + q + 2k, +1)
     auto keys = [&](int j, uint64_t& k0, uint64_t& k1) {
         int idx = 4 * j + q + 2 * k;
@@ -220,7 +238,10 @@ __device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_
         for (int j = 0; j < 4; ++j) {
             uint64_t k0, k1;
             keys(j, k0, k1);
-            if (!partial || live_j(rr, j)) accum16(src[j], k0, k1, s0, s1);
+            if (!partial || live_j(rr, j)) {
+                accum16(src[j], k0, k1, s0, s1);
+                if constexpr (TEXT) count16(src[j], n_nl, n_cont);
+            }
         }
         fold_round<Cfg<VARIANT>::BCAST>(s0, s1, a0, a1, sk0, sk1, partial ? (int)(nb - nr * 4) : 4, lane);
     };
@@ -262,6 +283,40 @@ __device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_
         a0 += mul32x32(k0) + w1;
         a1 += mul32x32(k1) + w0;
     }
+    if constexpr (TEXT) {
+        // bytes [E, len) not covered by the stripes above come from the last stripe, which always
+        // spans them (len - E is 1..64); `last` depends only on k, so only lanes 0..3 count it
+        const uint64_t E = (nb << 10) + (ns << 6);
+        const uint64_t p0 = len - 64 + 16 * (uint64_t)k;
+        const uint32_t skip = E > p0 ? (uint32_t)(E - p0 < 16 ? E - p0 : 16) : 0u;
+        const uint32_t w[4] = {last.x, last.y, last.z, last.w};
+#ifdef OXH_DEBUG_LANES
+        const uint32_t dbg_ring = n_nl;
+#endif
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const int sd = (int)skip - 4 * d;
+            const uint32_t m = sd <= 0 ? 0xFFFFFFFFu : (sd >= 4 ? 0u : (0xFFFFFFFFu << (8 * sd)));
+            if (lane < 4) {
+                n_nl += count_nl32(w[d] & m);
+                n_cont += count_cont32(w[d] & m);
+            }
+        }
+#ifdef OXH_DEBUG_LANES
+        counts[2 + 3 * lane] = dbg_ring;
+        counts[3 + 3 * lane] = n_nl;
+        counts[4 + 3 * lane] = skip;
+#endif
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            n_nl += (uint32_t)__shfl_xor((int)n_nl, off, 64);
+            n_cont += (uint32_t)__shfl_xor((int)n_cont, off, 64);
+        }
+        if (lane == 0) {
+            counts[0] = 1 + (uint64_t)n_nl;
+            counts[1] = len - (uint64_t)n_cont;
+        }
+    }
     // merge: lane k contributes mix2Accs for accumulator pair k; sum over the quad
     uint64_t mlo = mul_fold64(a0 ^ kMrgLo[2 * k], a1 ^ kMrgLo[2 * k + 1]);
     uint64_t mhi = mul_fold64(a0 ^ kMrgHi[2 * k], a1 ^ kMrgHi[2 * k + 1]);
@@ -276,12 +331,11 @@ __device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_
 }
 
 // K1: one wave per item. DESC = descriptor table (offsets/lens); otherwise fixed-size chunks.
-template <bool DESC, int VARIANT>
-__global__ __launch_bounds__(256) void xxh3_wave_kernel(const uint8_t* __restrict__ arena,
-                                                        const uint64_t* __restrict__ offsets,
-                                                        const uint64_t* __restrict__ lens, uint64_t n,
-                                                        uint64_t chunk, uint64_t total,
-                                                        uint64_t* __restrict__ out) {
+// TEXT: also write (num_lines, num_chars) per item to `counts` (K1T, text metadata fused).
+template <bool DESC, int VARIANT, bool TEXT>
+__device__ __forceinline__ void wave_item(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offsets,
+                                          const uint64_t* __restrict__ lens, uint64_t n, uint64_t chunk,
+                                          uint64_t total, uint64_t* __restrict__ out, uint64_t* __restrict__ counts) {
     __shared__ uint64_t lds_sec[24];
     if constexpr (Cfg<VARIANT>::KEYS_LDS) {
         if (threadIdx.x < 24) lds_sec[threadIdx.x] = kSecW[threadIdx.x];
@@ -311,10 +365,38 @@ __global__ __launch_bounds__(256) void xxh3_wave_kernel(const uint8_t* __restric
             const U128 h = xxh3_lane_short(p, len);
             o[0] = h.lo;
             o[1] = h.hi;
+            if constexpr (TEXT) {
+                uint32_t nl = 0, cont = 0;
+                for (uint64_t b = 0; b < len; ++b) {
+                    nl += p[b] == 0x0A;
+                    cont += (p[b] & 0xC0) == 0x80;
+                }
+                counts[2 * item] = 1 + (uint64_t)nl;
+                counts[2 * item + 1] = len - (uint64_t)cont;
+            }
         }
         return;
     }
-    wave_long<VARIANT>(p, len, o, lane, lds_sec);
+    wave_long<VARIANT, TEXT>(p, len, o, lane, lds_sec, TEXT ? counts + 2 * item : nullptr);
+}
+
+template <bool DESC, int VARIANT>
+__global__ __launch_bounds__(256) void xxh3_wave_kernel(const uint8_t* __restrict__ arena,
+                                                        const uint64_t* __restrict__ offsets,
+                                                        const uint64_t* __restrict__ lens, uint64_t n,
+                                                        uint64_t chunk, uint64_t total,
+                                                        uint64_t* __restrict__ out) {
+    wave_item<DESC, VARIANT, false>(arena, offsets, lens, n, chunk, total, out, nullptr);
+}
+
+// K1T: K1 + text metadata counts in the same HBM pass (descriptor tables only).
+template <int VARIANT>
+__global__ __launch_bounds__(256) void xxh3_text_wave_kernel(const uint8_t* __restrict__ arena,
+                                                             const uint64_t* __restrict__ offsets,
+                                                             const uint64_t* __restrict__ lens, uint64_t n,
+                                                             uint64_t* __restrict__ out,
+                                                             uint64_t* __restrict__ counts) {
+    wave_item<true, VARIANT, true>(arena, offsets, lens, n, 0, 0, out, counts);
 }
 
 // K1s: one lane per item (any length; intended for short items).
@@ -386,7 +468,7 @@ __global__ __launch_bounds__(256) void xxh3_blocksum_kernel(const uint8_t* __res
 // different CUs). Lanes 0..7 each own one accumulator; block sums stream in GROUP steps at a time
 // with the next group's loads in flight while the current group is chained.
 __global__ __launch_bounds__(64) void xxh3_chain_kernel(ChainBatch batch) {
-    constexpr int GROUP = 16;
+    constexpr int GROUP = 128;
     const ChainJob job = batch.job[blockIdx.x];
     const uint8_t* __restrict__ p = job.p;
     const uint64_t len = job.len;
@@ -394,27 +476,47 @@ __global__ __launch_bounds__(64) void xxh3_chain_kernel(ChainBatch batch) {
     const int lane = threadIdx.x;
     const int i = lane & 7;
     const uint64_t nb = (len - 1) >> 10;
-    uint64_t acc = kInitW[i];
+    // The chain acc <- scramble(acc + S_b) is carried as x = acc + S_b in 32-bit halves so that the
+    // critical path per step is shift -> xor -> v_mad_u64_u32 (which also adds S_{b+1}) -> add:
+    //   y = x ^ (x >> 47) ^ key;  x' = y * P32_1 + S_{b+1}
+    //   lo(x') = lo(yl * P + S), hi(x') = hi(yl * P + S) + yh * P   (yh * P off the critical path)
     const uint64_t sk = kSecW[16 + i];
-    uint64_t b = 0;
-    if (nb >= GROUP) {
-        uint64_t cur[GROUP];
+    const uint32_t kl = (uint32_t)sk, kh = (uint32_t)(sk >> 32);
+    uint64_t acc = kInitW[i];
+    auto step = [&](uint32_t& xl, uint32_t& xh, uint64_t s_next) {
+        const uint32_t yl = (xl ^ kl) ^ (xh >> 15);
+        const uint32_t yh = xh ^ kh;
+        uint32_t t = yh * P32_1;  // v_mul_lo_u32, in parallel with the mad below
+        asm("" : "+v"(t));        // keep hipcc from folding it into a second, dependent v_mad_u64_u32
+        const uint64_t m = (uint64_t)yl * P32_1 + s_next;
+        xh = (uint32_t)(m >> 32) + t;
+        xl = (uint32_t)m;
+    };
+    if (nb > 0) {
+        uint64_t x0 = acc + sums[i];
+        uint32_t xl = (uint32_t)x0, xh = (uint32_t)(x0 >> 32);
+        uint64_t b = 1;  // x holds acc + S_0; each step scrambles and adds the next block's sum
+        if (nb > GROUP) {
+            uint64_t cur[GROUP];
 #pragma unroll
-        for (int t = 0; t < GROUP; ++t) cur[t] = sums[(uint64_t)t * 8 + i];
-        const uint64_t ngroups = nb / GROUP;
-        for (uint64_t gi = 0; gi < ngroups; ++gi) {
-            const uint64_t gn = (gi + 1 < ngroups) ? gi + 1 : gi;
-            uint64_t nxt[GROUP];
+            for (int t = 0; t < GROUP; ++t) cur[t] = sums[(1 + (uint64_t)t) * 8 + i];
+            const uint64_t ngroups = (nb - 1) / GROUP;
+            for (uint64_t gi = 0; gi < ngroups; ++gi) {
+                const uint64_t gn = (gi + 1 < ngroups) ? gi + 1 : gi;
+                uint64_t nxt[GROUP];
 #pragma unroll
-            for (int t = 0; t < GROUP; ++t) nxt[t] = sums[(gn * GROUP + t) * 8 + i];
+                for (int t = 0; t < GROUP; ++t) nxt[t] = sums[(1 + gn * GROUP + t) * 8 + i];
 #pragma unroll
-            for (int t = 0; t < GROUP; ++t) acc = scramble1(acc + cur[t], sk);
+                for (int t = 0; t < GROUP; ++t) step(xl, xh, cur[t]);
 #pragma unroll
-            for (int t = 0; t < GROUP; ++t) cur[t] = nxt[t];
+                for (int t = 0; t < GROUP; ++t) cur[t] = nxt[t];
+            }
+            b = 1 + ngroups * GROUP;
         }
-        b = ngroups * GROUP;
+        for (; b < nb; ++b) step(xl, xh, sums[b * 8 + i]);
+        step(xl, xh, 0);  // the last full block's scramble
+        acc = ((uint64_t)xh << 32) | xl;
     }
-    for (; b < nb; ++b) acc = scramble1(acc + sums[b * 8 + i], sk);
     // partial block stripes + last stripe: lane i owns accumulator i here (scalar per lane)
     const uint64_t ns = ((len - 1) - (nb << 10)) >> 6;
     const uint8_t* pb = p + (nb << 10);
@@ -450,6 +552,34 @@ __global__ __launch_bounds__(64) void xxh3_chain_kernel(ChainBatch batch) {
     if (lane == 0) {
         job.out[0] = avalanche_xxh3(len * P64_1 + mlo);
         job.out[1] = avalanche_xxh3(~(len * P64_2) + mhi);
+    }
+}
+
+// Text counts of one large buffer without hashing it (oversize text files, whose digest comes from
+// K1L): counts[0] += newlines, counts[1] += UTF-8 continuation bytes (caller zeroes counts first).
+__global__ __launch_bounds__(256) void text_count_kernel(const uint8_t* __restrict__ p, uint64_t len,
+                                                         unsigned long long* __restrict__ counts) {
+    uint32_t nl = 0, cont = 0;
+    const uint64_t n16 = len / 16;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
+        uint4 d;
+        __builtin_memcpy(&d, p + 16 * i, 16);
+        count16(d, nl, cont);
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (len & 15)) {
+        const uint8_t b = p[16 * n16 + threadIdx.x];
+        nl += b == 0x0A;
+        cont += (b & 0xC0) == 0x80;
+    }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        nl += (uint32_t)__shfl_xor((int)nl, off, 64);
+        cont += (uint32_t)__shfl_xor((int)cont, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&counts[0], (unsigned long long)nl);
+        atomicAdd(&counts[1], (unsigned long long)cont);
     }
 }
 
@@ -489,6 +619,8 @@ template __global__ void xxh3_wave_kernel<true, 64>(const uint8_t*, const uint64
 template __global__ void xxh3_wave_kernel<false, 64>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 template __global__ void xxh3_wave_kernel<true, 72>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 template __global__ void xxh3_wave_kernel<false, 72>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_text_wave_kernel<0>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t*, uint64_t*);
+template __global__ void xxh3_text_wave_kernel<72>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t*, uint64_t*);
 template __global__ void xxh3_blocksum_kernel<true>(const uint8_t*, uint64_t, uint64_t*);
 template __global__ void xxh3_blocksum_kernel<false>(const uint8_t*, uint64_t, uint64_t*);
 

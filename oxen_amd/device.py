@@ -44,6 +44,22 @@ def xxh3_128_batch_device(arena: torch.Tensor, offsets: torch.Tensor, lens: torc
     return out
 
 
+def xxh3_128_text_batch_device(arena: torch.Tensor, offsets: torch.Tensor, lens: torch.Tensor,
+                               out: Optional[torch.Tensor] = None, counts: Optional[torch.Tensor] = None,
+                               stream=None):
+    """K1T: digests + (num_lines, num_chars) per item in one HBM pass."""
+    _require_cuda(arena, offsets, lens)
+    n = lens.numel()
+    if out is None:
+        out = torch.empty((n, 2), dtype=torch.int64, device=arena.device)
+    if counts is None:
+        counts = torch.empty((n, 2), dtype=torch.int64, device=arena.device)
+    _capi.check(_capi.lib().oxh_xxh3_128_text_batch_device(arena.data_ptr(), offsets.data_ptr(), lens.data_ptr(), n,
+                                                           out.data_ptr(), counts.data_ptr(), _stream(stream)),
+                "oxh_xxh3_128_text_batch_device")
+    return out, counts
+
+
 def chunk_digests_device(buf: torch.Tensor, chunk: int, nbytes: Optional[int] = None,
                          out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
     _require_cuda(buf)

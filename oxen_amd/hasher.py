@@ -99,6 +99,47 @@ def hash_files_128bit(paths: Sequence[str], ctx: Optional[_capi.Context] = None)
     return digests, [int(s) for s in sizes], [int(s) for s in status]
 
 
+def hash_files_text_128bit(paths: Sequence[str], ctx: Optional[_capi.Context] = None):
+    """K1T: digests plus the text metadata liboxen computes in a second pass
+    (repositories/metadata/text.rs:11-20): returns (digests, sizes, status, metadata) where
+    metadata[i] = {"text": {"num_lines": L, "num_chars": C}} (MetadataText's serde shape), or None
+    where status[i] != 0."""
+    ctx = ctx or default_context()
+    n = len(paths)
+    if n == 0:
+        return [], [], [], []
+    arr = (ctypes.c_char_p * n)(*[os.fsencode(str(p)) for p in paths])
+    out = np.zeros((n, 2), dtype=np.uint64)
+    sizes = np.zeros(n, dtype=np.uint64)
+    status = np.zeros(n, dtype=np.int32)
+    counts = np.zeros((n, 2), dtype=np.uint64)
+    _capi.check(_capi.lib().oxh_hash_files_text(ctx.handle, arr, n, out.ctypes.data_as(_capi._u64p),
+                                                sizes.ctypes.data_as(_capi._u64p),
+                                                status.ctypes.data_as(_capi._i32p),
+                                                counts.ctypes.data_as(_capi._u64p)), "oxh_hash_files_text")
+    digests = [(_to_u128(lo, hi) if st == 0 else None) for (lo, hi), st in zip(out, status)]
+    meta = [({"text": {"num_lines": int(c[0]), "num_chars": int(c[1])}} if st == 0 else None)
+            for c, st in zip(counts, status)]
+    return digests, [int(s) for s in sizes], [int(s) for s in status], meta
+
+
+def text_file_nodes(paths: Sequence[str], ctx: Optional[_capi.Context] = None):
+    """The hashing half of add.rs:833-842 for text files, batched: content hash and text counts in one
+    GPU pass (K1T), then metadata_hash = XXH3(serde_json(metadata)) and combined_hash =
+    XXH3(content LE || metadata LE) in batched passes. Returns a list of dicts (None for unreadable
+    files) with keys hash, num_bytes, metadata, metadata_hash, combined_hash."""
+    ctx = ctx or default_context()
+    digests, sizes, status, meta = hash_files_text_128bit(paths, ctx)
+    ok = [i for i, st in enumerate(status) if st == 0]
+    mh = hash_streams_128bit([metadata_json(meta[i]).encode("utf-8") for i in ok], ctx)
+    comb = hash_streams_128bit([digests[i].to_bytes(16, "little") + m.to_bytes(16, "little") for i, m in zip(ok, mh)], ctx)
+    res: list = [None] * len(paths)
+    for j, i in enumerate(ok):
+        res[i] = {"hash": digests[i], "num_bytes": sizes[i], "metadata": meta[i], "metadata_hash": mh[j],
+                  "combined_hash": comb[j]}
+    return res
+
+
 # ---------------------------------------------------------------------------- hasher.rs mirror
 def hash_buffer_128bit(buffer: bytes) -> int:
     """hasher.rs:28-30."""

@@ -338,3 +338,65 @@ def test_empty_batch(cuda):
     z = torch.zeros(0, dtype=torch.int64, device=cuda)
     out = xxh3_128_batch_device(torch.zeros(8, dtype=torch.uint8, device=cuda), z, z)
     assert out.shape == (0, 2)
+
+
+def _text_counts(b: bytes):
+    return 1 + b.count(b"\n"), sum(1 for x in b if (x & 0xC0) != 0x80)
+
+
+def test_text_counts_fused_every_length(cuda, oracle_lib):
+    """K1T: digests identical to K1 and text counts exact for every length class, aligned and not."""
+    import torch
+
+    from oxen_amd.device import xxh3_128_text_batch_device
+
+    rng = np.random.default_rng(9)
+    alphabet = np.frombuffer("ab\nc é漢\n🐂 z\n".encode(), dtype=np.uint8)
+    lens = list(range(0, 300)) + [1023, 1024, 1025, 4095, 4096, 4097, 8191, 8192, 49_292, 65_536, 100_003]
+    span = sum(lens) + 64 * len(lens)
+    host = alphabet[rng.integers(0, len(alphabet), span)]
+    offs = np.cumsum([0] + [L + int(rng.integers(0, 17)) for L in lens[:-1]]).astype(np.uint64)
+    arena = torch.from_numpy(host).to(cuda)
+    out, counts = xxh3_128_text_batch_device(arena, torch.from_numpy(offs.view(np.int64)).to(cuda),
+                                             torch.from_numpy(np.array(lens, dtype=np.uint64).view(np.int64)).to(cuda))
+    got = _u64(out)
+    cnt = counts.cpu().numpy()
+    for i, L in enumerate(lens):
+        b = host[int(offs[i]):int(offs[i]) + L].tobytes()
+        assert (int(got[i, 0]), int(got[i, 1])) == oracle_lib.xxh3_128(b), L
+        assert tuple(int(x) for x in cnt[i]) == _text_counts(b), L
+
+
+def test_text_file_nodes_config1(ctx, golden, tmp_path):
+    """Config 1 end to end: content hash, text metadata, metadata hash and combined hash of every
+    file of the 1 000-file text repo (add.rs:833-842) match the goldens."""
+    from oxen_amd import hasher
+    from oxen_amd.workloads import write_text_repo
+
+    paths = write_text_repo(str(tmp_path))
+    nodes = hasher.text_file_nodes(paths, ctx)
+    want = {r["path"]: r for r in golden("text_repo.json")["files"]}
+    for p, nd in zip(paths, nodes):
+        r = want[os.path.relpath(p, str(tmp_path))]
+        assert format(nd["hash"], "x") == r["hex"]
+        assert hasher.metadata_json(nd["metadata"]) == r["metadata_json"]
+        assert format(nd["metadata_hash"], "x") == r["metadata_hash"]
+        assert format(nd["combined_hash"], "x") == r["combined_hash"]
+
+
+def test_text_files_oversize_and_errors(cuda, tmp_path):
+    from oxen_amd import _capi, hasher
+
+    rng = np.random.default_rng(4)
+    texts = [("x\n" * 700_000 + "é").encode(), b"", b"\n", "🐂".encode() * 1000]
+    paths = []
+    for i, t in enumerate(texts):
+        p = tmp_path / f"t{i}.txt"
+        p.write_bytes(t)
+        paths.append(str(p))
+    paths.append(str(tmp_path / "missing.txt"))
+    with _capi.Context(0, staging_bytes=1 << 20) as c:  # the 1.4 MB file is oversize
+        d, sizes, st, meta = hasher.hash_files_text_128bit(paths, c)
+    assert st[-1] != 0 and meta[-1] is None
+    for t, m in zip(texts, meta):
+        assert (m["text"]["num_lines"], m["text"]["num_chars"]) == _text_counts(t)
