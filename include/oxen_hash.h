@@ -99,6 +99,17 @@ int oxh_hash_buffers(oxh_ctx* ctx, const uint8_t* const* bufs, const uint64_t* l
 int oxh_hash_files(oxh_ctx* ctx, const char* const* paths, uint64_t n, uint64_t* out,
                    uint64_t* sizes, int32_t* status);
 
+/* The add loop's hash and version-store copy, fused (add.rs:507-516, 718, 743;
+ * storage/local.rs:104-121; util/fs/atomic_file.rs:363-463): each file is read ONCE into pinned
+ * staging and hashed by K1; when its blob is not already in the store it is written from the same
+ * pinned bytes to {versions_root}/{hex[..2]}/{hex[2..]}/data (hex = unpadded {:x}) via a temp file
+ * + rename. The reference reads a new file three times and hashes it twice (verify-before-publish);
+ * here the published bytes are the hashed bytes, so the check holds by construction.
+ * stored[i] = 1 if a blob was written, 0 if it already existed or the file failed (see status:
+ * OXH_ERR_IO for unreadable files or a failed publish). */
+int oxh_add_files(oxh_ctx* ctx, const char* const* paths, uint64_t n, const char* versions_root,
+                  uint64_t* out, uint64_t* sizes, int32_t* status, int32_t* stored);
+
 /* Text-metadata fusion (K1T): the same digests as oxh_hash_files plus, per file, the counts liboxen's
  * text metadata reads in a second full pass (repositories/metadata/text.rs:11-20 ->
  * util/fs.rs:217-263): counts[2i] = num_lines (1 + number of b'\n'), counts[2i+1] = num_chars

@@ -45,6 +45,9 @@ def lib():
         L.oxo_xxh3_128_batch.restype = None
         L.oxo_hash_files.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_uint64, _u64p, _u64p, _i32p, ctypes.c_int]
         L.oxo_hash_files.restype = None
+        L.oxo_add_files.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_uint64, ctypes.c_char_p, _u64p, _u64p,
+                                    _i32p, _i32p, ctypes.c_int]
+        L.oxo_add_files.restype = None
         L.oxo_chunk_digests.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, _u64p, ctypes.c_int]
         L.oxo_chunk_digests.restype = None
         L.oxo_format_hex.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_char_p]
@@ -97,6 +100,19 @@ def hash_files(paths: list[str], threads: int = 1):
     status = np.zeros(n, dtype=np.int32)
     lib().oxo_hash_files(arr, n, _ptr(out), _ptr(sizes), _ptr(status, _i32p), int(threads))
     return out, sizes, status
+
+
+def add_files(paths: list[str], versions_root: str, threads: int = 1):
+    """Reference add loop restated (hash, then store_version_from_reader with verify-before-publish)."""
+    n = len(paths)
+    arr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
+    out = np.zeros((n, 2), dtype=np.uint64)
+    sizes = np.zeros(n, dtype=np.uint64)
+    status = np.zeros(n, dtype=np.int32)
+    stored = np.zeros(n, dtype=np.int32)
+    lib().oxo_add_files(arr, n, os.fsencode(versions_root), _ptr(out), _ptr(sizes), _ptr(status, _i32p),
+                        _ptr(stored, _i32p), int(threads))
+    return out, sizes, status, stored
 
 
 def chunk_digests(data: np.ndarray, chunk: int, threads: int = 1) -> np.ndarray:

@@ -9,6 +9,7 @@
 //   * device-resident batches go straight to the kernels.
 // There is no CPU hashing path here: every digest this library returns was computed on the GPU.
 #include <hip/hip_runtime.h>
+#include <errno.h>
 #include <fcntl.h>
 #include <stdint.h>
 #include <string.h>
@@ -331,17 +332,34 @@ struct Trace {
     }
 };
 
+// Called for every item of a drained slot whose digest is known, with the staged (pinned) bytes
+// still in place: lets a caller consume the exact bytes that were hashed (fused version-store copy).
+using ItemSink = std::function<void(uint64_t id, const uint8_t* bytes, uint64_t len, uint64_t lo, uint64_t hi)>;
+
 struct Pending {
     bool busy = false;
     std::vector<uint64_t> ids;  // caller indices of the staged items
 };
 
-int drain_slot(oxh_ctx* c, int s, Pending& p, uint64_t* out, uint64_t* counts = nullptr) {
+int drain_slot(oxh_ctx* c, int s, Pending& p, uint64_t* out, uint64_t* counts = nullptr,
+               const ItemSink* sink = nullptr, const int32_t* status = nullptr) {
     if (!p.busy) return OXH_OK;
     HIP_TRY(hipEventSynchronize(c->ev_done[s]));
     for (size_t j = 0; j < p.ids.size(); ++j) {
         out[2 * p.ids[j]] = c->h_out[s][2 * j];
         out[2 * p.ids[j] + 1] = c->h_out[s][2 * j + 1];
+    }
+    if (sink) {
+        const uint64_t M = c->max_items;
+        const size_t cnt = p.ids.size();
+        const int ntasks = (int)std::min<size_t>(cnt, (size_t)c->pool->size() * 4);
+        c->pool->parallel_for(ntasks, [&](int t) {
+            for (size_t j = (size_t)t; j < cnt; j += (size_t)ntasks) {
+                const uint64_t id = p.ids[j];
+                if (status && status[id] != OXH_OK) continue;
+                (*sink)(id, c->h_stage[s] + c->h_desc[s][j], c->h_desc[s][M + j], c->h_out[s][2 * j], c->h_out[s][2 * j + 1]);
+            }
+        });
     }
     if (counts)
         for (size_t j = 0; j < p.ids.size(); ++j) {
@@ -513,7 +531,8 @@ int oxh_combined_hash_device(const uint64_t* d_content, const uint64_t* d_metada
 // `reader(i, dst)` directly into the pinned slot; lens[i] is known up front.
 static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
                            const std::function<int(uint64_t, uint8_t*)>& fill, uint64_t* out, int32_t* status,
-                           bool short_only_lane, Trace* tr = nullptr, uint64_t* counts = nullptr) {
+                           bool short_only_lane, Trace* tr = nullptr, uint64_t* counts = nullptr,
+                           const ItemSink* sink = nullptr) {
     Trace local;
     if (!tr) tr = &local;
     Pending pend[NSLOT];
@@ -530,7 +549,7 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
                 if (!batch.empty()) break;
                 // oversize item: read it fully into a host buffer, then stream through slot 0
                 for (int s = 0; s < NSLOT; ++s) {
-                    int rc = drain_slot(c, s, pend[s], out, counts);
+                    int rc = drain_slot(c, s, pend[s], out, counts, sink, status);
                     if (rc) return rc;
                 }
                 std::vector<uint8_t> tmp(L);
@@ -539,6 +558,7 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
                 if (st == OXH_OK) {
                     int rc = oversize_item(c, tmp.data(), L, out + 2 * i, counts ? counts + 2 * i : nullptr);
                     if (rc) return rc;
+                    if (sink) (*sink)(i, tmp.data(), L, out[2 * i], out[2 * i + 1]);
                 } else {
                     out[2 * i] = out[2 * i + 1] = 0;
                 }
@@ -554,7 +574,7 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
         const int s = slot;
         slot = (slot + 1) % NSLOT;
         double t0 = Trace::now();
-        int rc = drain_slot(c, s, pend[s], out, counts);
+        int rc = drain_slot(c, s, pend[s], out, counts, sink, status);
         if (rc) return rc;
         double t1 = Trace::now();
         tr->drain += t1 - t0;
@@ -594,7 +614,7 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
     }
     double t3 = Trace::now();
     for (int s = 0; s < NSLOT; ++s) {
-        int rc = drain_slot(c, s, pend[s], out, counts);
+        int rc = drain_slot(c, s, pend[s], out, counts, sink, status);
         if (rc) return rc;
     }
     tr->drain += Trace::now() - t3;
@@ -648,7 +668,7 @@ static int read_whole(const char* path, uint8_t* dst, uint64_t len) {
 }
 
 static int hash_files_impl(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* sizes, int32_t* status,
-                           uint64_t* counts) {
+                           uint64_t* counts, const ItemSink* sink = nullptr) {
     if (!c || (n && (!paths || !out))) return fail(OXH_ERR_INVALID, "bad arguments");
     std::lock_guard<std::mutex> g(c->mu);
     HIP_TRY(hipSetDevice(c->device));
@@ -673,7 +693,7 @@ static int hash_files_impl(oxh_ctx* c, const char* const* paths, uint64_t n, uin
     int rc = hash_host_items(c, n, lens.data(), [&](uint64_t i, uint8_t* dst) {
         if (st[i] != OXH_OK) return (int)st[i];
         return read_whole(paths[i], dst, lens[i]);
-    }, out, st2.data(), false, &tr, counts);
+    }, out, st2.data(), false, &tr, counts, sink);
     if (rc) return rc;
     for (uint64_t i = 0; i < n; ++i) {
         if (sizes) sizes[i] = lens[i];
@@ -690,6 +710,66 @@ int oxh_hash_files_text(oxh_ctx* c, const char* const* paths, uint64_t n, uint64
                         uint64_t* counts) {
     if (n && !counts) return fail(OXH_ERR_INVALID, "counts is NULL");
     return hash_files_impl(c, paths, n, out, sizes, status, counts);
+}
+
+// Publish `data` as the version blob of digest (lo, hi): {root}/{hex[..2]}/{hex[2..]}/data
+// (storage/local.rs:66-75), skipped when present (local.rs:112), written as tmp + rename so a reader
+// never sees a partial blob (util/fs/atomic_file.rs). Returns 1 if written, 0 if it existed, <0 on error.
+static int store_version_blob(const std::string& root, uint64_t lo, uint64_t hi, const uint8_t* data, uint64_t len) {
+    char hex[40];
+    const int hl = oxh_format_hex(lo, hi, hex);
+    const std::string top = root + "/" + std::string(hex, std::min(hl, 2));
+    const std::string dir = top + "/" + std::string(hex + std::min(hl, 2));
+    const std::string path = dir + "/data";
+    struct stat sb;
+    if (stat(path.c_str(), &sb) == 0) return 0;
+    if (mkdir(top.c_str(), 0755) != 0 && errno != EEXIST) {
+        // first blob under a new root: create the root's missing parents too (mkdir -p)
+        for (size_t i = 1; i <= root.size(); ++i)
+            if (i == root.size() || root[i] == '/') {
+                const std::string part = root.substr(0, i);
+                if (mkdir(part.c_str(), 0755) != 0 && errno != EEXIST) return -1;
+            }
+        if (mkdir(top.c_str(), 0755) != 0 && errno != EEXIST) return -1;
+    }
+    if (mkdir(dir.c_str(), 0755) != 0 && errno != EEXIST) return -1;
+    static std::atomic<uint64_t> seq{0};
+    const std::string tmp = dir + "/.data.tmp." + std::to_string((long)getpid()) + "." + std::to_string(seq.fetch_add(1));
+    const int fd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_EXCL | O_CLOEXEC, 0644);
+    if (fd < 0) return -1;
+    uint64_t put = 0;
+    while (put < len) {
+        const ssize_t w = write(fd, data + put, len - put);
+        if (w <= 0) {
+            close(fd);
+            unlink(tmp.c_str());
+            return -1;
+        }
+        put += (uint64_t)w;
+    }
+    if (close(fd) != 0 || rename(tmp.c_str(), path.c_str()) != 0) {
+        unlink(tmp.c_str());
+        return -1;
+    }
+    return 1;
+}
+
+int oxh_add_files(oxh_ctx* c, const char* const* paths, uint64_t n, const char* versions_root, uint64_t* out,
+                  uint64_t* sizes, int32_t* status, int32_t* stored) {
+    if (n && (!versions_root || !stored || !status)) return fail(OXH_ERR_INVALID, "versions_root/status/stored is NULL");
+    const std::string root(versions_root ? versions_root : "");
+    for (uint64_t i = 0; i < n; ++i) stored[i] = 0;
+    std::vector<uint8_t> pub_err(n, 0);
+    ItemSink sink = [&](uint64_t id, const uint8_t* bytes, uint64_t len, uint64_t lo, uint64_t hi) {
+        const int r = store_version_blob(root, lo, hi, bytes, len);
+        stored[id] = r > 0 ? 1 : 0;
+        if (r < 0) pub_err[id] = 1;
+    };
+    const int rc = hash_files_impl(c, paths, n, out, sizes, status, nullptr, &sink);
+    if (rc) return rc;
+    for (uint64_t i = 0; i < n; ++i)
+        if (pub_err[i]) status[i] = OXH_ERR_IO;  // could not publish the blob: the add of this file fails
+    return OXH_OK;
 }
 
 int oxh_xxh3_128_text_batch_device(const void* d_arena, const uint64_t* d_offsets, const uint64_t* d_lens, uint64_t n,

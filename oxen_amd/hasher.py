@@ -99,6 +99,32 @@ def hash_files_128bit(paths: Sequence[str], ctx: Optional[_capi.Context] = None)
     return digests, [int(s) for s in sizes], [int(s) for s in status]
 
 
+def add_files(paths: Sequence[str], versions_root: str, ctx: Optional[_capi.Context] = None):
+    """Fused hash + version-store publish (oxh_add_files): returns (digests, sizes, status, stored).
+    stored[i] is True when the blob {versions_root}/{hex[:2]}/{hex[2:]}/data was written now."""
+    ctx = ctx or default_context()
+    n = len(paths)
+    if n == 0:
+        return [], [], [], []
+    arr = (ctypes.c_char_p * n)(*[os.fsencode(str(p)) for p in paths])
+    out = np.zeros((n, 2), dtype=np.uint64)
+    sizes = np.zeros(n, dtype=np.uint64)
+    status = np.zeros(n, dtype=np.int32)
+    stored = np.zeros(n, dtype=np.int32)
+    _capi.check(_capi.lib().oxh_add_files(ctx.handle, arr, n, os.fsencode(str(versions_root)),
+                                          out.ctypes.data_as(_capi._u64p), sizes.ctypes.data_as(_capi._u64p),
+                                          status.ctypes.data_as(_capi._i32p), stored.ctypes.data_as(_capi._i32p)),
+                "oxh_add_files")
+    digests = [(_to_u128(lo, hi) if st == 0 else None) for (lo, hi), st in zip(out, status)]
+    return digests, [int(s) for s in sizes], [int(s) for s in status], [bool(s) for s in stored]
+
+
+def version_path(versions_root: str, digest: int) -> str:
+    """LocalVersionStore::version_path (storage/local.rs:66-75): {root}/{hex[..2]}/{hex[2..]}/data."""
+    h = format_hex(digest)
+    return os.path.join(versions_root, h[:2], h[2:], "data")
+
+
 def hash_files_text_128bit(paths: Sequence[str], ctx: Optional[_capi.Context] = None):
     """K1T: digests plus the text metadata liboxen computes in a second pass
     (repositories/metadata/text.rs:11-20): returns (digests, sizes, status, metadata) where

@@ -400,3 +400,33 @@ def test_text_files_oversize_and_errors(cuda, tmp_path):
     assert st[-1] != 0 and meta[-1] is None
     for t, m in zip(texts, meta):
         assert (m["text"]["num_lines"], m["text"]["num_chars"]) == _text_counts(t)
+
+
+def test_add_files_fused_version_store(ctx, oracle_lib, golden, tmp_path):
+    """oxh_add_files: one read, K1 hash, blob published from the same pinned bytes; the store it
+    builds is identical to the reference loop's (oracle restatement of add + store_version_from_reader)."""
+    from oxen_amd import hasher
+
+    recs = [r for r in golden("data_test.json")["files"] if r["copied"]]
+    paths = [os.path.join(GOLDEN, "data_test", r["path"]) for r in recs]
+    paths.append(paths[0])  # the same content twice: second add finds the blob
+    paths.append(str(tmp_path / "missing.bin"))
+    root = str(tmp_path / ".oxen" / "versions" / "files")  # parents created on first publish
+    d, sizes, st, stored = hasher.add_files(paths, root, ctx)
+    assert st[-1] != 0 and stored[-1] is False
+    for p, r, dg in zip(paths, recs, d):
+        assert format(dg, "x") == r["hex"]
+        blob = hasher.version_path(root, dg)
+        assert open(blob, "rb").read() == open(p, "rb").read()
+    # identical content is stored once
+    n_unique = len({r["hex"] for r in recs})
+    assert sum(stored) == n_unique
+    # a second add stores nothing new
+    d2, _, st2, stored2 = hasher.add_files(paths[:-1], root, ctx)
+    assert not any(stored2) and d2 == d[:-1]
+    # the reference loop builds the same store
+    ref_root = str(tmp_path / "ref" / "versions" / "files")
+    out, _, rst, rstored = oracle_lib.add_files(paths[:-1], ref_root, threads=4)
+    assert (rst == 0).all()
+    walk = lambda r: sorted(os.path.relpath(os.path.join(dp, f), r) for dp, _, fs in os.walk(r) for f in fs)
+    assert walk(root) == walk(ref_root)

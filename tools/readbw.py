@@ -83,6 +83,12 @@ def main():
         if ref is None:
             ref = d
         assert torch.equal(ref, d), f"variant {v} digests differ from variant 0"
+    # K1T (hash + fused text counts) on the same arena: the price of the fusion
+    from oxen_amd.device import xxh3_128_text_batch_device
+
+    cnt = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+    variants["k1t_text_fused"] = lambda: (_capi.lib().oxh_set_kernel_variant(0),
+                                         xxh3_128_text_batch_device(da.arena, da.offsets, da.lens, out, cnt))
     # K1 (default variant) on skewed pitches and on a 4x larger batch (tail effect)
     _capi.lib().oxh_set_kernel_variant(0)
     for pad in (256, 4096):
