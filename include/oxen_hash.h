@@ -110,6 +110,16 @@ int oxh_hash_files(oxh_ctx* ctx, const char* const* paths, uint64_t n, uint64_t*
 int oxh_add_files(oxh_ctx* ctx, const char* const* paths, uint64_t n, const char* versions_root,
                   uint64_t* out, uint64_t* sizes, int32_t* status, int32_t* stored);
 
+/* Bulk re-hash of a version store: LocalVersionStore::clean_corrupted_versions
+ * (storage/local.rs:417-610, `oxen fsck`). Walks {versions_root}/{prefix}/{suffix}/data, hashes every
+ * blob on the GPU (files batched exactly as oxh_hash_files) and compares the unpadded hex digest with
+ * prefix+suffix. Corrupted or unreadable blobs have their {suffix} directory removed unless dry_run.
+ * result[4] = {scanned, corrupted, cleaned, errors} -- the fields of CleanCorruptedVersionsResult
+ * (view/versions.rs), counted with the reference's rules: a non-directory under the root is an
+ * error; a non-directory under a prefix is skipped; an unreadable blob is an error (not scanned) and
+ * is removed unless dry_run; a failed removal is an error. */
+int oxh_clean_corrupted_versions(oxh_ctx* ctx, const char* versions_root, int dry_run, uint64_t* result);
+
 /* Text-metadata fusion (K1T): the same digests as oxh_hash_files plus, per file, the counts liboxen's
  * text metadata reads in a second full pass (repositories/metadata/text.rs:11-20 ->
  * util/fs.rs:217-263): counts[2i] = num_lines (1 + number of b'\n'), counts[2i+1] = num_chars

@@ -127,3 +127,53 @@ def format_hex(lo: int, hi: int) -> str:
     buf = ctypes.create_string_buffer(40)
     lib().oxo_format_hex(lo, hi, buf)
     return buf.value.decode()
+
+
+def clean_corrupted_versions(versions_root: str, dry_run: bool = False, threads: int = 1) -> dict:
+    """storage/local.rs:417-610 restated: walk {root}/{prefix}/{suffix}/data, hash every blob with the
+    C oracle (fs::read + hash_buffer), compare with prefix+suffix, remove_dir_all mismatches and
+    unreadable blobs unless dry_run. Same counting rules as the reference (see include/oxen_hash.h)."""
+    import shutil
+
+    errors = 0
+    prefixes = []
+    for e in os.scandir(versions_root):
+        if e.is_dir(follow_symlinks=False):
+            prefixes.append(e)
+        else:
+            errors += 1
+    dirs, expected = [], []
+    for pre in prefixes:
+        try:
+            entries = list(os.scandir(pre.path))
+        except OSError:
+            errors += 1
+            continue
+        for e in entries:
+            if not e.is_dir(follow_symlinks=False):
+                continue
+            dirs.append(e.path)
+            expected.append(pre.name + e.name)
+    out, _, status = hash_files([os.path.join(d, "data") for d in dirs], threads=threads)
+    scanned = corrupted = cleaned = 0
+    for d, exp, (lo, hi), st in zip(dirs, expected, out, status):
+        if st != 0:
+            errors += 1
+            if not dry_run:
+                try:
+                    shutil.rmtree(d)
+                    cleaned += 1
+                except OSError:
+                    pass
+            continue
+        scanned += 1
+        if format((int(hi) << 64) | int(lo), "x") == exp:
+            continue
+        corrupted += 1
+        if not dry_run:
+            try:
+                shutil.rmtree(d)
+                cleaned += 1
+            except OSError:
+                errors += 1
+    return {"scanned": scanned, "corrupted": corrupted, "cleaned": cleaned, "errors": errors}

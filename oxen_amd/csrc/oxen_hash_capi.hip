@@ -9,8 +9,10 @@
 //   * device-resident batches go straight to the kernels.
 // There is no CPU hashing path here: every digest this library returns was computed on the GPU.
 #include <hip/hip_runtime.h>
+#include <dirent.h>
 #include <errno.h>
 #include <fcntl.h>
+#include <ftw.h>
 #include <stdint.h>
 #include <string.h>
 #include <sys/stat.h>
@@ -769,6 +771,91 @@ int oxh_add_files(oxh_ctx* c, const char* const* paths, uint64_t n, const char* 
     if (rc) return rc;
     for (uint64_t i = 0; i < n; ++i)
         if (pub_err[i]) status[i] = OXH_ERR_IO;  // could not publish the blob: the add of this file fails
+    return OXH_OK;
+}
+
+static int remove_tree_cb(const char* p, const struct stat*, int, struct FTW*) { return remove(p); }
+
+// std::fs::remove_dir_all: depth-first, does not follow symlinks.
+static bool remove_dir_all(const std::string& dir) {
+    return nftw(dir.c_str(), remove_tree_cb, 64, FTW_DEPTH | FTW_PHYS) == 0;
+}
+
+int oxh_clean_corrupted_versions(oxh_ctx* c, const char* versions_root, int dry_run, uint64_t* result) {
+    if (!c || !versions_root || !result) return fail(OXH_ERR_INVALID, "bad arguments");
+    uint64_t errors = 0, scanned = 0, corrupted = 0, cleaned = 0;
+    // prefix dirs (local.rs:461-474): anything that is not a directory counts as an error
+    std::vector<std::string> prefixes;
+    {
+        DIR* d = opendir(versions_root);
+        if (!d) return fail(OXH_ERR_IO, std::string("cannot read ") + versions_root);
+        while (struct dirent* e = readdir(d)) {
+            if (!strcmp(e->d_name, ".") || !strcmp(e->d_name, "..")) continue;
+            const std::string p = std::string(versions_root) + "/" + e->d_name;
+            struct stat sb;
+            if (lstat(p.c_str(), &sb) == 0 && S_ISDIR(sb.st_mode))
+                prefixes.push_back(e->d_name);
+            else
+                ++errors;
+        }
+        closedir(d);
+    }
+    std::sort(prefixes.begin(), prefixes.end());
+    // suffix dirs (local.rs:480-518): non-directories are skipped; expected hash = prefix + suffix
+    std::vector<std::string> dirs, expected, data;
+    for (const std::string& pre : prefixes) {
+        const std::string pdir = std::string(versions_root) + "/" + pre;
+        DIR* d = opendir(pdir.c_str());
+        if (!d) {
+            ++errors;
+            continue;
+        }
+        while (struct dirent* e = readdir(d)) {
+            if (!strcmp(e->d_name, ".") || !strcmp(e->d_name, "..")) continue;
+            const std::string sdir = pdir + "/" + e->d_name;
+            struct stat sb;
+            if (lstat(sdir.c_str(), &sb) != 0) {
+                ++errors;
+                continue;
+            }
+            if (!S_ISDIR(sb.st_mode)) continue;
+            dirs.push_back(sdir);
+            expected.push_back(pre + e->d_name);
+            data.push_back(sdir + "/data");
+        }
+        closedir(d);
+    }
+    const uint64_t n = dirs.size();
+    std::vector<const char*> paths(n);
+    for (uint64_t i = 0; i < n; ++i) paths[i] = data[i].c_str();
+    std::vector<uint64_t> out(2 * n), sizes(n);
+    std::vector<int32_t> status(n);
+    const int rc = hash_files_impl(c, paths.data(), n, out.data(), sizes.data(), status.data(), nullptr);
+    if (rc) return rc;
+    for (uint64_t i = 0; i < n; ++i) {
+        bool remove_it = false;
+        if (status[i] != OXH_OK) {  // fs::read failed: an error, not scanned (local.rs:527-537)
+            ++errors;
+            remove_it = !dry_run;
+            if (remove_it && remove_dir_all(dirs[i])) ++cleaned;
+            continue;
+        }
+        ++scanned;
+        char hex[40];
+        const int hl = oxh_format_hex(out[2 * i], out[2 * i + 1], hex);
+        if (expected[i].size() == (size_t)hl && memcmp(expected[i].data(), hex, hl) == 0) continue;
+        ++corrupted;  // local.rs:561-581
+        if (!dry_run) {
+            if (remove_dir_all(dirs[i]))
+                ++cleaned;
+            else
+                ++errors;
+        }
+    }
+    result[0] = scanned;
+    result[1] = corrupted;
+    result[2] = cleaned;
+    result[3] = errors;
     return OXH_OK;
 }
 

@@ -119,6 +119,20 @@ def add_files(paths: Sequence[str], versions_root: str, ctx: Optional[_capi.Cont
     return digests, [int(s) for s in sizes], [int(s) for s in status], [bool(s) for s in stored]
 
 
+def clean_corrupted_versions(versions_root: str, dry_run: bool = False, ctx: Optional[_capi.Context] = None) -> dict:
+    """`oxen fsck`: LocalVersionStore::clean_corrupted_versions (storage/local.rs:417-610) as one batched
+    GPU re-hash of every {versions_root}/{prefix}/{suffix}/data. Returns CleanCorruptedVersionsResult's
+    fields: scanned, corrupted, cleaned, errors, elapsed (seconds)."""
+    ctx = ctx or default_context()
+    res = np.zeros(4, dtype=np.uint64)
+    t0 = time.perf_counter()
+    _capi.check(_capi.lib().oxh_clean_corrupted_versions(ctx.handle, os.fsencode(str(versions_root)), int(bool(dry_run)),
+                                                         res.ctypes.data_as(_capi._u64p)),
+                "oxh_clean_corrupted_versions")
+    return {"scanned": int(res[0]), "corrupted": int(res[1]), "cleaned": int(res[2]), "errors": int(res[3]),
+            "elapsed": time.perf_counter() - t0}
+
+
 def version_path(versions_root: str, digest: int) -> str:
     """LocalVersionStore::version_path (storage/local.rs:66-75): {root}/{hex[..2]}/{hex[2..]}/data."""
     h = format_hex(digest)

@@ -430,3 +430,56 @@ def test_add_files_fused_version_store(ctx, oracle_lib, golden, tmp_path):
     assert (rst == 0).all()
     walk = lambda r: sorted(os.path.relpath(os.path.join(dp, f), r) for dp, _, fs in os.walk(r) for f in fs)
     assert walk(root) == walk(ref_root)
+
+
+def test_clean_corrupted_versions(ctx, oracle_lib, tmp_path):
+    """`oxen fsck` as one batched GPU re-hash: same counts and the same surviving store as the oracle."""
+    from _store import make_version_store
+
+    from oxen_amd import hasher
+
+    hexer = lambda b: oracle_lib.format_hex(*oracle_lib.xxh3_128(b))
+    gpu_root, ref_root = str(tmp_path / "gpu"), str(tmp_path / "ref")
+    dry, real, again = make_version_store(gpu_root, hexer)
+    make_version_store(ref_root, hexer)
+    strip = lambda r: {k: r[k] for k in ("scanned", "corrupted", "cleaned", "errors")}
+    assert strip(hasher.clean_corrupted_versions(gpu_root, dry_run=True, ctx=ctx)) == dry
+    assert strip(hasher.clean_corrupted_versions(gpu_root, dry_run=False, ctx=ctx)) == real
+    assert oracle_lib.clean_corrupted_versions(ref_root, dry_run=False, threads=4) == real
+    walk = lambda r: sorted(os.path.relpath(os.path.join(dp, f), r) for dp, _, fs in os.walk(r) for f in fs)
+    assert walk(gpu_root) == walk(ref_root)
+    assert strip(hasher.clean_corrupted_versions(gpu_root, dry_run=False, ctx=ctx)) == again
+
+
+@pytest.mark.parametrize("second", [False, True])
+@pytest.mark.parametrize("vnode_size", [10_000, 7])
+def test_commit_driver(ctx, second, vnode_size):
+    """K2 end to end: every vnode id and dir hash of a commit from three batched GPU passes equals the
+    scalar restatement of commit_writer.rs (oracle/commit_oracle.py)."""
+    import _commit
+
+    from oracle import commit_oracle
+    from oxen_amd import merkle
+
+    entries, existing = _commit.staged_commit(n_files=500, n_dirs=9, second=second)
+    vn, dh = merkle.commit_tree(_commit.to_staged(entries), _commit.to_staged(existing), vnode_size, _commit.salt,
+                                ctx=ctx)
+    rvn, rdh = commit_oracle.commit_tree(entries, existing, vnode_size, _commit.salt)
+    for d in rvn:
+        assert [v.id.value for v in vn[d][0]] == [i for i, _ in rvn[d]], d
+    assert {d: h.value for d, h in dh.items()} == rdh
+
+
+def test_commit_driver_image_repo_shape(ctx):
+    """C3's tree (200 000 files in 1 000 dirs): root and images/ dir streams are ~10 MB each and go
+    through the wave kernel; the split dirs' vnode streams through the lane kernel."""
+    import _commit
+
+    from oracle import commit_oracle
+    from oxen_amd import merkle
+
+    entries, _ = _commit.staged_commit(n_files=200_000, n_dirs=1000)
+    vn, dh = merkle.commit_tree(_commit.to_staged(entries), None, 10_000, _commit.salt, ctx=ctx)
+    rvn, rdh = commit_oracle.commit_tree(entries, {}, 10_000, _commit.salt)
+    assert {d: [v.id.value for v in vn[d][0]] for d in vn} == {d: [i for i, _ in rvn[d]] for d in rvn}
+    assert {d: h.value for d, h in dh.items()} == rdh

@@ -3,6 +3,7 @@ import io
 import os
 
 import numpy as np
+import pytest
 
 from oxen_amd import merkle, workloads
 
@@ -92,3 +93,29 @@ def test_metadata_json_matches_serde(golden):
     r0 = golden("text_repo.json")["files"][0]
     assert metadata_json({"text": {"num_lines": 1, "num_chars": 14}}) == r0["metadata_json"]
     assert metadata_json(None) == "null"
+
+
+@pytest.mark.parametrize("second", [False, True])
+@pytest.mark.parametrize("vnode_size", [10_000, 7])
+def test_commit_driver_host_logic(monkeypatch, oracle_lib, second, vnode_size):
+    """K2 commit driver (split_into_vnodes + compute_dir_node) against the scalar restatement, with the
+    batched GPU hash swapped for the oracle so the host-side tree logic is checked on CPU."""
+    import _commit
+
+    from oracle import commit_oracle
+    from oxen_amd import hasher, merkle
+
+    def cpu_streams(streams, ctx=None):
+        return [oracle_lib.xxh3_128_int(s) for s in streams]
+
+    monkeypatch.setattr(hasher, "hash_streams_128bit", cpu_streams)
+    entries, existing = _commit.staged_commit(n_files=120, n_dirs=5, second=second)
+    vn, dh = merkle.commit_tree(_commit.to_staged(entries), _commit.to_staged(existing), vnode_size, _commit.salt)
+    rvn, rdh = commit_oracle.commit_tree(entries, existing, vnode_size, _commit.salt)
+    assert set(vn) == set(rvn)
+    for d in rvn:
+        assert [v.id.value for v in vn[d][0]] == [i for i, _ in rvn[d]], d
+        assert [[c.path for c in v.entries] for v in vn[d][0]] == [[n[0] for n in ns] for _, ns in rvn[d]], d
+    assert {d: h.value for d, h in dh.items()} == rdh
+    if vnode_size == 7:
+        assert max(len(v[0]) for v in vn.values()) > 1

@@ -82,3 +82,14 @@ def test_unpadded_hex_and_missing_file(oracle_lib, tmp_path):
     assert len(h) == 31
     out, sizes, status = oracle_lib.hash_files([str(tmp_path / "nope.txt")])
     assert status[0] != 0
+
+
+def test_clean_corrupted_versions_oracle(oracle_lib, tmp_path):
+    """The fsck restatement (storage/local.rs:417-610) counts like the reference on a damaged store."""
+    from _store import make_version_store
+
+    root = str(tmp_path / "files")
+    dry, real, again = make_version_store(root, lambda b: oracle_lib.format_hex(*oracle_lib.xxh3_128(b)))
+    assert oracle_lib.clean_corrupted_versions(root, dry_run=True, threads=4) == dry
+    assert oracle_lib.clean_corrupted_versions(root, dry_run=False, threads=4) == real
+    assert oracle_lib.clean_corrupted_versions(root, dry_run=False, threads=4) == again
