@@ -25,11 +25,13 @@
 #include <condition_variable>
 #include <functional>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "../../include/oxen_hash.h"
+#include "pool.hpp"
 #include "xxh3_device.hpp"
 
 namespace oxh {
@@ -153,79 +155,6 @@ int launch_lane(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens
     return OXH_OK;
 }
 
-// ---------------------------------------------------------------- a small blocking thread pool
-class Pool {
-   public:
-    explicit Pool(int n) {
-        for (int i = 0; i < n; ++i) th_.emplace_back([this] { run(); });
-    }
-    ~Pool() {
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (auto& t : th_) t.join();
-    }
-    int size() const { return (int)th_.size(); }
-    // Run fn(t) for t in [0, ntasks) across the pool; blocks until all are done.
-    void parallel_for(int ntasks, const std::function<void(int)>& fn) {
-        if (ntasks <= 0) return;
-        std::atomic<int> next{0}, done{0};
-        std::mutex dmu;
-        std::condition_variable dcv;
-        auto body = [&] {
-            for (;;) {
-                const int t = next.fetch_add(1);
-                if (t >= ntasks) break;
-                fn(t);
-                if (done.fetch_add(1) + 1 == ntasks) {
-                    std::lock_guard<std::mutex> g(dmu);
-                    dcv.notify_all();
-                }
-            }
-        };
-        const int nw = std::min(ntasks, size());
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            for (int i = 0; i < nw; ++i) q_.push_back(body);
-        }
-        cv_.notify_all();
-        std::unique_lock<std::mutex> lk(dmu);
-        dcv.wait(lk, [&] { return done.load() == ntasks; });
-        // the helpers may still be returning from `body`; wait until none holds a reference
-        std::unique_lock<std::mutex> g(mu_);
-        idle_cv_.wait(g, [&] { return busy_ == 0 && q_.empty(); });
-    }
-
-   private:
-    void run() {
-        for (;;) {
-            std::function<void()> job;
-            {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
-                if (stop_ && q_.empty()) return;
-                job = std::move(q_.back());
-                q_.pop_back();
-                ++busy_;
-            }
-            job();
-            {
-                std::lock_guard<std::mutex> lk(mu_);
-                --busy_;
-            }
-            idle_cv_.notify_all();
-        }
-    }
-    std::vector<std::thread> th_;
-    std::vector<std::function<void()>> q_;
-    std::mutex mu_;
-    std::condition_variable cv_, idle_cv_;
-    int busy_ = 0;
-    bool stop_ = false;
-};
-
 int default_threads() {
     const char* e = getenv("OXH_NUM_THREADS");  // cf. OXEN_NUM_THREADS (util/concurrency.rs:1-45)
     if (e && atoi(e) > 0) return atoi(e);
@@ -249,7 +178,7 @@ struct oxh_ctx {
     uint64_t* h_cnt[NSLOT] = {};  // text counts (num_lines, num_chars) per item, K1T
     uint64_t* d_cnt[NSLOT] = {};
     hipEvent_t ev_copied[NSLOT] = {}, ev_done[NSLOT] = {};
-    Pool* pool = nullptr;
+    oxh::Pool* pool = nullptr;
     std::mutex mu;
 };
 
@@ -304,23 +233,38 @@ int large_device(oxh_ctx*, const uint8_t* d_buf, uint64_t len, uint64_t* d_out, 
     return large_batch_device(&d_buf, &len, 1, d_out, st);
 }
 
+// OXH_DEBUG_STEPS=1: one stderr line per runtime step (locating stalls without a debugger)
+static const bool g_steps = getenv("OXH_DEBUG_STEPS") != nullptr;
+#define STEP(...)                                  \
+    do {                                           \
+        if (g_steps) {                             \
+            fprintf(stderr, "[oxh-step] " __VA_ARGS__); \
+            fputc('\n', stderr);                   \
+        }                                          \
+    } while (0)
+
 // One staged batch: items [0, cnt) already in h_stage[s] at h_desc offsets; launch and queue D2H.
 int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_only, bool short_items, bool text) {
     const uint64_t M = c->max_items;
+    STEP("submit s=%d bytes=%llu cnt=%llu lane=%d short=%d", s, (unsigned long long)bytes, (unsigned long long)cnt,
+         (int)any_short_only, (int)short_items);
     HIP_TRY(hipMemcpyAsync(c->d_stage[s], c->h_stage[s], bytes, hipMemcpyHostToDevice, c->copy_stream));
     HIP_TRY(hipMemcpyAsync(c->d_desc[s], c->h_desc[s], cnt * 8, hipMemcpyHostToDevice, c->copy_stream));
     HIP_TRY(hipMemcpyAsync(c->d_desc[s] + M, c->h_desc[s] + M, cnt * 8, hipMemcpyHostToDevice, c->copy_stream));
     HIP_TRY(hipEventRecord(c->ev_copied[s], c->copy_stream));
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[s], 0));
+    STEP("copies queued s=%d", s);
     int rc = text ? launch_text(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->d_cnt[s], c->stream,
                                 short_items)
              : any_short_only ? launch_lane(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->stream)
                               : launch_wave(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->stream,
                                             short_items);
     if (rc) return rc;
+    STEP("launched s=%d", s);
     HIP_TRY(hipMemcpyAsync(c->h_out[s], c->d_out[s], cnt * 16, hipMemcpyDeviceToHost, c->stream));
     if (text) HIP_TRY(hipMemcpyAsync(c->h_cnt[s], c->d_cnt[s], cnt * 16, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipEventRecord(c->ev_done[s], c->stream));
+    STEP("submitted s=%d", s);
     return OXH_OK;
 }
 
@@ -343,10 +287,37 @@ struct Pending {
     std::vector<uint64_t> ids;  // caller indices of the staged items
 };
 
+// Wait for slot s's digests. Polls (a slot is at most a few hundred MiB: milliseconds of work) and,
+// after OXH_WAIT_LIMIT_S seconds (default 60), reports which stage never finished instead of
+// blocking forever.
+int wait_slot(oxh_ctx* c, int s, const Pending& p) {
+    static const double limit = getenv("OXH_WAIT_LIMIT_S") ? atof(getenv("OXH_WAIT_LIMIT_S")) : 60.0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spin = 0;; ++spin) {
+        const hipError_t q = hipEventQuery(c->ev_done[s]);
+        if (q == hipSuccess) return OXH_OK;
+        if (q != hipErrorNotReady) return fail(OXH_ERR_HIP, std::string("slot event: ") + hipGetErrorString(q));
+        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        if ((spin & 1023) == 0 &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
+            const uint64_t M = c->max_items;
+            fprintf(stderr, "[oxh] slot %d stalled: items=%zu copied=%s copy_stream=%s stream=%s first lens:", s,
+                    p.ids.size(), hipGetErrorName(hipEventQuery(c->ev_copied[s])),
+                    hipGetErrorName(hipStreamQuery(c->copy_stream)), hipGetErrorName(hipStreamQuery(c->stream)));
+            for (size_t j = 0; j < std::min<size_t>(p.ids.size(), 16); ++j)
+                fprintf(stderr, " %llu@%llu", (unsigned long long)c->h_desc[s][M + j], (unsigned long long)c->h_desc[s][j]);
+            fprintf(stderr, "\n");
+            return fail(OXH_ERR_HIP, "timed out waiting for a staged batch (see stderr)");
+        }
+    }
+}
+
 int drain_slot(oxh_ctx* c, int s, Pending& p, uint64_t* out, uint64_t* counts = nullptr,
                const ItemSink* sink = nullptr, const int32_t* status = nullptr) {
     if (!p.busy) return OXH_OK;
-    HIP_TRY(hipEventSynchronize(c->ev_done[s]));
+    STEP("drain s=%d", s);
+    if (int rc = wait_slot(c, s, p)) return rc;
+    STEP("drained s=%d", s);
     for (size_t j = 0; j < p.ids.size(); ++j) {
         out[2 * p.ids[j]] = c->h_out[s][2 * j];
         out[2 * p.ids[j] + 1] = c->h_out[s][2 * j + 1];
@@ -453,7 +424,7 @@ int oxh_ctx_create(int device, uint64_t staging_bytes, oxh_ctx** out) {
         if (hipEventCreateWithFlags(&c->ev_copied[s], hipEventDisableTiming) != hipSuccess) return cleanup(OXH_ERR_HIP, "event");
         if (hipEventCreateWithFlags(&c->ev_done[s], hipEventDisableTiming) != hipSuccess) return cleanup(OXH_ERR_HIP, "event");
     }
-    c->pool = new Pool(default_threads());
+    c->pool = new oxh::Pool(default_threads());
     *out = c;
     return OXH_OK;
 }
@@ -594,6 +565,7 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
             off += hlen[j];
         }
         // fill it: parallel readers / copiers write straight into pinned memory
+        STEP("fill s=%d items=%zu", s, batch.size());
         std::vector<int32_t> st(batch.size(), OXH_OK);
         const int ntasks = (int)std::min<size_t>(batch.size(), (size_t)c->pool->size() * 4);
         c->pool->parallel_for(ntasks, [&](int t) {
@@ -615,6 +587,7 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
         pend[s].ids = batch;
     }
     double t3 = Trace::now();
+    STEP("final drain");
     for (int s = 0; s < NSLOT; ++s) {
         int rc = drain_slot(c, s, pend[s], out, counts, sink, status);
         if (rc) return rc;
@@ -645,8 +618,10 @@ int oxh_hash_buffers(oxh_ctx* c, const uint8_t* const* bufs, const uint64_t* len
 int oxh_hash_streams(oxh_ctx* c, const uint8_t* streams, const uint64_t* offsets, const uint64_t* lens, uint64_t n,
                      uint64_t* out) {
     if (!c || (n && (!streams || !offsets || !lens || !out))) return fail(OXH_ERR_INVALID, "bad arguments");
+    STEP("hash_streams n=%llu", (unsigned long long)n);
     std::lock_guard<std::mutex> g(c->mu);
     HIP_TRY(hipSetDevice(c->device));
+    STEP("hash_streams locked");
     return hash_host_items(c, n, lens, [&](uint64_t i, uint8_t* dst) {
         if (lens[i]) memcpy(dst, streams + offsets[i], lens[i]);
         return OXH_OK;
@@ -762,7 +737,14 @@ int oxh_add_files(oxh_ctx* c, const char* const* paths, uint64_t n, const char* 
     const std::string root(versions_root ? versions_root : "");
     for (uint64_t i = 0; i < n; ++i) stored[i] = 0;
     std::vector<uint8_t> pub_err(n, 0);
+    // identical content twice in one call: exactly one item publishes (the others find it claimed)
+    std::mutex claim_mu;
+    std::set<std::pair<uint64_t, uint64_t>> claimed;
     ItemSink sink = [&](uint64_t id, const uint8_t* bytes, uint64_t len, uint64_t lo, uint64_t hi) {
+        {
+            std::lock_guard<std::mutex> g(claim_mu);
+            if (!claimed.insert({lo, hi}).second) return;
+        }
         const int r = store_version_blob(root, lo, hi, bytes, len);
         stored[id] = r > 0 ? 1 : 0;
         if (r < 0) pub_err[id] = 1;

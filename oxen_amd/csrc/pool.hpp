@@ -1,0 +1,85 @@
+// oxen_amd/csrc/pool.hpp -- the runtime's blocking thread pool (file readers / copiers / writers).
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace oxh {
+class Pool {
+   public:
+    explicit Pool(int n) {
+        for (int i = 0; i < n; ++i) th_.emplace_back([this] { run(); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    int size() const { return (int)th_.size(); }
+    // Run fn(t) for t in [0, ntasks) across the pool; blocks until all are done.
+    void parallel_for(int ntasks, const std::function<void(int)>& fn) {
+        if (ntasks <= 0) return;
+        std::atomic<int> next{0}, done{0};
+        std::mutex dmu;
+        std::condition_variable dcv;
+        auto body = [&] {
+            for (;;) {
+                const int t = next.fetch_add(1);
+                if (t >= ntasks) break;
+                fn(t);
+                if (done.fetch_add(1) + 1 == ntasks) {
+                    std::lock_guard<std::mutex> g(dmu);
+                    dcv.notify_all();
+                }
+            }
+        };
+        const int nw = std::min(ntasks, size());
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            for (int i = 0; i < nw; ++i) q_.push_back(body);
+        }
+        cv_.notify_all();
+        {
+            std::unique_lock<std::mutex> lk(dmu);
+            dcv.wait(lk, [&] { return done.load() == ntasks; });
+        }  // release dmu: the worker that finished the last task may still be about to take it
+        // the helpers may still be returning from `body`; wait until none holds a reference
+        std::unique_lock<std::mutex> g(mu_);
+        idle_cv_.wait(g, [&] { return busy_ == 0 && q_.empty(); });
+    }
+
+   private:
+    void run() {
+        for (;;) {
+            std::function<void()> job;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+                if (stop_ && q_.empty()) return;
+                job = std::move(q_.back());
+                q_.pop_back();
+                ++busy_;
+            }
+            job();
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                --busy_;
+            }
+            idle_cv_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::vector<std::function<void()>> q_;
+    std::mutex mu_;
+    std::condition_variable cv_, idle_cv_;
+    int busy_ = 0;
+    bool stop_ = false;
+};
+
+}  // namespace oxh

@@ -119,3 +119,17 @@ def test_commit_driver_host_logic(monkeypatch, oracle_lib, second, vnode_size):
     assert {d: h.value for d, h in dh.items()} == rdh
     if vnode_size == 7:
         assert max(len(v[0]) for v in vn.values()) > 1
+
+
+def test_thread_pool_stress(tmp_path):
+    """The runtime's thread pool survives 100 000 back-to-back parallel_for calls of ragged sizes
+    (regression: the caller kept the completion mutex while waiting for the pool to go idle, so the
+    worker finishing the last task could block on it forever)."""
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "pool_stress")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-I", os.path.join(root, "oxen_amd", "csrc"),
+                    os.path.join(root, "tests", "native", "pool_stress.cpp"), "-o", exe], check=True)
+    r = subprocess.run([exe, "100000"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "done" in r.stdout

@@ -115,6 +115,14 @@ def main():
     res["cpu_ref_add_GiBs"] = round(nbytes / res["cpu_ref_add_s"] / 2**30, 2)
     res["add_blobs_written"] = [int(sum(gstored)), int(rstored.sum())]
     res["add_digests_bit_exact"] = [(int(hi) << 64) | int(lo) for lo, hi in rout] == gd
+    # `oxen fsck` over the store the add just built (dry run: counts only), GPU vs the restated loop
+    t0 = time.perf_counter()
+    gf = hasher.clean_corrupted_versions(vroot, dry_run=True, ctx=ctx)
+    res["gpu_fsck_s"] = round(time.perf_counter() - t0, 3)
+    t0 = time.perf_counter()
+    rf = oracle.clean_corrupted_versions(rroot, dry_run=True, threads=a.threads)
+    res["cpu_ref_fsck_s"] = round(time.perf_counter() - t0, 3)
+    res["fsck_counts"] = [{k: gf[k] for k in rf}, rf]
     shutil.rmtree(os.path.join(a.dir, ".oxen_gpu"), ignore_errors=True)
     shutil.rmtree(os.path.join(a.dir, ".oxen_ref"), ignore_errors=True)
 
