@@ -178,7 +178,8 @@ struct oxh_ctx {
     uint64_t* h_cnt[NSLOT] = {};  // text counts (num_lines, num_chars) per item, K1T
     uint64_t* d_cnt[NSLOT] = {};
     hipEvent_t ev_copied[NSLOT] = {}, ev_done[NSLOT] = {};
-    oxh::Pool* pool = nullptr;
+    oxh::Pool* pool = nullptr;   // readers / copiers (fill)
+    oxh::Pool* wpool = nullptr;  // consumers of hashed bytes (fused publish), created on first use
     std::mutex mu;
 };
 
@@ -285,7 +286,16 @@ using ItemSink = std::function<void(uint64_t id, const uint8_t* bytes, uint64_t 
 struct Pending {
     bool busy = false;
     std::vector<uint64_t> ids;  // caller indices of the staged items
+    std::thread consumer;       // runs the ItemSink over the slot's items while the next slot fills
+    ~Pending() {
+        if (consumer.joinable()) consumer.join();
+    }
 };
+
+// The slot's bytes are still being consumed by the sink: wait before the slot is refilled.
+void join_consumer(Pending& p) {
+    if (p.consumer.joinable()) p.consumer.join();
+}
 
 // Wait for slot s's digests. Polls (a slot is at most a few hundred MiB: milliseconds of work) and,
 // after OXH_WAIT_LIMIT_S seconds (default 60), reports which stage never finished instead of
@@ -322,24 +332,29 @@ int drain_slot(oxh_ctx* c, int s, Pending& p, uint64_t* out, uint64_t* counts = 
         out[2 * p.ids[j]] = c->h_out[s][2 * j];
         out[2 * p.ids[j] + 1] = c->h_out[s][2 * j + 1];
     }
-    if (sink) {
-        const uint64_t M = c->max_items;
-        const size_t cnt = p.ids.size();
-        const int ntasks = (int)std::min<size_t>(cnt, (size_t)c->pool->size() * 4);
-        c->pool->parallel_for(ntasks, [&](int t) {
-            for (size_t j = (size_t)t; j < cnt; j += (size_t)ntasks) {
-                const uint64_t id = p.ids[j];
-                if (status && status[id] != OXH_OK) continue;
-                (*sink)(id, c->h_stage[s] + c->h_desc[s][j], c->h_desc[s][M + j], c->h_out[s][2 * j], c->h_out[s][2 * j + 1]);
-            }
-        });
-    }
     if (counts)
         for (size_t j = 0; j < p.ids.size(); ++j) {
             counts[2 * p.ids[j]] = c->h_cnt[s][2 * j];
             counts[2 * p.ids[j] + 1] = c->h_cnt[s][2 * j + 1];
         }
     p.busy = false;
+    if (sink) {
+        // hand the slot to the consumer pool; the caller refills it only after join_consumer()
+        if (!c->wpool) c->wpool = new oxh::Pool(c->pool->size());
+        p.consumer = std::thread([c, s, sink, status, ids = std::move(p.ids)] {
+            const uint64_t M = c->max_items;
+            const size_t cnt = ids.size();
+            const int ntasks = (int)std::min<size_t>(cnt, (size_t)c->wpool->size() * 4);
+            c->wpool->parallel_for(ntasks, [&](int t) {
+                for (size_t j = (size_t)t; j < cnt; j += (size_t)ntasks) {
+                    const uint64_t id = ids[j];
+                    if (status && status[id] != OXH_OK) continue;
+                    (*sink)(id, c->h_stage[s] + c->h_desc[s][j], c->h_desc[s][M + j], c->h_out[s][2 * j],
+                            c->h_out[s][2 * j + 1]);
+                }
+            });
+        });
+    }
     p.ids.clear();
     return OXH_OK;
 }
@@ -449,6 +464,7 @@ int oxh_ctx_destroy(oxh_ctx* c) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     delete c->pool;
+    delete c->wpool;
     delete c;
     return OXH_OK;
 }
@@ -524,6 +540,7 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
                 for (int s = 0; s < NSLOT; ++s) {
                     int rc = drain_slot(c, s, pend[s], out, counts, sink, status);
                     if (rc) return rc;
+                    join_consumer(pend[s]);
                 }
                 std::vector<uint8_t> tmp(L);
                 int st = fill(i, tmp.data());
@@ -548,6 +565,7 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
         slot = (slot + 1) % NSLOT;
         double t0 = Trace::now();
         int rc = drain_slot(c, s, pend[s], out, counts, sink, status);
+        join_consumer(pend[s]);  // this slot's previous bytes were consumed before it is refilled
         if (rc) return rc;
         double t1 = Trace::now();
         tr->drain += t1 - t0;
@@ -585,6 +603,14 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
         tr->batches++;
         pend[s].busy = true;
         pend[s].ids = batch;
+        if (sink) {
+            // publish the previous slot while the next one fills: its digests are due now
+            const int prev = (s + NSLOT - 1) % NSLOT;
+            const double t4 = Trace::now();
+            rc = drain_slot(c, prev, pend[prev], out, counts, sink, status);
+            tr->drain += Trace::now() - t4;
+            if (rc) return rc;
+        }
     }
     double t3 = Trace::now();
     STEP("final drain");
@@ -592,6 +618,7 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
         int rc = drain_slot(c, s, pend[s], out, counts, sink, status);
         if (rc) return rc;
     }
+    for (int s = 0; s < NSLOT; ++s) join_consumer(pend[s]);
     tr->drain += Trace::now() - t3;
     if (tr->on)
         fprintf(stderr, "[oxh] items=%llu batches=%d stat=%.3fs fill=%.3fs drain-wait=%.3fs submit=%.3fs threads=%d\n",
@@ -767,15 +794,20 @@ int oxh_clean_corrupted_versions(oxh_ctx* c, const char* versions_root, int dry_
     if (!c || !versions_root || !result) return fail(OXH_ERR_INVALID, "bad arguments");
     uint64_t errors = 0, scanned = 0, corrupted = 0, cleaned = 0;
     // prefix dirs (local.rs:461-474): anything that is not a directory counts as an error
+    // 1 = directory, 0 = not, -1 = file_type() failed (an error in the reference's counts)
+    auto is_dir = [](const std::string& path, unsigned char d_type) {
+        if (d_type != DT_UNKNOWN) return d_type == DT_DIR ? 1 : 0;  // readdir's type, like DirEntry::file_type
+        struct stat sb;
+        if (lstat(path.c_str(), &sb) != 0) return -1;
+        return S_ISDIR(sb.st_mode) ? 1 : 0;
+    };
     std::vector<std::string> prefixes;
     {
         DIR* d = opendir(versions_root);
         if (!d) return fail(OXH_ERR_IO, std::string("cannot read ") + versions_root);
         while (struct dirent* e = readdir(d)) {
             if (!strcmp(e->d_name, ".") || !strcmp(e->d_name, "..")) continue;
-            const std::string p = std::string(versions_root) + "/" + e->d_name;
-            struct stat sb;
-            if (lstat(p.c_str(), &sb) == 0 && S_ISDIR(sb.st_mode))
+            if (is_dir(std::string(versions_root) + "/" + e->d_name, e->d_type) == 1)
                 prefixes.push_back(e->d_name);
             else
                 ++errors;
@@ -783,29 +815,39 @@ int oxh_clean_corrupted_versions(oxh_ctx* c, const char* versions_root, int dry_
         closedir(d);
     }
     std::sort(prefixes.begin(), prefixes.end());
-    // suffix dirs (local.rs:480-518): non-directories are skipped; expected hash = prefix + suffix
-    std::vector<std::string> dirs, expected, data;
-    for (const std::string& pre : prefixes) {
-        const std::string pdir = std::string(versions_root) + "/" + pre;
+    // suffix dirs (local.rs:480-518), one task per prefix as in the reference: non-directories are
+    // skipped; expected hash = prefix + suffix
+    struct Found {
+        std::vector<std::string> dirs, expected;
+        uint64_t errors = 0;
+    };
+    std::vector<Found> found(prefixes.size());
+    c->pool->parallel_for((int)prefixes.size(), [&](int t) {
+        const std::string pdir = std::string(versions_root) + "/" + prefixes[t];
         DIR* d = opendir(pdir.c_str());
         if (!d) {
-            ++errors;
-            continue;
+            ++found[t].errors;
+            return;
         }
         while (struct dirent* e = readdir(d)) {
             if (!strcmp(e->d_name, ".") || !strcmp(e->d_name, "..")) continue;
-            const std::string sdir = pdir + "/" + e->d_name;
-            struct stat sb;
-            if (lstat(sdir.c_str(), &sb) != 0) {
-                ++errors;
-                continue;
-            }
-            if (!S_ISDIR(sb.st_mode)) continue;
-            dirs.push_back(sdir);
-            expected.push_back(pre + e->d_name);
-            data.push_back(sdir + "/data");
+            std::string sdir = pdir + "/" + e->d_name;
+            const int k = is_dir(sdir, e->d_type);
+            if (k < 0) ++found[t].errors;
+            if (k != 1) continue;
+            found[t].dirs.push_back(std::move(sdir));
+            found[t].expected.push_back(prefixes[t] + e->d_name);
         }
         closedir(d);
+    });
+    std::vector<std::string> dirs, expected, data;
+    for (Found& f : found) {
+        errors += f.errors;
+        for (size_t k = 0; k < f.dirs.size(); ++k) {
+            data.push_back(f.dirs[k] + "/data");
+            dirs.push_back(std::move(f.dirs[k]));
+            expected.push_back(std::move(f.expected[k]));
+        }
     }
     const uint64_t n = dirs.size();
     std::vector<const char*> paths(n);
