@@ -131,6 +131,29 @@ int oxh_hash_files_text(oxh_ctx* ctx, const char* const* paths, uint64_t n, uint
 int oxh_xxh3_128_text_batch_device(const void* d_arena, const uint64_t* d_offsets, const uint64_t* d_lens,
                                    uint64_t n, uint64_t* d_out, uint64_t* d_counts, void* stream);
 
+/* ---------------------------------------------------------------- content-defined chunking
+ * FastCDC v2020 as the block-level dedup experiment runs it (experiments/block-level-dedup/src/
+ * chunker/fastcdchunker.rs:83-98: `v2020::FastCDC::new(&content, 4096, chunk, 2 * chunk)`, crate
+ * fastcdc 3.2.1, Normalization::Level1, then `xxh3_128` of every chunk).
+ *
+ * Chunks n device-resident buffers (file i = d_arena[offsets[i] .. offsets[i] + lens[i]); `offsets`
+ * and `lens` are HOST arrays). On return first_chunk[0..n] (host, n+1 entries) holds each file's
+ * first chunk index; chunk k is d_arena[d_chunk_offsets[k] .. + d_chunk_lens[k]) (device arrays of
+ * `capacity` entries; oxh_fastcdc_max_chunks gives a bound). If d_digests is not NULL it receives
+ * XXH3-128 (lo, hi) of every chunk (2*capacity u64). Parameter ranges are the crate's asserts
+ * (min 64..1 MiB, avg 256..4 MiB, max 1 KiB..16 MiB, level 0..3); out-of-range -> OXH_ERR_INVALID.
+ * Blocks until the chunk table is complete. */
+int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint64_t* lens, uint64_t n,
+                       uint32_t min_size, uint32_t avg_size, uint32_t max_size, uint32_t level,
+                       uint64_t* d_chunk_offsets, uint64_t* d_chunk_lens, uint64_t* d_digests, uint64_t capacity,
+                       uint64_t* first_chunk, void* stream);
+/* Upper bound on the chunk count of files of these lengths (every chunk but a file's last is >= min). */
+uint64_t oxh_fastcdc_max_chunks(const uint64_t* lens, uint64_t n, uint32_t min_size);
+/* The compiled-in GEAR table (256 u64) and the (mask_s, mask_l) pair for an average size and
+ * normalization level (fastcdc v2020 MASKS[bits +/- level], bits = round(log2(avg))). Host only. */
+int oxh_fastcdc_gear(uint64_t* out256);
+int oxh_fastcdc_masks(uint32_t avg_size, uint32_t level, uint64_t* mask_s, uint64_t* mask_l);
+
 /* ---------------------------------------------------------------- K2: merkle parent nodes */
 /* get_combined_hash (hasher.rs:67-80) x n on the device:
  * XXH3-128(content.to_le_bytes() || metadata.to_le_bytes()), inputs as (lo, hi) pairs. */

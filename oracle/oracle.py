@@ -24,9 +24,8 @@ _i32p = ctypes.POINTER(ctypes.c_int32)
 
 def build(force: bool = False) -> str:
     """Compile the oracle with gcc (oracle/Makefile)."""
-    if force or not os.path.exists(LIB_PATH) or (
-        os.path.getmtime(LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "xxh3_oracle.c"))
-    ):
+    srcs = [os.path.join(_HERE, s) for s in ("xxh3_oracle.c", "fastcdc_oracle.c", "Makefile")]
+    if force or not os.path.exists(LIB_PATH) or any(os.path.getmtime(LIB_PATH) < os.path.getmtime(s) for s in srcs):
         subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return LIB_PATH
 

@@ -25,6 +25,7 @@ OXH_MODE_LANE = 2
 OXH_MODE_WAVE_SHORT = 3
 
 _u64 = ctypes.c_uint64
+_u32 = ctypes.c_uint32
 _u64p = ctypes.POINTER(ctypes.c_uint64)
 _i32p = ctypes.POINTER(ctypes.c_int32)
 _vp = ctypes.c_void_p
@@ -54,6 +55,10 @@ SIGNATURES = {
     "oxh_format_dec": (_int, [_u64, _u64, ctypes.c_char_p]),
     "oxh_fill_splitmix": (_int, [_vp, _u64, _u64, _vp]),
     "oxh_set_kernel_variant": (_int, [_int]),
+    "oxh_fastcdc_device": (_int, [_vp, _u64p, _u64p, _u64, _u32, _u32, _u32, _u32, _vp, _vp, _vp, _u64, _u64p, _vp]),
+    "oxh_fastcdc_max_chunks": (_u64, [_u64p, _u64, _u32]),
+    "oxh_fastcdc_gear": (_int, [_u64p]),
+    "oxh_fastcdc_masks": (_int, [_u32, _u32, _u64p, _u64p]),
 }
 
 _lib = None

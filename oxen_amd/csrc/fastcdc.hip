@@ -1,0 +1,559 @@
+// oxen_amd/csrc/fastcdc.hip -- FastCDC v2020 content-defined chunk boundaries on gfx950
+// (block-level dedup), and the chunk digests behind them.
+//
+// Reference: experiments/block-level-dedup/src/chunker/fastcdchunker.rs:83-98 calls
+// `fastcdc::v2020::FastCDC::new(&content, 4096, chunk, 2 * chunk)` (crate fastcdc 3.2.1, not
+// vendored) and names every chunk by the decimal xxh3_128 of its bytes. The crate's cut_gear rolls
+// a 64-bit gear hash `h = (h << 1) + GEAR[b]` from index `min` of every chunk and cuts at the first
+// position whose hash has no bit of mask_s (before `avg`) or mask_l (after it); else at `max`.
+//
+// The walk is serial per file (each cut decides where the next chunk's hash starts). The GPU
+// formulation splits it into three kernels:
+//   F1 cdc_scan_kernel    chip-wide, one wave per 256 KiB section, HBM-bound: the FULL-window gear
+//                         hash at every byte (all mask bits are below bit 48, so only the last 48
+//                         bytes matter and the hash of position p is a function of b[p-47 .. p]) and
+//                         a compact, position-ordered list of candidate positions per section
+//                         (flag bit 0: hash & mask_s == 0, bit 1: hash & mask_l == 0).
+//   F2 cdc_walk_kernel    one lane per section: a speculative walk that assumes a chunk starts at
+//                         the section start and cuts chunks from the candidate lists until it passes
+//                         the section end. The first 47 positions after a chunk's `min` see a hash
+//                         that started from 0 (truncated window); the walk recomputes those from the
+//                         bytes, everything later comes from the candidates.
+//   F3 cdc_stitch_kernel  one lane per file: follows the true walk section by section; as soon as
+//                         it lands on a start the speculative walk of that section also produced,
+//                         the rest of that section's list is exact (cut points depend only on the
+//                         chunk start), so it is copied; otherwise it walks on by itself.
+// Then the chunk table is compacted and K1 hashes every chunk (oxh_xxh3_128_batch_device).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "../../include/oxen_hash.h"
+#include "fastcdc_gear.h"
+
+namespace oxh {
+
+int set_error(int code, const std::string& msg);  // oxen_hash_capi.hip: oxh_last_error() text
+
+// fastcdc::v2020::MASKS, indexed by the number of one bits (entries 0..4 are padding)
+static constexpr uint64_t kCdcMasks[26] = {
+    0, 0, 0, 0, 0,
+    0x0000000001804110ULL, 0x0000000001803110ULL, 0x0000000018035100ULL, 0x0000001800035300ULL,
+    0x0000019000353000ULL, 0x0000590003530000ULL, 0x0000d90003530000ULL, 0x0000d90103530000ULL,
+    0x0000d90303530000ULL, 0x0000d90313530000ULL, 0x0000d90f03530000ULL, 0x0000d90303537000ULL,
+    0x0000d90703537000ULL, 0x0000d90707537000ULL, 0x0000d91707537000ULL, 0x0000d91747537000ULL,
+    0x0000d91767537000ULL, 0x0000d93767537000ULL, 0x0000d93777537000ULL, 0x0000d93777577000ULL,
+    0x0000db3777577000ULL,
+};
+
+constexpr uint32_t kSecDefault = 256 * 1024;  // section bytes (F1 wave / F2 lane unit)
+constexpr int kHashSpan = 47;          // positions after a chunk's start index with a truncated window
+
+struct CdcParams {
+    uint64_t min, avg, max;
+    uint64_t mask_s, mask_l;
+    uint64_t sec;      // section bytes: a multiple of 1 KiB
+    uint32_t cap;      // candidate entries stored per section
+    uint32_t speccap;  // speculative chunk starts stored per section
+};
+
+struct CdcFiles {
+    const uint8_t* arena;
+    const uint64_t* foff;      // [n] arena offset of each file
+    const uint64_t* flen;      // [n]
+    const uint64_t* sec_base;  // [n+1] first global section of each file
+    const uint32_t* sec_file;  // [n_sec] file of each section
+    uint32_t* cand;            // [n_sec * cap] (rel_pos << 2 | flags), position order
+    uint32_t* cand_cnt;        // [n_sec] true count (> cap: list truncated, dense fallback)
+    uint32_t* spec;            // [n_sec * speccap] speculative starts, relative to section start
+    uint32_t* spec_cnt;        // [n_sec]
+};
+
+__device__ __forceinline__ uint64_t gear_of(const uint64_t* __restrict__ g, uint32_t b) { return g[b]; }
+
+// ---------------------------------------------------------------- F1: candidates
+// Lane l of the wave owns bytes [16l, 16l+16) of a 1 KiB sub-block. Its first byte's hash needs the
+// state at the byte before it: H = hl(l-1) + hl(l-2) << 16 + hl(l-3) << 32 (mod the 48 live bits),
+// with hl(m) the hash lane m's 16 bytes alone produce from 0. Lanes 0..2 take lanes 61..63 of the
+// previous sub-block. Candidates are rare (~2^-bits), so the fast path only tests the bits the two
+// masks share and a rare path recomputes both flags for the sub-block.
+__global__ __launch_bounds__(256) void cdc_scan_kernel(CdcFiles f, CdcParams prm, uint64_t n_sec) {
+    __shared__ uint64_t lds_gear[256];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) lds_gear[i] = kGear[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const uint64_t sec = (uint64_t)blockIdx.x * 4 + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (sec >= n_sec) return;
+    const uint32_t file = f.sec_file[sec];
+    const uint64_t flen = f.flen[file];
+    const uint64_t sec_start = (sec - f.sec_base[file]) * prm.sec;
+    const uint64_t sec_len = flen - sec_start < prm.sec ? flen - sec_start : prm.sec;
+    const uint8_t* __restrict__ base = f.arena + f.foff[file] + sec_start;
+    const uint64_t common = prm.mask_s & prm.mask_l;
+    const uint32_t ch = (uint32_t)(common >> 32), cl = (uint32_t)common;
+    uint32_t* __restrict__ out = f.cand + sec * prm.cap;
+    uint32_t count = 0;  // wave-uniform
+
+    // carries: hl of the 3 lanes before lane 0 (bytes [-48, 0) of the section); zero at file start
+    // (positions < 47 of a file are never tested: every tested position is >= min + 47 >= 111)
+    uint64_t c1 = 0, c2 = 0, c3 = 0;  // hl of lanes 63, 62, 61 of the previous sub-block
+    if (sec_start > 0) {
+        // lanes 0..2 load the 48 bytes before the section: lane j holds bytes [-48 + 16j, -32 + 16j)
+        uint64_t hl = 0;
+        if (lane < 3) {
+            uint4 d;
+            __builtin_memcpy(&d, base - 48 + 16 * lane, 16);
+            const uint32_t w[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+            for (int j = 0; j < 16; ++j) hl = (hl << 1) + lds_gear[(w[j >> 2] >> (8 * (j & 3))) & 0xFF];
+        }
+        const uint64_t h0 = ((uint64_t)__builtin_amdgcn_readlane((int)(hl >> 32), 0) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)hl, 0);
+        const uint64_t h1 = ((uint64_t)__builtin_amdgcn_readlane((int)(hl >> 32), 1) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)hl, 1);
+        const uint64_t h2 = ((uint64_t)__builtin_amdgcn_readlane((int)(hl >> 32), 2) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)hl, 2);
+        c1 = h2;
+        c2 = h1;
+        c3 = h0;
+    }
+
+    const uint64_t nsub = (sec_len + 1023) >> 10;
+    for (uint64_t sb = 0; sb < nsub; ++sb) {
+        const uint64_t off = sb * 1024 + 16 * (uint64_t)lane;
+        const uint64_t live = off < sec_len ? (sec_len - off < 16 ? sec_len - off : 16) : 0;
+        uint32_t w[4] = {0, 0, 0, 0};
+        if (live == 16) {
+            uint4 d;
+            __builtin_memcpy(&d, base + off, 16);
+            w[0] = d.x;
+            w[1] = d.y;
+            w[2] = d.z;
+            w[3] = d.w;
+        } else if (live > 0) {  // the section's last partial 16 B: byte loads, constant indices
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                if ((uint64_t)j < live) w[j >> 2] |= (uint32_t)base[off + j] << (8 * (j & 3));
+        }
+        uint64_t g[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) g[j] = lds_gear[(w[j >> 2] >> (8 * (j & 3))) & 0xFF];
+        uint64_t hl = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) hl = (hl << 1) + g[j];
+        // previous three lanes' hl (lanes 0..2 from the carries)
+        const int hi = (int)(hl >> 32), lo = (int)(uint32_t)hl;
+        uint64_t p1 = ((uint64_t)(uint32_t)__shfl_up(hi, 1, 64) << 32) | (uint32_t)__shfl_up(lo, 1, 64);
+        uint64_t p2 = ((uint64_t)(uint32_t)__shfl_up(hi, 2, 64) << 32) | (uint32_t)__shfl_up(lo, 2, 64);
+        uint64_t p3 = ((uint64_t)(uint32_t)__shfl_up(hi, 3, 64) << 32) | (uint32_t)__shfl_up(lo, 3, 64);
+        if (lane == 0) { p1 = c1; p2 = c2; p3 = c3; }
+        if (lane == 1) { p2 = c1; p3 = c2; }
+        if (lane == 2) { p3 = c1; }
+        const uint64_t H = p1 + (p2 << 16) + (p3 << 32);
+        uint64_t h = H;
+        uint32_t anyz = 0xFFFFFFFFu;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            h = (h << 1) + g[j];
+            const uint32_t m = ((uint32_t)(h >> 32) & ch) | ((uint32_t)h & cl);
+            anyz = m < anyz ? m : anyz;
+        }
+        // bytes past the section end are not positions of this section
+        const bool maybe = (anyz == 0) && live > 0;
+        if (__builtin_amdgcn_ballot_w64(maybe) != 0) {
+            uint32_t fs = 0, fl = 0;  // per-byte flags of this lane
+            if (maybe) {
+                h = H;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    h = (h << 1) + g[j];
+                    if ((uint64_t)j < live) {
+                        fs |= ((h & prm.mask_s) == 0 ? 1u : 0u) << j;
+                        fl |= ((h & prm.mask_l) == 0 ? 1u : 0u) << j;
+                    }
+                }
+            }
+            const uint32_t any = fs | fl;
+            const uint32_t c = (uint32_t)__builtin_popcount(any);
+            // inclusive prefix over lanes
+            uint32_t incl = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = (uint32_t)__shfl_up((int)incl, o, 64);
+                if (lane >= o) incl += t;
+            }
+            uint32_t idx = count + incl - c;
+            uint32_t rest = any;
+            while (rest) {
+                const int j = __builtin_ctz(rest);
+                rest &= rest - 1;
+                if (idx < prm.cap)
+                    out[idx] = ((uint32_t)(off + j) << 2) | ((fs >> j) & 1u) | (((fl >> j) & 1u) << 1);
+                ++idx;
+            }
+            count += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        }
+        // carries for the next sub-block: hl of lanes 63, 62, 61
+        c1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(hi, 63) << 32) | (uint32_t)__builtin_amdgcn_readlane(lo, 63);
+        c2 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(hi, 62) << 32) | (uint32_t)__builtin_amdgcn_readlane(lo, 62);
+        c3 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(hi, 61) << 32) | (uint32_t)__builtin_amdgcn_readlane(lo, 61);
+    }
+    if (lane == 0) f.cand_cnt[sec] = count;
+}
+
+// ---------------------------------------------------------------- the walk (F2, F3)
+// Cursor over the candidate lists of one file, monotone in position.
+struct CandCursor {
+    uint64_t sec;  // global section index of the cursor
+    uint32_t idx;  // entry index within that section's list
+};
+
+// Full-window hash test of positions [lo, hi) (all inside one file, lo >= 47) by direct byte scan:
+// used where a section's candidate list overflowed. Returns the first position with
+// (hash & mask) == 0, or hi.
+__device__ uint64_t scan_bytes(const uint8_t* __restrict__ fbase, uint64_t lo, uint64_t hi, uint64_t mask,
+                               const uint64_t* __restrict__ gear) {
+    uint64_t h = 0;
+    for (uint64_t p = lo - kHashSpan; p < lo; ++p) h = (h << 1) + gear_of(gear, fbase[p]);
+    for (uint64_t p = lo; p < hi; ++p) {
+        h = (h << 1) + gear_of(gear, fbase[p]);
+        if ((h & mask) == 0) return p;
+    }
+    return hi;
+}
+
+// First position in [lo, hi) (file-relative) whose full-window hash matches `flag` (1: mask_s,
+// 2: mask_l), or hi. Advances the cursor (callers query increasing positions).
+__device__ uint64_t first_cand(const CdcFiles& f, const CdcParams& prm, uint64_t sec0, uint64_t nsec_file,
+                               const uint8_t* fbase, CandCursor& cur, uint64_t lo, uint64_t hi, uint32_t flag,
+                               const uint64_t* gear) {
+    if (lo >= hi) return hi;
+    uint64_t s = lo / prm.sec;
+    if (cur.sec < sec0 + s) {
+        cur.sec = sec0 + s;
+        cur.idx = 0;
+    }
+    if (cur.sec >= sec0 + nsec_file) return hi;
+    while (true) {
+        const uint64_t sec_start = (cur.sec - sec0) * prm.sec;
+        if (sec_start >= hi) return hi;
+        const uint32_t* list = f.cand + cur.sec * prm.cap;
+        const uint32_t cnt = f.cand_cnt[cur.sec];
+        const uint32_t stored = cnt < prm.cap ? cnt : prm.cap;
+        while (cur.idx < stored) {
+            const uint32_t e = list[cur.idx];
+            const uint64_t p = sec_start + (e >> 2);
+            if (p >= hi) return hi;
+            if (p >= lo && (e & flag)) return p;
+            // below lo, or in range without the flag: later queries start at or after this one's
+            // end (an L query follows an S query from eS on), so the entry is never needed again
+            ++cur.idx;
+        }
+        const uint64_t sec_end = sec_start + prm.sec;
+        if (cnt > prm.cap) {
+            // overflowed list: positions after the last stored entry were not recorded
+            const uint64_t after = stored ? sec_start + (list[stored - 1] >> 2) + 1 : sec_start;
+            const uint64_t a = lo > after ? lo : after;
+            const uint64_t b = hi < sec_end ? hi : sec_end;
+            if (a < b) {
+                const uint64_t m = scan_bytes(fbase, a, b, flag == 1 ? prm.mask_s : prm.mask_l, gear);
+                if (m < b) return m;
+            }
+        }
+        // move to the next section only if the query reaches into it: a later query (the L range
+        // after an S range) may still need this section
+        if (sec_end >= hi || cur.sec + 1 >= sec0 + nsec_file) return hi;
+        ++cur.sec;
+        cur.idx = 0;
+    }
+}
+
+// Length of the chunk that starts at file-relative position s (cut_gear on content[s..]).
+__device__ uint64_t cdc_cut(const CdcFiles& f, const CdcParams& prm, uint64_t sec0, uint64_t nsec_file,
+                            const uint8_t* fbase, uint64_t flen, uint64_t s, CandCursor& cur,
+                            const uint64_t* gear) {
+    uint64_t rem = flen - s;
+    if (rem <= prm.min) return rem;
+    uint64_t center = prm.avg;
+    if (rem > prm.max) rem = prm.max;
+    else if (rem < center) center = rem;
+    const uint64_t a0 = (prm.min / 2) * 2, eS = (center / 2) * 2, eL = (rem / 2) * 2;
+    // truncated window: the hash restarts from 0 at a0
+    uint64_t h = 0;
+    const uint64_t tend = a0 + kHashSpan < eL ? a0 + kHashSpan : eL;
+    for (uint64_t q = a0; q < tend; ++q) {
+        h = (h << 1) + gear_of(gear, fbase[s + q]);
+        if ((h & (q < eS ? prm.mask_s : prm.mask_l)) == 0) return q;
+    }
+    const uint64_t qs = a0 + kHashSpan;
+    if (qs < eS) {
+        const uint64_t p = first_cand(f, prm, sec0, nsec_file, fbase, cur, s + qs, s + eS, 1u, gear);
+        if (p < s + eS) return p - s;
+    }
+    const uint64_t ql = qs > eS ? qs : eS;
+    if (ql < eL) {
+        const uint64_t p = first_cand(f, prm, sec0, nsec_file, fbase, cur, s + ql, s + eL, 2u, gear);
+        if (p < s + eL) return p - s;
+    }
+    return rem;
+}
+
+// F2: speculative walk of one section from its start, recording chunk starts (relative to the
+// section start) until a start reaches the section end or the file end (that start is recorded too).
+__global__ __launch_bounds__(256) void cdc_walk_kernel(CdcFiles f, CdcParams prm, uint64_t n_sec) {
+    __shared__ uint64_t lds_gear[256];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) lds_gear[i] = kGear[i];
+    __syncthreads();
+    const uint64_t sec = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (sec >= n_sec) return;
+    const uint32_t file = f.sec_file[sec];
+    const uint64_t flen = f.flen[file];
+    const uint64_t sec0 = f.sec_base[file], nsec_file = f.sec_base[file + 1] - sec0;
+    const uint64_t sec_start = (sec - sec0) * prm.sec;
+    const uint64_t sec_end = sec_start + prm.sec < flen ? sec_start + prm.sec : flen;
+    const uint8_t* fbase = f.arena + f.foff[file];
+    uint32_t* out = f.spec + sec * prm.speccap;
+    CandCursor cur{sec, 0};
+    uint64_t s = sec_start;
+    uint32_t n = 0;
+    while (true) {
+        if (n < prm.speccap) out[n] = (uint32_t)(s - sec_start);
+        ++n;
+        if ((s >= sec_end && n > 1) || s >= flen) break;
+        s += cdc_cut(f, prm, sec0, nsec_file, fbase, flen, s, cur, lds_gear);
+    }
+    f.spec_cnt[sec] = n;
+}
+
+// F3: the true walk of one file, stitched from the speculative lists. Writes the file's chunk starts
+// (file-relative) to starts[out_base[file] ...] and the count to nchunks[file].
+__global__ __launch_bounds__(64) void cdc_stitch_kernel(CdcFiles f, CdcParams prm, uint64_t n_files,
+                                                         const uint64_t* __restrict__ out_base,
+                                                         uint64_t* __restrict__ starts,
+                                                         uint64_t* __restrict__ nchunks) {
+    __shared__ uint64_t lds_gear[256];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) lds_gear[i] = kGear[i];
+    __syncthreads();
+    const uint64_t file = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (file >= n_files) return;
+    const uint64_t flen = f.flen[file];
+    const uint64_t sec0 = f.sec_base[file], nsec_file = f.sec_base[file + 1] - sec0;
+    const uint8_t* fbase = f.arena + f.foff[file];
+    uint64_t* out = starts + out_base[file];
+    uint64_t n = 0, pos = 0;
+    CandCursor cur{sec0, 0};
+    for (uint64_t i = 0; i < nsec_file && pos < flen; ++i) {
+        const uint64_t sec = sec0 + i;
+        const uint64_t sec_start = i * prm.sec;
+        const uint64_t sec_end = sec_start + prm.sec < flen ? sec_start + prm.sec : flen;
+        if (pos >= sec_end) continue;
+        const uint32_t* spec = f.spec + sec * prm.speccap;
+        const uint32_t scnt = f.spec_cnt[sec];
+        const bool spec_ok = scnt <= prm.speccap;
+        uint32_t k = 0;
+        while (pos < sec_end) {
+            if (spec_ok) {
+                while (k < scnt && sec_start + spec[k] < pos) ++k;
+                if (k < scnt && sec_start + spec[k] == pos) {
+                    // converged: the rest of this section's speculative list is the true walk
+                    for (; k < scnt; ++k) {
+                        const uint64_t st = sec_start + spec[k];
+                        if (st >= sec_end || st >= flen) {
+                            pos = st;
+                            break;
+                        }
+                        out[n++] = st;
+                    }
+                    break;
+                }
+            }
+            out[n++] = pos;
+            if (cur.sec < sec) cur = CandCursor{sec, 0};
+            pos += cdc_cut(f, prm, sec0, nsec_file, fbase, flen, pos, cur, lds_gear);
+        }
+    }
+    nchunks[file] = n;
+}
+
+// Final chunk table: arena offset and length of every chunk, files in order.
+__global__ __launch_bounds__(256) void cdc_compact_kernel(const uint64_t* __restrict__ foff,
+                                                          const uint64_t* __restrict__ flen,
+                                                          const uint64_t* __restrict__ out_base,
+                                                          const uint64_t* __restrict__ starts,
+                                                          const uint64_t* __restrict__ first,  // [n+1] prefix of counts
+                                                          uint64_t n_files, uint64_t* __restrict__ c_off,
+                                                          uint64_t* __restrict__ c_len) {
+    // one block per file, threads stride its chunks
+    const uint64_t file = blockIdx.x;
+    if (file >= n_files) return;
+    const uint64_t n = first[file + 1] - first[file];
+    const uint64_t* st = starts + out_base[file];
+    for (uint64_t k = threadIdx.x; k < n; k += blockDim.x) {
+        const uint64_t a = st[k];
+        const uint64_t b = k + 1 < n ? st[k + 1] : flen[file];
+        c_off[first[file] + k] = foff[file] + a;
+        c_len[first[file] + k] = b - a;
+    }
+}
+
+}  // namespace oxh
+
+// ---------------------------------------------------------------- host side
+namespace {
+
+int cdc_fail(int code, const std::string& msg) { return oxh::set_error(code, msg); }
+
+#define CDC_HIP(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess) return cdc_fail(OXH_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+uint32_t log2_round(uint32_t v) {
+    const uint32_t b = 31 - (uint32_t)__builtin_clz(v);
+    const double x = (double)v, lo = (double)(1u << b);
+    return (x * x >= 2.0 * lo * lo) ? b + 1 : b;
+}
+
+// stream-ordered scratch, freed on every exit path
+struct Scratch {
+    hipStream_t st;
+    std::vector<void*> ptrs;
+    explicit Scratch(hipStream_t s) : st(s) {}
+    ~Scratch() {
+        for (void* p : ptrs) (void)hipFreeAsync(p, st);
+    }
+    template <class T>
+    hipError_t alloc(T** p, uint64_t count) {
+        const hipError_t e = hipMallocAsync((void**)p, std::max<uint64_t>(count, 1) * sizeof(T), st);
+        if (e == hipSuccess) ptrs.push_back(*p);
+        return e;
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int oxh_fastcdc_gear(uint64_t* out256) {
+    if (!out256) return cdc_fail(OXH_ERR_INVALID, "null output");
+    memcpy(out256, oxh::kGear, sizeof(oxh::kGear));
+    return OXH_OK;
+}
+
+int oxh_fastcdc_masks(uint32_t avg_size, uint32_t level, uint64_t* mask_s, uint64_t* mask_l) {
+    if (avg_size < 256 || avg_size > 4194304 || level > 3)
+        return cdc_fail(OXH_ERR_INVALID, "avg_size must be in [256, 4194304] and level in 0..3");
+    const uint32_t bits = log2_round(avg_size);
+    if (mask_s) *mask_s = oxh::kCdcMasks[bits + level];
+    if (mask_l) *mask_l = oxh::kCdcMasks[bits - level];
+    return OXH_OK;
+}
+
+uint64_t oxh_fastcdc_max_chunks(const uint64_t* lens, uint64_t n, uint32_t min_size) {
+    uint64_t t = 0;
+    for (uint64_t i = 0; i < n; ++i) t += lens[i] ? (lens[i] + min_size - 1) / std::max<uint32_t>(min_size, 1) : 0;
+    return t;
+}
+
+int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint64_t* lens, uint64_t n,
+                       uint32_t min_size, uint32_t avg_size, uint32_t max_size, uint32_t level,
+                       uint64_t* d_chunk_offsets, uint64_t* d_chunk_lens, uint64_t* d_digests, uint64_t capacity,
+                       uint64_t* first_chunk, void* stream) {
+    // v2020::FastCDC::with_level asserts (crate fastcdc 3.2.1)
+    if (min_size < 64 || min_size > 1048576) return cdc_fail(OXH_ERR_INVALID, "min_size must be in [64, 1048576]");
+    if (avg_size < 256 || avg_size > 4194304) return cdc_fail(OXH_ERR_INVALID, "avg_size must be in [256, 4194304]");
+    if (max_size < 1024 || max_size > 16777216) return cdc_fail(OXH_ERR_INVALID, "max_size must be in [1024, 16777216]");
+    if (level > 3) return cdc_fail(OXH_ERR_INVALID, "normalization level must be 0..3");
+    if (n > 0 && (!d_arena || !offsets || !lens || !first_chunk)) return cdc_fail(OXH_ERR_INVALID, "null argument");
+    if (!first_chunk) return cdc_fail(OXH_ERR_INVALID, "null first_chunk");
+    hipStream_t st = (hipStream_t)stream;
+    first_chunk[0] = 0;
+    if (n == 0) return OXH_OK;
+
+    oxh::CdcParams prm{};
+    prm.min = min_size;
+    prm.avg = avg_size;
+    prm.max = max_size;
+    int rc = oxh_fastcdc_masks(avg_size, level, &prm.mask_s, &prm.mask_l);
+    if (rc) return rc;
+    // candidate density ~ 2^-popcount(mask) per byte; store 8x the expected count (+64) per section,
+    // at most one per 64 B; a denser section keeps a truncated list and the walk scans its bytes
+    const double dens = std::ldexp(1.0, -__builtin_popcountll(prm.mask_s)) + std::ldexp(1.0, -__builtin_popcountll(prm.mask_l));
+    prm.sec = oxh::kSecDefault;
+    if (const char* e = getenv("OXH_CDC_SECTION_BYTES")) {  // tests: many small sections per file
+        const uint64_t v = strtoull(e, nullptr, 10);
+        if (v >= 1024 && v % 1024 == 0 && v <= (1u << 30)) prm.sec = v;
+    }
+    prm.cap = (uint32_t)std::min<double>(prm.sec / 64, 8.0 * dens * prm.sec + 64);
+    prm.speccap = (uint32_t)(prm.sec / min_size + 2 + (max_size + min_size - 1) / min_size);
+
+    std::vector<uint64_t> sec_base(n + 1), out_base(n + 1);
+    sec_base[0] = out_base[0] = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t L = lens[i];
+        sec_base[i + 1] = sec_base[i] + (L + prm.sec - 1) / prm.sec;
+        out_base[i + 1] = out_base[i] + (L + min_size - 1) / min_size + 1;
+    }
+    const uint64_t n_sec = sec_base[n];
+    std::vector<uint32_t> sec_file(std::max<uint64_t>(n_sec, 1));
+    for (uint64_t i = 0; i < n; ++i)
+        for (uint64_t s = sec_base[i]; s < sec_base[i + 1]; ++s) sec_file[s] = (uint32_t)i;
+
+    Scratch sc(st);
+    uint64_t *d_foff, *d_flen, *d_sec_base, *d_out_base, *d_starts, *d_nchunks, *d_first;
+    uint32_t *d_sec_file, *d_cand, *d_cand_cnt, *d_spec, *d_spec_cnt;
+    CDC_HIP(sc.alloc(&d_foff, n));
+    CDC_HIP(sc.alloc(&d_flen, n));
+    CDC_HIP(sc.alloc(&d_sec_base, n + 1));
+    CDC_HIP(sc.alloc(&d_out_base, n + 1));
+    CDC_HIP(sc.alloc(&d_nchunks, n));
+    CDC_HIP(sc.alloc(&d_first, n + 1));
+    CDC_HIP(sc.alloc(&d_starts, out_base[n]));
+    CDC_HIP(sc.alloc(&d_sec_file, n_sec));
+    CDC_HIP(sc.alloc(&d_cand, n_sec * prm.cap));
+    CDC_HIP(sc.alloc(&d_cand_cnt, n_sec));
+    CDC_HIP(sc.alloc(&d_spec, n_sec * prm.speccap));
+    CDC_HIP(sc.alloc(&d_spec_cnt, n_sec));
+    CDC_HIP(hipMemcpyAsync(d_foff, offsets, n * 8, hipMemcpyHostToDevice, st));
+    CDC_HIP(hipMemcpyAsync(d_flen, lens, n * 8, hipMemcpyHostToDevice, st));
+    CDC_HIP(hipMemcpyAsync(d_sec_base, sec_base.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+    CDC_HIP(hipMemcpyAsync(d_out_base, out_base.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+    if (n_sec) CDC_HIP(hipMemcpyAsync(d_sec_file, sec_file.data(), n_sec * 4, hipMemcpyHostToDevice, st));
+
+    oxh::CdcFiles f{(const uint8_t*)d_arena, d_foff, d_flen, d_sec_base, d_sec_file, d_cand, d_cand_cnt, d_spec, d_spec_cnt};
+    if (n_sec) {
+        hipLaunchKernelGGL(oxh::cdc_scan_kernel, dim3((unsigned)((n_sec + 3) / 4)), dim3(256), 0, st, f, prm, n_sec);
+        CDC_HIP(hipGetLastError());
+        hipLaunchKernelGGL(oxh::cdc_walk_kernel, dim3((unsigned)((n_sec + 255) / 256)), dim3(256), 0, st, f, prm, n_sec);
+        CDC_HIP(hipGetLastError());
+    }
+    hipLaunchKernelGGL(oxh::cdc_stitch_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, f, prm, n, d_out_base,
+                       d_starts, d_nchunks);
+    CDC_HIP(hipGetLastError());
+    std::vector<uint64_t> counts(n);
+    CDC_HIP(hipMemcpyAsync(counts.data(), d_nchunks, n * 8, hipMemcpyDeviceToHost, st));
+    CDC_HIP(hipStreamSynchronize(st));
+    for (uint64_t i = 0; i < n; ++i) first_chunk[i + 1] = first_chunk[i] + counts[i];
+    const uint64_t total = first_chunk[n];
+    if (total > capacity)
+        return cdc_fail(OXH_ERR_INVALID, "chunk capacity too small: need " + std::to_string(total) + " entries");
+    if (total && (!d_chunk_offsets || !d_chunk_lens)) return cdc_fail(OXH_ERR_INVALID, "null chunk table");
+    CDC_HIP(hipMemcpyAsync(d_first, first_chunk, (n + 1) * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(oxh::cdc_compact_kernel, dim3((unsigned)n), dim3(256), 0, st, d_foff, d_flen, d_out_base, d_starts,
+                       d_first, n, d_chunk_offsets, d_chunk_lens);
+    CDC_HIP(hipGetLastError());
+    if (d_digests && total) {
+        const int mode = avg_size <= 16384 ? OXH_MODE_WAVE_SHORT : OXH_MODE_WAVE;
+        rc = oxh_xxh3_128_batch_device(d_arena, d_chunk_offsets, d_chunk_lens, total, d_digests, mode, stream);
+        if (rc) return cdc_fail(rc, std::string("chunk digests: ") + oxh_last_error());
+    }
+    // the host vectors above were read by stream-ordered copies: finish before they go out of scope
+    CDC_HIP(hipStreamSynchronize(st));
+    return OXH_OK;
+}
+
+}  // extern "C"

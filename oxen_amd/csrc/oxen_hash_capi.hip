@@ -164,6 +164,11 @@ int default_threads() {
 
 }  // namespace
 
+namespace oxh {
+// for the other translation units of the library (fastcdc.hip)
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace oxh
+
 // ---------------------------------------------------------------- context
 struct oxh_ctx {
     int device = 0;

@@ -117,6 +117,34 @@ def fill_splitmix(buf: torch.Tensor, seed: int, nbytes: Optional[int] = None, st
     _capi.check(_capi.lib().oxh_fill_splitmix(buf.data_ptr(), nbytes, int(seed), _stream(stream)), "oxh_fill_splitmix")
 
 
+def fastcdc_device(arena: torch.Tensor, offsets, lens, min_size: int, avg_size: int, max_size: int,
+                   level: int = 1, digests: bool = True, stream=None):
+    """FastCDC v2020 chunks (+ XXH3-128 of every chunk) of device-resident files
+    arena[offsets[i] : offsets[i] + lens[i]] (offsets/lens are host sequences).
+    Returns (chunk_offsets, chunk_lens, chunk_digests or None) as int64 device tensors and
+    first_chunk (numpy uint64, n+1): file i's chunks are rows first_chunk[i] .. first_chunk[i+1]."""
+    _require_cuda(arena)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ln = np.ascontiguousarray(lens, dtype=np.uint64)
+    n = len(ln)
+    if len(offs) != n:
+        raise _capi.OxenError("offsets/lens must be the same length", _capi.OXH_ERR_INVALID)
+    if n and int((offs + ln).max()) > arena.numel() * arena.element_size():
+        raise _capi.OxenError("a file extends past the arena", _capi.OXH_ERR_INVALID)
+    L = _capi.lib()
+    cap = max(1, int(L.oxh_fastcdc_max_chunks(ln.ctypes.data_as(_capi._u64p), n, max(1, int(min_size)))))
+    c_off = torch.empty(cap, dtype=torch.int64, device=arena.device)
+    c_len = torch.empty(cap, dtype=torch.int64, device=arena.device)
+    dig = torch.empty((cap, 2), dtype=torch.int64, device=arena.device) if digests else None
+    first = np.zeros(n + 1, dtype=np.uint64)
+    _capi.check(L.oxh_fastcdc_device(arena.data_ptr(), offs.ctypes.data_as(_capi._u64p), ln.ctypes.data_as(_capi._u64p),
+                                     n, int(min_size), int(avg_size), int(max_size), int(level), c_off.data_ptr(),
+                                     c_len.data_ptr(), dig.data_ptr() if dig is not None else None, cap,
+                                     first.ctypes.data_as(_capi._u64p), _stream(stream)), "oxh_fastcdc_device")
+    total = int(first[n])
+    return c_off[:total], c_len[:total], (dig[:total] if dig is not None else None), first
+
+
 def to_numpy_u64(t: torch.Tensor) -> np.ndarray:
     return t.detach().cpu().numpy().view(np.uint64)
 

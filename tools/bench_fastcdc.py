@@ -1,0 +1,85 @@
+"""FastCDC v2020 chunking + chunk digests of device-resident blobs (BASELINE configs[4] shape:
+16 x 8 GiB, experiments/block-level-dedup). Prints one JSON line.
+
+    python tools/bench_fastcdc.py [--files 16] [--gib 8] [--chunk 65536] [--reps 3]
+
+Timed: one oxh_fastcdc_device call (F1 scan, F2 speculative walks, F3 stitch, compaction, K1 over the
+chunk table) with the inputs resident in HBM. The chunk table of the first file is checked against the
+C oracle on a prefix (oracle/fastcdc_oracle.c), which is also timed as the single-core CPU baseline.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--files", type=int, default=16)
+    ap.add_argument("--gib", type=float, default=8.0)
+    ap.add_argument("--chunk", type=int, default=65536)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--check-mib", type=int, default=256)
+    args = ap.parse_args()
+
+    import torch
+
+    from oracle import fastcdc as F
+    from oracle import oracle
+    from oxen_amd.device import fastcdc_device, fill_splitmix, to_numpy_u64
+
+    dev = torch.device("cuda:0")
+    size = int(args.gib * 2**30)
+    pitch = (size + 4095) // 4096 * 4096
+    arena = torch.empty(pitch * args.files, dtype=torch.uint8, device=dev)
+    fill_splitmix(arena, 77)
+    offs = np.arange(args.files, dtype=np.uint64) * np.uint64(pitch)
+    lens = np.full(args.files, size, dtype=np.uint64)
+    mn, av, mx = 4096, args.chunk, 2 * args.chunk
+    total = size * args.files
+
+    c_off, c_len, dig, first = fastcdc_device(arena, offs, lens, mn, av, mx)  # warm-up
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(args.reps):
+        t0 = time.perf_counter()
+        c_off, c_len, dig, first = fastcdc_device(arena, offs, lens, mn, av, mx)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    nchunks = int(first[-1])
+
+    # bit-exact check of a prefix of file 0 (chunks that end inside the prefix are final)
+    m = min(size, args.check_mib << 20)
+    host = arena[:m].cpu().numpy()
+    t0 = time.perf_counter()
+    want = F.chunks(host, mn, av, mx)
+    cpu_s = time.perf_counter() - t0
+    got_off = to_numpy_u64(c_off[: int(first[1])])
+    got_len = to_numpy_u64(c_len[: int(first[1])])
+    k = len(want) - 1  # the oracle's last chunk is cut by the prefix end
+    exact = bool(np.array_equal(got_off[:k], want[:k, 0]) and np.array_equal(got_len[:k], want[:k, 1]))
+    wd = oracle.batch(host, want[:k, 0], want[:k, 1], threads=16)
+    exact = exact and bool(np.array_equal(to_numpy_u64(dig[:k]).reshape(-1, 2), wd))
+    res = {"workload": f"{args.files} x {args.gib:g} GiB splitmix blobs, FastCDC v2020 min/avg/max {mn}/{av}/{mx} "
+                       f"+ XXH3-128 per chunk, device-resident",
+           "bytes": total, "chunks": nchunks, "mean_chunk": total / max(nchunks, 1),
+           "s_median": round(t, 4), "s_all": [round(x, 4) for x in times],
+           "GiB_s": round(total / t / 2**30, 1), "GB_s": round(total / t / 1e9, 1),
+           "prefix_checked_bytes": m, "prefix_chunks_bit_exact": exact,
+           "cpu_oracle_1core_GiB_s": round(m / cpu_s / 2**30, 3)}
+    print(json.dumps(res), flush=True)
+    if not exact:
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()
