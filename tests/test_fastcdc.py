@@ -205,13 +205,16 @@ def test_fastcdchunker_pack(cuda, oracle_lib, tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("warmup", ["0", None], ids=["nowarmup", "warmup"])
 @pytest.mark.parametrize("section", [1024, 4096, 65536])
 @pytest.mark.parametrize("cfg", [CONFIGS[0], CONFIGS[2], CONFIGS[3], CONFIGS[4]], ids=lambda c: "-".join(map(str, c)))
-def test_fastcdc_small_sections(cuda, oracle_lib, monkeypatch, section, cfg):
-    """Many sections per file (OXH_CDC_SECTION_BYTES): chunks span sections, speculative walks start
-    mid-chunk everywhere, candidate lists overflow at 1 KiB (the byte-scan fallback), and the stitch
-    has to re-walk wherever a speculative walk has not converged."""
+def test_fastcdc_small_sections(cuda, oracle_lib, monkeypatch, section, cfg, warmup):
+    """Many sections per file (OXH_CDC_SECTION_BYTES, raised to `max` where smaller): speculative walks
+    start mid-chunk everywhere, candidate lists overflow at 1 KiB sections (the byte-scan fallback),
+    and the stitch re-walks wherever a speculative walk has not converged (constant data never does)."""
     monkeypatch.setenv("OXH_CDC_SECTION_BYTES", str(section))
+    if warmup is not None:  # no warm-up: most sections fail the check and are re-walked (F3b)
+        monkeypatch.setenv("OXH_CDC_WARMUP_BYTES", warmup)
     rng = np.random.default_rng(section + cfg[1])
     text = np.frombuffer(b"".join(b"row %d,%d\n" % (i, i * 7 % 13) for i in range(60_000)), dtype=np.uint8)
     files = [rng.integers(0, 256, s, dtype=np.uint8) for s in (5, 4097, 65_537, 300_001)]
