@@ -15,6 +15,7 @@
 #include <ftw.h>
 #include <stdint.h>
 #include <string.h>
+#include <sys/resource.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -660,19 +661,271 @@ int oxh_hash_streams(oxh_ctx* c, const uint8_t* streams, const uint64_t* offsets
     }, out, nullptr, true);
 }
 
-static int read_whole(const char* path, uint8_t* dst, uint64_t len) {
-    int fd = open(path, O_RDONLY | O_CLOEXEC);
-    if (fd < 0) return OXH_ERR_IO;
-    uint64_t got = 0;
-    while (got < len) {
-        ssize_t r = pread(fd, dst + got, len - got, (off_t)got);
-        if (r <= 0) {
-            close(fd);
-            return OXH_ERR_IO;
-        }
-        got += (uint64_t)r;
+// ---------------------------------------------------------------- streaming file pipeline
+// The reference reads, stats and hashes each file inside one per-file closure (add.rs:462-539 ->
+// hasher.rs:126-148). Here T reader threads run the whole list without barriers or locks: each
+// claims the next files, opens + fstats one (one path walk), reserves its bytes in the slot being
+// filled with ONE atomic add (item count in the high bits, 256-B-rounded bytes in the low bits),
+// preads straight into the pinned slot and closes it. Reservations are monotone, so the first one
+// that does not fit seals the slot: every earlier one fits and every later one fails. The reader
+// that seals opens the next slot of the ring once the calling thread has freed it; the calling
+// thread submits a sealed slot when all its writers are done (H2D on the copy stream, K1/K1T, D2H)
+// and drains the previous slot while the readers fill the next one.
+namespace {
+
+// One 64-bit word per slot: bytes (31 bits) | items (19) | sealed (1) | generation (13). Every
+// reservation is a CAS on it, so a reader that read an older generation (the slot was sealed,
+// submitted and reopened meanwhile) can never act on the new one.
+constexpr int kWBytes = 31, kWItems = 19;
+constexpr uint64_t kBytesMask = (1ull << kWBytes) - 1, kItemsMask = (1ull << kWItems) - 1;
+constexpr uint64_t kSealedBit = 1ull << (kWBytes + kWItems);
+constexpr int kGenShift = kWBytes + kWItems + 1;
+inline uint64_t w_bytes(uint64_t w) { return w & kBytesMask; }
+inline uint64_t w_items(uint64_t w) { return (w >> kWBytes) & kItemsMask; }
+
+struct SlotFill {
+    std::atomic<int> state{0};         // 0 free, 1 filling (or sealed, not yet submitted), 2 submitted
+    std::atomic<uint64_t> word{0};
+    std::atomic<uint64_t> done{0};     // writers finished
+};
+
+struct FileStream {
+    oxh_ctx* c;
+    const char* const* paths;
+    uint64_t n;
+    SlotFill slot[NSLOT];
+    std::atomic<int> cur{0};
+    std::atomic<int> readers_left{0};
+    std::atomic<bool> abort{false};
+    std::atomic<uint64_t> next{0};
+    std::vector<uint64_t> lens;
+    std::vector<int32_t> st;
+    std::vector<uint64_t> ids[NSLOT];
+    std::mutex omu;
+    std::vector<uint64_t> oversize;
+    std::mutex cmu;  // the calling thread sleeps on ccv until a slot is complete
+    std::condition_variable ccv;
+    void wake() {
+        std::lock_guard<std::mutex> g(cmu);
+        ccv.notify_all();
     }
-    close(fd);
+};
+
+inline void pause_us(int us) { std::this_thread::sleep_for(std::chrono::microseconds(us)); }
+
+// Open slot t for filling (generation + 1, empty, unsealed) once the calling thread has freed it.
+bool open_slot(FileStream& fs, int t) {
+    SlotFill& nx = fs.slot[t];
+    while (nx.state.load(std::memory_order_acquire) != 0) {
+        if (fs.abort.load(std::memory_order_relaxed)) return false;
+        pause_us(5);
+    }
+    const uint64_t gen = (nx.word.load(std::memory_order_relaxed) >> kGenShift) + 1;
+    nx.done.store(0, std::memory_order_relaxed);
+    nx.word.store((gen << kGenShift) & ~0ull, std::memory_order_release);
+    nx.state.store(1, std::memory_order_release);
+    fs.cur.store(t, std::memory_order_release);
+    return true;
+}
+
+// Reserve L bytes for item i; returns the slot (and offset), or -1 on abort.
+int reserve(FileStream& fs, uint64_t i, uint64_t L, uint64_t& off) {
+    oxh_ctx* c = fs.c;
+    const uint64_t M = c->max_items, cap = c->stage_bytes;
+    const uint64_t need = align_up(L);
+    for (;;) {
+        if (fs.abort.load(std::memory_order_relaxed)) return -1;
+        const int s = fs.cur.load(std::memory_order_acquire);
+        SlotFill& sl = fs.slot[s];
+        uint64_t w = sl.word.load(std::memory_order_acquire);
+        if (w & kSealedBit) {  // full: wait for the sealer to open the next slot
+            while (fs.cur.load(std::memory_order_acquire) == s && !fs.abort.load(std::memory_order_relaxed)) pause_us(2);
+            continue;
+        }
+        const uint64_t o = w_bytes(w), j = w_items(w);
+        if (o + L <= cap && j < M) {
+            if (!sl.word.compare_exchange_weak(w, w + (1ull << kWBytes) + need, std::memory_order_acq_rel)) continue;
+            off = o;
+            c->h_desc[s][j] = o;
+            c->h_desc[s][M + j] = L;
+            fs.ids[s][j] = i;
+            return s;
+        }
+        // does not fit: seal it (one reader wins) and open the next slot of the ring
+        if (!sl.word.compare_exchange_strong(w, w | kSealedBit, std::memory_order_acq_rel)) continue;
+        if (sl.done.load(std::memory_order_acquire) == j) fs.wake();  // its writers are all done
+        if (!open_slot(fs, (s + 1) % NSLOT)) return -1;
+    }
+}
+
+void reader_loop(FileStream& fs) {
+    oxh_ctx* c = fs.c;
+    constexpr uint64_t kClaim = 8;
+    for (;;) {
+        const uint64_t i0 = fs.next.fetch_add(kClaim);
+        if (i0 >= fs.n || fs.abort.load(std::memory_order_relaxed)) break;
+        for (uint64_t i = i0; i < std::min(fs.n, i0 + kClaim); ++i) {
+            struct stat sb;
+            const int fd = fs.paths[i] ? open(fs.paths[i], O_RDONLY | O_CLOEXEC | O_NONBLOCK) : -1;
+            if (fd < 0) {
+                fs.st[i] = OXH_ERR_IO;
+                continue;
+            }
+            if (fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode)) {
+                close(fd);
+                fs.st[i] = OXH_ERR_IO;
+                continue;
+            }
+            const uint64_t L = (uint64_t)sb.st_size;
+            fs.lens[i] = L;
+            if (L > c->stage_bytes) {  // read later through the oversize path
+                close(fd);
+                std::lock_guard<std::mutex> g(fs.omu);
+                fs.oversize.push_back(i);
+                continue;
+            }
+            uint64_t off = 0;
+            const int s = reserve(fs, i, L, off);
+            if (s < 0) {
+                close(fd);
+                break;
+            }
+            uint8_t* dst = c->h_stage[s] + off;
+            uint64_t got = 0;
+            while (got < L) {
+                const ssize_t k = pread(fd, dst + got, L - got, (off_t)got);
+                if (k <= 0) {
+                    fs.st[i] = OXH_ERR_IO;
+                    break;
+                }
+                got += (uint64_t)k;
+            }
+            close(fd);
+            // the last writer of a sealed slot wakes the calling thread
+            const uint64_t d = fs.slot[s].done.fetch_add(1, std::memory_order_acq_rel) + 1;
+            const uint64_t w = fs.slot[s].word.load(std::memory_order_acquire);
+            if ((w & kSealedBit) && d == w_items(w)) fs.wake();
+        }
+    }
+    if (fs.readers_left.fetch_sub(1, std::memory_order_acq_rel) == 1) fs.wake();
+}
+
+}  // namespace
+
+static int stream_files(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* lens_out,
+                        int32_t* st_out, uint64_t* counts, const ItemSink* sink) {
+    FileStream fs;
+    fs.c = c;
+    fs.paths = paths;
+    fs.n = n;
+    fs.lens.assign(n, 0);
+    fs.st.assign(n, OXH_OK);
+    for (int s = 0; s < NSLOT; ++s) fs.ids[s].resize(c->max_items);
+    fs.slot[0].state.store(1);
+    fs.slot[0].word.store(1ull << kGenShift);
+    Trace tr;
+    const double t_start = Trace::now();
+    const int nreaders = (int)std::max<uint64_t>(1, std::min<uint64_t>(n, (uint64_t)c->pool->size()));
+    fs.readers_left.store(nreaders);
+    std::vector<std::thread> readers;
+    readers.reserve(nreaders);
+    for (int r = 0; r < nreaders; ++r) readers.emplace_back([&fs] { reader_loop(fs); });
+    Pending pend[NSLOT];
+    int rc = OXH_OK;
+    const uint64_t M = c->max_items;
+    int s = 0;  // next slot to submit (slots are filled and submitted in ring order)
+    for (;;) {
+        // wait until slot s is sealed (or the readers are done) and its writers have finished
+        SlotFill& sl = fs.slot[s];
+        const double tw = Trace::now();
+        uint64_t cnt = 0;
+        bool last = false;  // set when this is the final, partial slot
+        for (;;) {
+            const bool finished = fs.readers_left.load(std::memory_order_acquire) == 0;
+            uint64_t w = sl.word.load(std::memory_order_acquire);
+            if (finished && sl.state.load(std::memory_order_acquire) == 1 && !(w & kSealedBit)) {
+                // the readers are done: seal the last, partial slot ourselves
+                sl.word.fetch_or(kSealedBit, std::memory_order_acq_rel);
+                w |= kSealedBit;
+                last = true;
+            }
+            if ((w & kSealedBit) || (finished && sl.state.load(std::memory_order_acquire) != 1)) {
+                cnt = (w & kSealedBit) && sl.state.load(std::memory_order_acquire) == 1 ? w_items(w) : 0;
+                if (cnt == 0 && finished) break;
+                if (cnt && sl.done.load(std::memory_order_acquire) == cnt) break;
+            }
+            // sleep until a reader reports a completed slot (bounded: a missed wake-up costs 1 ms)
+            std::unique_lock<std::mutex> lk(fs.cmu);
+            fs.ccv.wait_for(lk, std::chrono::milliseconds(1), [&] {
+                const uint64_t x = sl.word.load(std::memory_order_acquire);
+                return fs.readers_left.load(std::memory_order_acquire) == 0 ||
+                       ((x & kSealedBit) && sl.done.load(std::memory_order_acquire) == w_items(x));
+            });
+        }
+        tr.fill += Trace::now() - tw;
+        if (cnt == 0) break;  // only possible for the last, empty slot
+        uint64_t bytes = 0;
+        for (uint64_t j = 0; j < cnt; ++j) bytes = std::max(bytes, c->h_desc[s][j] + c->h_desc[s][M + j]);
+        const double t0 = Trace::now();
+        sl.state.store(2, std::memory_order_release);
+        rc = submit_slot(c, s, bytes, cnt, false, bytes / cnt <= kShortItemBytes, counts != nullptr);
+        if (rc) break;
+        pend[s].busy = true;
+        pend[s].ids.assign(fs.ids[s].begin(), fs.ids[s].begin() + (ptrdiff_t)cnt);
+        tr.submit += Trace::now() - t0;
+        tr.batches++;
+        // drain the slot submitted in the previous round while the readers fill the next one: it is
+        // the slot they move into after that, so it is free well before they get there
+        const int t = (s + NSLOT - 1) % NSLOT;
+        const double t1 = Trace::now();
+        rc = drain_slot(c, t, pend[t], out, counts, sink, fs.st.data());
+        if (rc) break;
+        join_consumer(pend[t]);
+        tr.drain += Trace::now() - t1;
+        if (fs.slot[t].state.load(std::memory_order_acquire) == 2) fs.slot[t].state.store(0, std::memory_order_release);
+        if (last) break;
+        s = (s + 1) % NSLOT;
+    }
+    if (rc) fs.abort.store(true);
+    for (auto& th : readers) th.join();
+    const double t3 = Trace::now();
+    for (int k = 0; k < NSLOT && rc == OXH_OK; ++k) rc = drain_slot(c, k, pend[k], out, counts, sink, fs.st.data());
+    for (int k = 0; k < NSLOT; ++k) join_consumer(pend[k]);
+    tr.drain += Trace::now() - t3;
+    if (rc) return rc;
+    // files larger than a staging slot, one at a time through the oversize path (K1L)
+    std::sort(fs.oversize.begin(), fs.oversize.end());
+    for (uint64_t i : fs.oversize) {
+        std::vector<uint8_t> tmp(fs.lens[i]);
+        const int fd = open(paths[i], O_RDONLY | O_CLOEXEC | O_NONBLOCK);
+        uint64_t got = 0;
+        if (fd >= 0) {
+            while (got < fs.lens[i]) {
+                const ssize_t k = pread(fd, tmp.data() + got, fs.lens[i] - got, (off_t)got);
+                if (k <= 0) break;
+                got += (uint64_t)k;
+            }
+            close(fd);
+        }
+        if (got != fs.lens[i]) {
+            fs.st[i] = OXH_ERR_IO;
+            continue;
+        }
+        rc = oversize_item(c, tmp.data(), fs.lens[i], out + 2 * i, counts ? counts + 2 * i : nullptr);
+        if (rc) return rc;
+        if (sink) (*sink)(i, tmp.data(), fs.lens[i], out[2 * i], out[2 * i + 1]);
+    }
+    if (tr.on)
+        fprintf(stderr, "[oxh] files=%llu batches=%d total=%.3fs coord-wait-fill=%.3fs drain-wait=%.3fs submit=%.3fs readers=%d\n",
+                (unsigned long long)n, tr.batches, Trace::now() - t_start, tr.fill, tr.drain, tr.submit, nreaders);
+    for (uint64_t i = 0; i < n; ++i) {
+        if (fs.st[i] != OXH_OK) {
+            out[2 * i] = out[2 * i + 1] = 0;
+            if (counts) counts[2 * i] = counts[2 * i + 1] = 0;
+        }
+        if (lens_out) lens_out[i] = fs.lens[i];
+        if (st_out) st_out[i] = fs.st[i];
+    }
     return OXH_OK;
 }
 
@@ -681,34 +934,8 @@ static int hash_files_impl(oxh_ctx* c, const char* const* paths, uint64_t n, uin
     if (!c || (n && (!paths || !out))) return fail(OXH_ERR_INVALID, "bad arguments");
     std::lock_guard<std::mutex> g(c->mu);
     HIP_TRY(hipSetDevice(c->device));
-    // stat pass (util::fs::metadata in add.rs:716/741), parallel
-    Trace tr;
-    const double ts = Trace::now();
-    std::vector<uint64_t> lens(n, 0);
-    std::vector<int32_t> st(n, OXH_OK);
-    const int ntasks = (int)std::min<uint64_t>(n, (uint64_t)c->pool->size() * 4);
-    c->pool->parallel_for(ntasks, [&](int t) {
-        for (uint64_t i = (uint64_t)t; i < n; i += (uint64_t)ntasks) {
-            struct stat sb;
-            if (!paths[i] || stat(paths[i], &sb) != 0 || !S_ISREG(sb.st_mode)) {
-                st[i] = OXH_ERR_IO;
-            } else {
-                lens[i] = (uint64_t)sb.st_size;
-            }
-        }
-    });
-    tr.stat = Trace::now() - ts;
-    std::vector<int32_t> st2(n, OXH_OK);
-    int rc = hash_host_items(c, n, lens.data(), [&](uint64_t i, uint8_t* dst) {
-        if (st[i] != OXH_OK) return (int)st[i];
-        return read_whole(paths[i], dst, lens[i]);
-    }, out, st2.data(), false, &tr, counts, sink);
-    if (rc) return rc;
-    for (uint64_t i = 0; i < n; ++i) {
-        if (sizes) sizes[i] = lens[i];
-        if (status) status[i] = st2[i];
-    }
-    return OXH_OK;
+    if (n == 0) return OXH_OK;
+    return stream_files(c, paths, n, out, sizes, status, counts, sink);
 }
 
 int oxh_hash_files(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* sizes, int32_t* status) {
