@@ -3,7 +3,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-TAG=${TAG:-r01}
+TAG=${TAG:-r01c}
 WL=${WL:-c2}
 mkdir -p gpurun_out
 BENCH="python3 bench.py --workload $WL --steps 10 --warmup 2 --no-cpu-baseline"
