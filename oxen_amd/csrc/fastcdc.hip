@@ -35,6 +35,7 @@
 #include <algorithm>
 #include <cmath>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/oxen_hash.h"
@@ -73,7 +74,9 @@ struct CdcFiles {
     const uint64_t* flen;      // [n]
     const uint64_t* sec_base;  // [n+1] first global section of each file
     const uint32_t* sec_file;  // [n_sec] file of each section
-    uint32_t* cand;            // [n_sec * cap] (rel_pos << 2 | flags), position order
+    uint32_t* cand;            // [n_sec * cap] candidate groups: offset in the section (16-aligned), in order
+    uint64_t* cand_h;          // [n_sec * cap] full-window hash before each group's first byte (mod 2^48)
+    uint4* cand_b;             // [n_sec * cap] the group's 16 bytes (the walk resolves flags from these)
     uint32_t* cand_cnt;        // [n_sec] true count (> cap: list truncated, dense fallback)
     uint32_t* spec;            // [n_sec * speccap] speculative starts, relative to section start
     uint32_t* spec_cnt;        // [n_sec]
@@ -81,27 +84,76 @@ struct CdcFiles {
 
 __device__ __forceinline__ uint64_t gear_of(const uint64_t* __restrict__ g, uint32_t b) { return g[b]; }
 
+// DPP wave_shr:1 (GFX9): lane l gets x from lane l-1; lane 0 keeps `old`
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t x, uint32_t old) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, 0x138, 0xf, 0xf, false);
+}
+// (a & b) | c in one VALU op
+__device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ uint32_t min_u32(uint32_t a, uint32_t b) { return a < b ? a : b; }
+
+// 16 bytes at p[pos .. pos+16) of a file of length flen as four little-endian words (zeros past the
+// end): one raw buffer load (gfx950 buffer loads take any alignment) instead of 16 dependent byte
+// loads -- the walk's latency is made of these.
+__device__ __forceinline__ uint4 load16_file(const uint8_t* __restrict__ fbase, uint64_t pos, uint64_t flen) {
+    if (pos >= flen) return make_uint4(0, 0, 0, 0);
+    if (flen - pos >= 16) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(fbase + pos), (short)0, 16, 0x00020000);
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, 0u, 0, 0);
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+        if (pos + (uint64_t)j < flen) w[j >> 2] |= (uint32_t)fbase[pos + j] << (8 * (j & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+__device__ __forceinline__ uint32_t byte_of(const uint4& v, int j) {
+    const uint32_t w = j < 4 ? v.x : j < 8 ? v.y : j < 12 ? v.z : v.w;
+    return (w >> (8 * (j & 3))) & 0xFF;
+}
+
 // ---------------------------------------------------------------- F1: candidates
 // Lane l of the wave owns bytes [16l, 16l+16) of a 1 KiB sub-block. Its first byte's hash needs the
 // state at the byte before it: H = hl(l-1) + hl(l-2) << 16 + hl(l-3) << 32 (mod the 48 live bits),
 // with hl(m) the hash lane m's 16 bytes alone produce from 0. Lanes 0..2 take lanes 61..63 of the
 // previous sub-block. Candidates are rare (~2^-bits), so the fast path only tests the bits the two
 // masks share and a rare path recomputes both flags for the sub-block.
-__global__ __launch_bounds__(256) void cdc_scan_kernel(CdcFiles f, CdcParams prm, uint64_t n_sec) {
-    __shared__ uint64_t lds_gear[256];
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) lds_gear[i] = kGear[i];
+//
+// The gear lookups are random 8-byte LDS gathers: with one shared table, the 32 lanes of a
+// ds_read_b64 group collide on bank pairs (~3.2 cycles per group instead of 1). With COPIES = 32 the
+// table is stored 32 times, copy c entirely in bank pair c (entry k of copy c at u64 index 32k + c,
+// 64 KiB), and lane l reads copy l % 32: no two lanes of a group ever share a bank, so every gather
+// costs the conflict-free 2 cycles. WAVES waves per workgroup share one table.
+//
+// SH: run the whole hash 16 bits to the left (table entries GEAR << 16, masks << 16). Only bits
+// below 48 matter, so nothing is lost, and when the bits both masks share are all >= 16 they land
+// in the high 32-bit word: the per-byte fast test is then one AND on one register.
+template <int D, int COPIES, int WAVES, bool SH>
+__global__ __launch_bounds__(64 * WAVES) void cdc_scan_kernel(CdcFiles f, CdcParams prm, uint64_t n_sec) {
+    __shared__ uint64_t lds_tab[256 * COPIES];
+    for (int i = threadIdx.x; i < 256 * COPIES; i += blockDim.x) lds_tab[i] = kGear[i / COPIES] << (SH ? 16 : 0);
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const uint64_t sec = (uint64_t)blockIdx.x * 4 + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t* lds_gear = lds_tab + (COPIES == 1 ? 0 : (lane & (COPIES - 1)));  // index b * COPIES
+    const uint64_t sec = (uint64_t)blockIdx.x * WAVES + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (sec >= n_sec) return;
     const uint32_t file = f.sec_file[sec];
     const uint64_t flen = f.flen[file];
     const uint64_t sec_start = (sec - f.sec_base[file]) * prm.sec;
     const uint64_t sec_len = flen - sec_start < prm.sec ? flen - sec_start : prm.sec;
     const uint8_t* __restrict__ base = f.arena + f.foff[file] + sec_start;
-    const uint64_t common = prm.mask_s & prm.mask_l;
-    const uint32_t ch = (uint32_t)(common >> 32), cl = (uint32_t)common;
+    const uint64_t mask_s = prm.mask_s << (SH ? 16 : 0), mask_l = prm.mask_l << (SH ? 16 : 0);
+    const uint64_t common = mask_s & mask_l;
+    const uint32_t ch = (uint32_t)(common >> 32), cl = (uint32_t)common;  // SH: cl == 0 (host checks)
     uint32_t* __restrict__ out = f.cand + sec * prm.cap;
+    uint64_t* __restrict__ out_h = f.cand_h + sec * prm.cap;
+    uint4* __restrict__ out_b = f.cand_b + sec * prm.cap;
     uint32_t count = 0;  // wave-uniform
 
     // carries: hl of the 3 lanes before lane 0 (bytes [-48, 0) of the section); zero at file start
@@ -115,7 +167,7 @@ __global__ __launch_bounds__(256) void cdc_scan_kernel(CdcFiles f, CdcParams prm
             __builtin_memcpy(&d, base - 48 + 16 * lane, 16);
             const uint32_t w[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
-            for (int j = 0; j < 16; ++j) hl = (hl << 1) + lds_gear[(w[j >> 2] >> (8 * (j & 3))) & 0xFF];
+            for (int j = 0; j < 16; ++j) hl = (hl << 1) + lds_gear[((w[j >> 2] >> (8 * (j & 3))) & 0xFF) * COPIES];
         }
         const uint64_t h0 = ((uint64_t)__builtin_amdgcn_readlane((int)(hl >> 32), 0) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)hl, 0);
         const uint64_t h1 = ((uint64_t)__builtin_amdgcn_readlane((int)(hl >> 32), 1) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)hl, 1);
@@ -136,104 +188,93 @@ __global__ __launch_bounds__(256) void cdc_scan_kernel(CdcFiles f, CdcParams prm
         const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo, 0, 2 /* nt */);
         return make_uint4(v.x, v.y, v.z, v.w);
     };
-    auto process = [&](const uint4 d, uint64_t sb) {
+    // FULL: all 1024 bytes of the sub-block lie in the section (every sub-block but the last)
+    auto process = [&](const uint4 d, uint64_t sb, auto full_tag) {
+        constexpr bool FULL = decltype(full_tag)::value;
         const uint64_t off = sb * 1024 + 16 * (uint64_t)lane;
-        const uint64_t live = off < sec_len ? (sec_len - off < 16 ? sec_len - off : 16) : 0;
+        uint64_t live = 16;
         uint32_t w[4] = {d.x, d.y, d.z, d.w};
-        if (live > 0 && live < 16) {  // the section's last partial 16 B: byte loads, constant indices
-            w[0] = w[1] = w[2] = w[3] = 0;
+        if constexpr (!FULL) {
+            live = off < sec_len ? (sec_len - off < 16 ? sec_len - off : 16) : 0;
+            if (live > 0 && live < 16) {  // the section's last partial 16 B: byte loads, constant indices
+                w[0] = w[1] = w[2] = w[3] = 0;
 #pragma unroll
-            for (int j = 0; j < 16; ++j)
-                if ((uint64_t)j < live) w[j >> 2] |= (uint32_t)base[off + j] << (8 * (j & 3));
+                for (int j = 0; j < 16; ++j)
+                    if ((uint64_t)j < live) w[j >> 2] |= (uint32_t)base[off + j] << (8 * (j & 3));
+            }
         }
         uint64_t g[16];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) g[j] = lds_gear[(w[j >> 2] >> (8 * (j & 3))) & 0xFF];
+        for (int j = 0; j < 16; ++j) g[j] = lds_gear[((w[j >> 2] >> (8 * (j & 3))) & 0xFF) * COPIES];
         uint64_t hl = 0;
 #pragma unroll
         for (int j = 0; j < 16; ++j) hl = (hl << 1) + g[j];
-        // previous three lanes' hl (lanes 0..2 from the carries)
-        const int hi = (int)(hl >> 32), lo = (int)(uint32_t)hl;
-        uint64_t p1 = ((uint64_t)(uint32_t)__shfl_up(hi, 1, 64) << 32) | (uint32_t)__shfl_up(lo, 1, 64);
-        uint64_t p2 = ((uint64_t)(uint32_t)__shfl_up(hi, 2, 64) << 32) | (uint32_t)__shfl_up(lo, 2, 64);
-        uint64_t p3 = ((uint64_t)(uint32_t)__shfl_up(hi, 3, 64) << 32) | (uint32_t)__shfl_up(lo, 3, 64);
-        if (lane == 0) { p1 = c1; p2 = c2; p3 = c3; }
-        if (lane == 1) { p2 = c1; p3 = c2; }
-        if (lane == 2) { p3 = c1; }
+        // previous three lanes' hl: DPP wave shifts by one lane; lanes shifted in from "before lane
+        // 0" take the carries (lanes 63, 62, 61 of the previous sub-block) as the DPP `old` value
+        const uint32_t hi = (uint32_t)(hl >> 32), lo = (uint32_t)hl;
+        const uint32_t p1h = wave_shr1(hi, (uint32_t)(c1 >> 32)), p1l = wave_shr1(lo, (uint32_t)c1);
+        const uint32_t p2h = wave_shr1(p1h, (uint32_t)(c2 >> 32)), p2l = wave_shr1(p1l, (uint32_t)c2);
+        const uint32_t p3h = wave_shr1(p2h, (uint32_t)(c3 >> 32)), p3l = wave_shr1(p2l, (uint32_t)c3);
+        const uint64_t p1 = ((uint64_t)p1h << 32) | p1l, p2 = ((uint64_t)p2h << 32) | p2l;
+        const uint64_t p3 = ((uint64_t)p3h << 32) | p3l;
         const uint64_t H = p1 + (p2 << 16) + (p3 << 32);
         uint64_t h = H;
         uint32_t anyz = 0xFFFFFFFFu;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             h = (h << 1) + g[j];
-            const uint32_t m = ((uint32_t)(h >> 32) & ch) | ((uint32_t)h & cl);
-            anyz = m < anyz ? m : anyz;
+            if constexpr (SH) anyz = min_u32(anyz, (uint32_t)(h >> 32) & ch);
+            else anyz = min_u32(anyz, and_or((uint32_t)h, cl, (uint32_t)(h >> 32) & ch));
         }
         // bytes past the section end are not positions of this section
-        const bool maybe = (anyz == 0) && live > 0;
-        if (__builtin_amdgcn_ballot_w64(maybe) != 0) {
-            uint32_t fs = 0, fl = 0;  // per-byte flags of this lane
-            if (maybe) {
-                h = H;
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    h = (h << 1) + g[j];
-                    if ((uint64_t)j < live) {
-                        fs |= ((h & prm.mask_s) == 0 ? 1u : 0u) << j;
-                        fl |= ((h & prm.mask_l) == 0 ? 1u : 0u) << j;
-                    }
-                }
+        const bool maybe = (anyz == 0) && (FULL || live > 0);
+        // a lane whose 16 bytes may hold a candidate records its group (offset + the hash before it);
+        // the walk resolves the exact mask_s / mask_l flags of the group when it needs them
+        const uint64_t bal = __builtin_amdgcn_ballot_w64(maybe);
+        if (bal != 0) {
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            const uint32_t idx = count + below;
+            if (maybe && idx < prm.cap) {
+                out[idx] = (uint32_t)off;
+                out_h[idx] = SH ? (H >> 16) : H;
+                out_b[idx] = make_uint4(w[0], w[1], w[2], w[3]);
             }
-            const uint32_t any = fs | fl;
-            const uint32_t c = (uint32_t)__builtin_popcount(any);
-            // inclusive prefix over lanes
-            uint32_t incl = c;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t t = (uint32_t)__shfl_up((int)incl, o, 64);
-                if (lane >= o) incl += t;
-            }
-            uint32_t idx = count + incl - c;
-            uint32_t rest = any;
-            while (rest) {
-                const int j = __builtin_ctz(rest);
-                rest &= rest - 1;
-                if (idx < prm.cap)
-                    out[idx] = ((uint32_t)(off + j) << 2) | ((fs >> j) & 1u) | (((fl >> j) & 1u) << 1);
-                ++idx;
-            }
-            count += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            count += (uint32_t)__builtin_popcountll(bal);
         }
         // carries for the next sub-block: hl of lanes 63, 62, 61
-        c1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(hi, 63) << 32) | (uint32_t)__builtin_amdgcn_readlane(lo, 63);
-        c2 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(hi, 62) << 32) | (uint32_t)__builtin_amdgcn_readlane(lo, 62);
-        c3 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(hi, 61) << 32) | (uint32_t)__builtin_amdgcn_readlane(lo, 61);
+        c1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 63) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
+        c2 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 62) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)lo, 62);
+        c3 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 61) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)lo, 61);
     };
     // software pipeline: D sub-blocks (D KiB per wave) in flight while one is folded
-    constexpr int D = 8;
     uint4 ring[D];
 #pragma unroll
     for (int d = 0; d < D; ++d) ring[d] = load_sub((uint64_t)d);
+    const uint64_t nfull = sec_len >> 10;
     uint64_t sb = 0;
-    for (; sb + D <= nsub; sb += D) {
+    for (; sb + D <= nfull; sb += D) {
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            process(ring[d], sb + d);
+            process(ring[d], sb + d, std::true_type{});
             ring[d] = load_sub(sb + d + D);
             __builtin_amdgcn_sched_barrier(0);
         }
     }
+    // the last < D sub-blocks (the final one may be partial) are already in the ring
 #pragma unroll
     for (int d = 0; d < D; ++d)
-        if (sb + d < nsub) process(ring[d], sb + d);
+        if (sb + d < nsub) process(ring[d], sb + d, std::false_type{});
     if (lane == 0) f.cand_cnt[sec] = count;
 }
 
 // ---------------------------------------------------------------- the walk (F2, F3)
 // Cursor over the candidate lists of one file, monotone in position.
 struct CandCursor {
-    uint64_t sec;  // global section index of the cursor
-    uint32_t idx;  // entry index within that section's list
+    uint64_t sec;   // global section index of the cursor
+    uint32_t idx;   // group index within that section's list
+    uint32_t rsec_idx = 0xFFFFFFFFu;  // the last resolved group (sec low bits + idx) and its flags
+    uint64_t rsec = ~0ull;
+    uint32_t rfs = 0, rfl = 0;
 };
 
 // Full-window hash test of positions [lo, hi) (all inside one file, lo >= 47) by direct byte scan:
@@ -241,20 +282,46 @@ struct CandCursor {
 // (hash & mask) == 0, or hi.
 __device__ uint64_t scan_bytes(const uint8_t* __restrict__ fbase, uint64_t lo, uint64_t hi, uint64_t mask,
                                const uint64_t* __restrict__ gear) {
+    // hi <= the file length (queries never pass it)
     uint64_t h = 0;
-    for (uint64_t p = lo - kHashSpan; p < lo; ++p) h = (h << 1) + gear_of(gear, fbase[p]);
-    for (uint64_t p = lo; p < hi; ++p) {
-        h = (h << 1) + gear_of(gear, fbase[p]);
-        if ((h & mask) == 0) return p;
+    for (uint64_t p = lo - kHashSpan; p < hi; p += 16) {
+        const uint4 v = load16_file(fbase, p, hi);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint64_t q = p + (uint64_t)j;
+            if (q >= hi) return hi;
+            h = (h << 1) + gear_of(gear, byte_of(v, j));
+            if (q >= lo && (h & mask) == 0) return q;
+        }
     }
     return hi;
+}
+
+// Exact mask_s / mask_l flags (bit j = position g + j) of a candidate group: roll the 16 bytes F1
+// stored with it from the hash F1 recorded before it (no re-read of the file: the walk is
+// latency-bound and the lists stay in the L2 / Infinity Cache).
+__device__ __forceinline__ void resolve_group(const uint4 v, uint64_t g, uint64_t H, uint64_t flen,
+                                              const CdcParams& prm, const uint64_t* __restrict__ gear,
+                                              uint32_t& fs, uint32_t& fl) {
+    fs = fl = 0;
+    uint64_t h = H;
+    const uint32_t live = flen - g < 16 ? (uint32_t)(flen - g) : 16u;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        h = (h << 1) + gear_of(gear, byte_of(v, j));
+        fs |= ((h & prm.mask_s) == 0 ? 1u : 0u) << j;
+        fl |= ((h & prm.mask_l) == 0 ? 1u : 0u) << j;
+    }
+    const uint32_t keep = live >= 16 ? 0xFFFFu : ((1u << live) - 1u);
+    fs &= keep;
+    fl &= keep;
 }
 
 // First position in [lo, hi) (file-relative) whose full-window hash matches `flag` (1: mask_s,
 // 2: mask_l), or hi. Advances the cursor (callers query increasing positions).
 __device__ uint64_t first_cand(const CdcFiles& f, const CdcParams& prm, uint64_t sec0, uint64_t nsec_file,
-                               const uint8_t* fbase, CandCursor& cur, uint64_t lo, uint64_t hi, uint32_t flag,
-                               const uint64_t* gear) {
+                               const uint8_t* fbase, uint64_t flen, CandCursor& cur, uint64_t lo, uint64_t hi,
+                               uint32_t flag, const uint64_t* gear) {
     if (lo >= hi) return hi;
     uint64_t s = lo / prm.sec;
     if (cur.sec < sec0 + s) {
@@ -266,21 +333,33 @@ __device__ uint64_t first_cand(const CdcFiles& f, const CdcParams& prm, uint64_t
         const uint64_t sec_start = (cur.sec - sec0) * prm.sec;
         if (sec_start >= hi) return hi;
         const uint32_t* list = f.cand + cur.sec * prm.cap;
+        const uint64_t* hs = f.cand_h + cur.sec * prm.cap;
         const uint32_t cnt = f.cand_cnt[cur.sec];
         const uint32_t stored = cnt < prm.cap ? cnt : prm.cap;
         while (cur.idx < stored) {
-            const uint32_t e = list[cur.idx];
-            const uint64_t p = sec_start + (e >> 2);
-            if (p >= hi) return hi;
-            if (p >= lo && (e & flag)) return p;
-            // below lo, or in range without the flag: later queries start at or after this one's
-            // end (an L query follows an S query from eS on), so the entry is never needed again
+            const uint64_t g = sec_start + list[cur.idx];
+            if (g >= hi) return hi;
+            if (g + 16 > lo) {  // the group overlaps [lo, hi)
+                if (cur.rsec != cur.sec || cur.rsec_idx != cur.idx) {
+                    resolve_group(f.cand_b[cur.sec * prm.cap + cur.idx], g, hs[cur.idx], flen, prm, gear, cur.rfs, cur.rfl);
+                    cur.rsec = cur.sec;
+                    cur.rsec_idx = cur.idx;
+                }
+                uint32_t m = flag == 1 ? cur.rfs : cur.rfl;
+                if (lo > g) m &= ~0u << (uint32_t)(lo - g);                  // positions >= lo
+                if (hi < g + 16) m &= (1u << (uint32_t)(hi - g)) - 1u;       // positions < hi
+                if (m) return g + (uint64_t)__builtin_ctz(m);
+                // the rest of the group lies beyond hi: the next query (from hi on) needs it again
+                if (g + 16 > hi) return hi;
+            }
+            // below lo, or done with: later queries start at or after this one's end (an L query
+            // follows an S query from eS on), so the group is never needed again
             ++cur.idx;
         }
         const uint64_t sec_end = sec_start + prm.sec;
         if (cnt > prm.cap) {
-            // overflowed list: positions after the last stored entry were not recorded
-            const uint64_t after = stored ? sec_start + (list[stored - 1] >> 2) + 1 : sec_start;
+            // overflowed list: positions after the last stored group were not recorded
+            const uint64_t after = stored ? sec_start + list[stored - 1] + 16 : sec_start;
             const uint64_t a = lo > after ? lo : after;
             const uint64_t b = hi < sec_end ? hi : sec_end;
             if (a < b) {
@@ -309,18 +388,25 @@ __device__ uint64_t cdc_cut(const CdcFiles& f, const CdcParams& prm, uint64_t se
     // truncated window: the hash restarts from 0 at a0
     uint64_t h = 0;
     const uint64_t tend = a0 + kHashSpan < eL ? a0 + kHashSpan : eL;
-    for (uint64_t q = a0; q < tend; ++q) {
-        h = (h << 1) + gear_of(gear, fbase[s + q]);
+    // the 47 bytes from a0: three 16-byte loads issued together
+    const uint4 t0 = load16_file(fbase, s + a0, flen), t1 = load16_file(fbase, s + a0 + 16, flen),
+                t2 = load16_file(fbase, s + a0 + 32, flen);
+#pragma unroll
+    for (int k = 0; k < kHashSpan; ++k) {
+        const uint64_t q = a0 + (uint64_t)k;
+        if (q >= tend) break;
+        const uint32_t b = k < 16 ? byte_of(t0, k) : k < 32 ? byte_of(t1, k - 16) : byte_of(t2, k - 32);
+        h = (h << 1) + gear_of(gear, b);
         if ((h & (q < eS ? prm.mask_s : prm.mask_l)) == 0) return q;
     }
     const uint64_t qs = a0 + kHashSpan;
     if (qs < eS) {
-        const uint64_t p = first_cand(f, prm, sec0, nsec_file, fbase, cur, s + qs, s + eS, 1u, gear);
+        const uint64_t p = first_cand(f, prm, sec0, nsec_file, fbase, flen, cur, s + qs, s + eS, 1u, gear);
         if (p < s + eS) return p - s;
     }
     const uint64_t ql = qs > eS ? qs : eS;
     if (ql < eL) {
-        const uint64_t p = first_cand(f, prm, sec0, nsec_file, fbase, cur, s + ql, s + eL, 2u, gear);
+        const uint64_t p = first_cand(f, prm, sec0, nsec_file, fbase, flen, cur, s + ql, s + eL, 2u, gear);
         if (p < s + eL) return p - s;
     }
     return rem;
@@ -618,9 +704,10 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     prm.max = max_size;
     int rc = oxh_fastcdc_masks(avg_size, level, &prm.mask_s, &prm.mask_l);
     if (rc) return rc;
-    // candidate density ~ 2^-popcount(mask) per byte; store 8x the expected count (+64) per section,
-    // at most one per 64 B; a denser section keeps a truncated list and the walk scans its bytes
-    const double dens = std::ldexp(1.0, -__builtin_popcountll(prm.mask_s)) + std::ldexp(1.0, -__builtin_popcountll(prm.mask_l));
+    // F1 records a 16-byte group wherever the bits both masks share are clear at one of its bytes:
+    // ~16 * 2^-popcount(common) groups per 16 bytes. Store 8x the expected count (+64) per section,
+    // at most one per group; a denser section keeps a truncated list and the walk scans its bytes.
+    const double dens = std::min(1.0, 16.0 * std::ldexp(1.0, -__builtin_popcountll(prm.mask_s & prm.mask_l))) / 16.0;
     prm.sec = oxh::kSecDefault;
     if (const char* e = getenv("OXH_CDC_SECTION_BYTES")) {  // tests: many small sections per file
         const uint64_t v = strtoull(e, nullptr, 10);
@@ -635,7 +722,7 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     if (prm.sec < max_rounded) prm.sec = max_rounded;
     if (!getenv("OXH_CDC_SECTION_BYTES") && prm.sec < 4 * max_rounded) prm.sec = 4 * max_rounded;
     if (const char* e = getenv("OXH_CDC_WARMUP_BYTES")) prm.warmup = strtoull(e, nullptr, 10);  // tests
-    prm.cap = (uint32_t)std::min<double>(prm.sec / 64, 8.0 * dens * prm.sec + 64);
+    prm.cap = (uint32_t)std::min<double>(prm.sec / 16, 8.0 * dens * prm.sec + 64);
     prm.speccap = (uint32_t)(prm.sec / min_size + 2 + (max_size + min_size - 1) / min_size);
 
     std::vector<uint64_t> sec_base(n + 1);
@@ -649,12 +736,16 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     Scratch sc(st);
     uint64_t *d_foff, *d_flen, *d_sec_base, *d_first, *d_exit, *d_out_base;
     uint32_t *d_sec_file, *d_cand, *d_cand_cnt, *d_spec, *d_spec_cnt, *d_status, *d_k0, *d_count, *d_fix;
+    uint64_t* d_cand_h;
+    uint4* d_cand_b;
     CDC_HIP(sc.alloc(&d_foff, n));
     CDC_HIP(sc.alloc(&d_flen, n));
     CDC_HIP(sc.alloc(&d_sec_base, n + 1));
     CDC_HIP(sc.alloc(&d_first, n + 1));
     CDC_HIP(sc.alloc(&d_sec_file, n_sec));
     CDC_HIP(sc.alloc(&d_cand, n_sec * prm.cap));
+    CDC_HIP(sc.alloc(&d_cand_h, n_sec * prm.cap));
+    CDC_HIP(sc.alloc(&d_cand_b, n_sec * prm.cap));
     CDC_HIP(sc.alloc(&d_cand_cnt, n_sec));
     CDC_HIP(sc.alloc(&d_spec, n_sec * prm.speccap));
     CDC_HIP(sc.alloc(&d_spec_cnt, n_sec));
@@ -669,10 +760,23 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     CDC_HIP(hipMemcpyAsync(d_sec_base, sec_base.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
     if (n_sec) CDC_HIP(hipMemcpyAsync(d_sec_file, sec_file.data(), n_sec * 4, hipMemcpyHostToDevice, st));
 
-    oxh::CdcFiles f{(const uint8_t*)d_arena, d_foff, d_flen, d_sec_base, d_sec_file, d_cand, d_cand_cnt, d_spec, d_spec_cnt};
+    oxh::CdcFiles f{(const uint8_t*)d_arena, d_foff, d_flen, d_sec_base, d_sec_file, d_cand, d_cand_h, d_cand_b, d_cand_cnt, d_spec, d_spec_cnt};
     oxh::CdcStitch sti{d_status, d_k0, d_count, d_exit, d_fix, d_out_base};
     if (n_sec) {
-        hipLaunchKernelGGL(oxh::cdc_scan_kernel, dim3((unsigned)((n_sec + 3) / 4)), dim3(256), 0, st, f, prm, n_sec);
+        // F1 shape (diagnostic override OXH_CDC_SCAN): 0 = one shared table, 4 waves/WG, 8 KiB in
+        // flight per wave (default); 1 = 32 bank-private table copies, 8 waves/WG (no LDS bank
+        // conflicts; measured no faster: F1 is VALU-issue-bound, not LDS-bound)
+        static const int scan_shape = getenv("OXH_CDC_SCAN") ? atoi(getenv("OXH_CDC_SCAN")) : 0;
+        const bool sh = (((prm.mask_s & prm.mask_l) << 16) & 0xFFFFFFFFull) == 0;
+        auto scan = sh ? oxh::cdc_scan_kernel<8, 1, 4, true> : oxh::cdc_scan_kernel<8, 1, 4, false>;
+        int waves = 4;
+        if (scan_shape == 1) {
+            scan = sh ? oxh::cdc_scan_kernel<8, 32, 8, true> : oxh::cdc_scan_kernel<8, 32, 8, false>;
+            waves = 8;
+        } else if (scan_shape == 2) {
+            scan = oxh::cdc_scan_kernel<8, 1, 4, false>;  // unshifted, for A/B
+        }
+        hipLaunchKernelGGL(scan, dim3((unsigned)((n_sec + waves - 1) / waves)), dim3(64 * waves), 0, st, f, prm, n_sec);
         CDC_HIP(hipGetLastError());
         hipLaunchKernelGGL(oxh::cdc_walk_kernel, dim3((unsigned)((n_sec + 255) / 256)), dim3(256), 0, st, f, prm, n_sec);
         CDC_HIP(hipGetLastError());
