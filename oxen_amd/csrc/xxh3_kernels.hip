@@ -183,10 +183,17 @@ __device__ __forceinline__ uint4 bload16(__amdgpu_buffer_rsrc_t rsrc, uint32_t v
 // The long path (len > 240) for one buffer, executed by one full wave. Writes out[0..1] from lane 0.
 // All input loads are raw buffer loads (gfx950 supports unaligned buffer access, so any start offset
 // is fine); the descriptor is re-based every 1 GiB so 32-bit offsets cover buffers of any length.
-template <int VARIANT, bool TEXT>
+//
+// BS (byte shift, 1..3; 0 = none): the item starts bs bytes past a dword boundary. Buffer loads at
+// such offsets run ~25 % slower than dword-aligned ones (measured: tools/k1_align_probe.py), so the
+// loads are issued from the dword-aligned base p - bs and every 16-byte piece is re-aligned in
+// registers with v_alignbyte_b32; the dword after a lane's piece comes from the next lane of its row
+// (DPP row_ror:15), for a row's last lane from the next load of the row, and for the last lane of
+// the last load from one extra dword load per round (4 active lanes).
+template <int VARIANT, bool TEXT, bool BS>
 __device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_t len,
                                           uint64_t* __restrict__ out, int lane, const uint64_t* lds_sec,
-                                          uint64_t* __restrict__ counts) {
+                                          uint64_t* __restrict__ counts, uint32_t bs = 0) {
     const int g = lane >> 4, q = (lane >> 2) & 3, k = lane & 3;
     uint32_t n_nl = 0, n_cont = 0;  // TEXT only
     // stripe keys: secret words (4j + q + 2k, +1)
@@ -210,8 +217,8 @@ __device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_
     // round rr lives in 1 GiB window rr >> 18; descriptor over that window (wave-uniform, SALU work)
     auto window_rsrc = [&](uint64_t rr) {
         const uint64_t base = (rr >> 18) << 30;
-        const uint64_t rem = len - base;
-        return __builtin_amdgcn_make_buffer_rsrc((void*)(p + base), (short)0,
+        const uint64_t rem = len - base + (BS ? bs : 0);
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(p + base - (BS ? bs : 0)), (short)0,
                                                  (int)(rem < 0x7FFFFFFFull ? rem : 0x7FFFFFFFull), kRsrcFlags);
     };
     // Rounds 0 .. nr-1 are full (4 scrambled blocks); round nr is the partial final round: blocks
@@ -226,13 +233,43 @@ __device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_
         const bool in_part = fin_row_full | (fin_row_part & ((uint64_t)(4 * j + q) < ns));
         return (rr < nr) | ((rr == nr) & in_part);
     };
-    auto load_round = [&](uint64_t rr, uint4 (&dst)[4]) {
+    auto load_round = [&](uint64_t rr, uint4 (&dst)[4], uint32_t& ext) {
         const __amdgpu_buffer_rsrc_t rsrc = window_rsrc(rr);
         const uint32_t vo = (uint32_t)(rr & 0x3FFFF) * 4096u + lane_off;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) dst[j] = bload16<Cfg<VARIANT>::NT>(rsrc, live_j(rr, j) ? vo + j * 256 : kOOB);
+        for (int j = 0; j < 4; ++j) {
+            // BS: the first lane of the stripe after a partial block's last live stripe loads too (its
+            // first dword completes the last live piece; dwords past the item read as 0)
+            const bool extra = BS && (rr == nr) & fin_row_part & ((uint64_t)(4 * j + q) == ns) & (k == 0);
+            dst[j] = bload16<Cfg<VARIANT>::NT>(rsrc, (live_j(rr, j) | extra) ? vo + j * 256 : kOOB);
+        }
+        if constexpr (BS) {
+            // the dword right after the row's block, for the row's last lane (lanes 15, 31, 47, 63)
+            const bool l15 = (lane & 15) == 15;
+            ext = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (l15 && live_j(rr, 3)) ? vo + 3 * 256 + 16 : kOOB, 0,
+                                                       Cfg<VARIANT>::NT ? 2 : 0);
+        } else {
+            ext = 0;
+        }
     };
-    auto fold4 = [&](const uint4 (&src)[4], uint64_t rr, bool partial) {
+    // BS: item bytes [o, o+16) of every piece from the aligned pieces (see above)
+    auto realign = [&](uint4 (&src)[4], uint32_t ext) {
+        if constexpr (BS) {
+            const bool l15 = (lane & 15) == 15;
+            uint32_t nb[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) nb[j] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)src[j].x, 0x12F, 0xf, 0xf, false);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t n0 = l15 ? (j < 3 ? nb[j + 1] : ext) : nb[j];
+                const uint4 a = src[j];
+                src[j] = make_uint4(__builtin_amdgcn_alignbyte(a.y, a.x, bs), __builtin_amdgcn_alignbyte(a.z, a.y, bs),
+                                    __builtin_amdgcn_alignbyte(a.w, a.z, bs), __builtin_amdgcn_alignbyte(n0, a.w, bs));
+            }
+        }
+    };
+    auto fold4 = [&](uint4 (&src)[4], uint32_t ext, uint64_t rr, bool partial) {
+        realign(src, ext);
         uint64_t s0 = 0, s1 = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -256,14 +293,15 @@ __device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_
         // short item (an 8 KiB chunk is 2 rounds) costs one memory round trip.
         constexpr int D = Cfg<VARIANT>::DEPTH;
         uint4 ring[D][4];
+        uint32_t ext[D];
 #pragma unroll
-        for (int d = 0; d < D; ++d) load_round((uint64_t)d, ring[d]);
+        for (int d = 0; d < D; ++d) load_round((uint64_t)d, ring[d], ext[d]);
         uint64_t r = 0;
         for (; r + D <= nr; r += D) {  // every slot holds a full round
 #pragma unroll
             for (int d = 0; d < D; ++d) {
-                fold4(ring[d], r + d, false);
-                load_round(r + d + D, ring[d]);
+                fold4(ring[d], ext[d], r + d, false);
+                load_round(r + d + D, ring[d], ext[d]);
                 // keep slot d+1's arithmetic below this point: otherwise the scheduler hoists its
                 // data-only adds above the refill and hipcc has to drain every load (vmcnt(0))
                 __builtin_amdgcn_sched_barrier(0);
@@ -272,8 +310,8 @@ __device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_
         // rounds r .. nr (at most D, the last one partial) are already in slots 0 .. nr - r
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            if (r + d < nr) fold4(ring[d], r + d, false);
-            else if (r + d == nr) fold4(ring[d], r + d, true);
+            if (r + d < nr) fold4(ring[d], ext[d], r + d, false);
+            else if (r + d == nr) fold4(ring[d], ext[d], r + d, true);
         }
     }
     // last stripe, at len - 64, with the secret shifted to offset 121
@@ -377,7 +415,13 @@ __device__ __forceinline__ void wave_item(const uint8_t* __restrict__ arena, con
         }
         return;
     }
-    wave_long<VARIANT, TEXT>(p, len, o, lane, lds_sec, TEXT ? counts + 2 * item : nullptr);
+    // byte-shifted items take the dword-aligned load path unless the last full stripe ends within 4 B
+    // of the item end (then the dword after it would straddle the end and read as 0)
+    const uint32_t bs = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
+    const uint64_t nb_ = (len - 1) >> 10;
+    const uint64_t E = (nb_ << 10) + ((((len - 1) - (nb_ << 10)) >> 6) << 6);
+    if (bs && len - E >= 4) wave_long<VARIANT, TEXT, true>(p, len, o, lane, lds_sec, TEXT ? counts + 2 * item : nullptr, bs);
+    else wave_long<VARIANT, TEXT, false>(p, len, o, lane, lds_sec, TEXT ? counts + 2 * item : nullptr);
 }
 
 template <bool DESC, int VARIANT>
