@@ -764,8 +764,10 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     oxh::CdcStitch sti{d_status, d_k0, d_count, d_exit, d_fix, d_out_base};
     if (n_sec) {
         // F1 shape (diagnostic override OXH_CDC_SCAN): 0 = one shared table, 4 waves/WG, 8 KiB in
-        // flight per wave (default); 1 = 32 bank-private table copies, 8 waves/WG (no LDS bank
-        // conflicts; measured no faster: F1 is VALU-issue-bound, not LDS-bound)
+        // flight per wave (default); 1 = 32 bank-private table copies, 8 waves/WG; 2 = unshifted
+        // hash domain. Measured: no LDS bank conflicts (1), ring depth 2-8, 5-8 waves
+        // per SIMD and two interleaved sub-blocks per wave all land within +-4 %: F1 is bound by
+        // VALU issue (~103 instructions per KiB, a third of them 64-bit shift-adds).
         static const int scan_shape = getenv("OXH_CDC_SCAN") ? atoi(getenv("OXH_CDC_SCAN")) : 0;
         const bool sh = (((prm.mask_s & prm.mask_l) << 16) & 0xFFFFFFFFull) == 0;
         auto scan = sh ? oxh::cdc_scan_kernel<8, 1, 4, true> : oxh::cdc_scan_kernel<8, 1, 4, false>;
