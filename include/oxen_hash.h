@@ -127,6 +127,15 @@ int oxh_clean_corrupted_versions(oxh_ctx* ctx, const char* versions_root, int dr
  * HBM pass; the caller uses them only for files it classifies as text. */
 int oxh_hash_files_text(oxh_ctx* ctx, const char* const* paths, uint64_t n, uint64_t* out,
                         uint64_t* sizes, int32_t* status, uint64_t* counts);
+/* K1T + the data-type sniff: as oxh_hash_files_text, plus is_utf8[i] = util::fs::is_utf8 of file i
+ * (util/fs.rs:652-668: its first min(size, 4096) bytes are UTF-8, or the first error is a sequence cut
+ * off by the end of that prefix; 0 for unreadable files), computed on the same staged bytes -- the
+ * mime/data-type decision of add.rs:809-810 then needs no third read of the file. */
+int oxh_hash_files_text_utf8(oxh_ctx* ctx, const char* const* paths, uint64_t n, uint64_t* out,
+                             uint64_t* sizes, int32_t* status, uint64_t* counts, int32_t* is_utf8);
+/* Device-resident is_utf8 sniff: d_flags[i] (int32) for item i of the arena (first 4 KiB). */
+int oxh_utf8_prefix_device(const void* d_arena, const uint64_t* d_offsets, const uint64_t* d_lens, uint64_t n,
+                           int32_t* d_flags, void* stream);
 /* Device-resident K1T: as oxh_xxh3_128_batch_device plus d_counts (2n u64: num_lines, num_chars). */
 int oxh_xxh3_128_text_batch_device(const void* d_arena, const uint64_t* d_offsets, const uint64_t* d_lens,
                                    uint64_t n, uint64_t* d_out, uint64_t* d_counts, void* stream);

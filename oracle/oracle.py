@@ -176,3 +176,43 @@ def clean_corrupted_versions(versions_root: str, dry_run: bool = False, threads:
             except OSError:
                 errors += 1
     return {"scanned": scanned, "corrupted": corrupted, "cleaned": cleaned, "errors": errors}
+
+
+def is_utf8_prefix(data: bytes) -> bool:
+    """util/fs.rs:652-668 (is_utf8) on bytes already read: the first min(len, 4096) bytes decode as
+    UTF-8, or the first error is a sequence cut off by the end ("unexpected end of data" = Rust's
+    Utf8Error::error_len() == None). Python's strict UTF-8 decoder (no surrogates, no overlongs,
+    <= U+10FFFF) applies the same validity rules as core::str::from_utf8."""
+    b = bytes(data[:4096])
+    if not b:
+        return True
+    try:
+        b.decode("utf-8")
+        return True
+    except UnicodeDecodeError as e:
+        return e.reason == "unexpected end of data"
+
+
+def is_utf8_prefix_dfa(data: bytes) -> bool:
+    """The same predicate as core::str::run_utf8_validation walks it (second-byte ranges per lead),
+    restated independently of Python's decoder; tests cross-check the two."""
+    b = bytes(data[:4096])
+    i, n = 0, len(b)
+    second = {0xE0: (0xA0, 0xBF), 0xED: (0x80, 0x9F), 0xF0: (0x90, 0xBF), 0xF4: (0x80, 0x8F)}
+    while i < n:
+        c = b[i]
+        if c < 0x80:
+            i += 1
+            continue
+        width = 2 if 0xC2 <= c <= 0xDF else 3 if 0xE0 <= c <= 0xEF else 4 if 0xF0 <= c <= 0xF4 else 0
+        if width == 0:
+            return False
+        lo, hi = second.get(c, (0x80, 0xBF))
+        for k in range(1, width):
+            if i + k >= n:
+                return True  # cut off by the end of the prefix
+            x = b[i + k]
+            if not ((lo <= x <= hi) if k == 1 else (0x80 <= x <= 0xBF)):
+                return False
+        i += width
+    return True

@@ -49,6 +49,8 @@ SIGNATURES = {
     "oxh_clean_corrupted_versions": (_int, [_vp, ctypes.c_char_p, _int, _u64p]),
     "oxh_hash_files_text": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64, _u64p, _u64p, _i32p, _u64p]),
     "oxh_xxh3_128_text_batch_device": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
+    "oxh_hash_files_text_utf8": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64, _u64p, _u64p, _i32p, _u64p, _i32p]),
+    "oxh_utf8_prefix_device": (_int, [_vp, _vp, _vp, _u64, _vp, _vp]),
     "oxh_combined_hash_device": (_int, [_vp, _vp, _u64, _vp, _vp]),
     "oxh_hash_streams": (_int, [_vp, _vp, _u64p, _u64p, _u64, _u64p]),
     "oxh_format_hex": (_int, [_u64, _u64, ctypes.c_char_p]),

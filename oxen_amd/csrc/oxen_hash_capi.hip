@@ -47,6 +47,7 @@ __global__ void fill_splitmix_kernel(uint64_t*, uint64_t, uint64_t);
 template <int VARIANT>
 __global__ void xxh3_text_wave_kernel(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t*, uint64_t*);
 __global__ void text_count_kernel(const uint8_t*, uint64_t, unsigned long long*);
+__global__ void utf8_prefix_kernel(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, int32_t*);
 __global__ void fill_splitmix_tail_kernel(uint8_t*, uint64_t, uint64_t, uint64_t);
 }  // namespace oxh
 
@@ -183,6 +184,9 @@ struct oxh_ctx {
     uint64_t* d_out[NSLOT] = {};
     uint64_t* h_cnt[NSLOT] = {};  // text counts (num_lines, num_chars) per item, K1T
     uint64_t* d_cnt[NSLOT] = {};
+    int32_t* h_utf8[NSLOT] = {};  // is_utf8 of each item's first 4 KiB (util/fs.rs:652-668)
+    int32_t* d_utf8[NSLOT] = {};
+    int32_t* utf8_out = nullptr;  // per call (calls on a context are serialised): where is_utf8 goes
     hipEvent_t ev_copied[NSLOT] = {}, ev_done[NSLOT] = {};
     oxh::Pool* pool = nullptr;   // readers / copiers (fill)
     oxh::Pool* wpool = nullptr;  // consumers of hashed bytes (fused publish), created on first use
@@ -270,6 +274,12 @@ int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_
     STEP("launched s=%d", s);
     HIP_TRY(hipMemcpyAsync(c->h_out[s], c->d_out[s], cnt * 16, hipMemcpyDeviceToHost, c->stream));
     if (text) HIP_TRY(hipMemcpyAsync(c->h_cnt[s], c->d_cnt[s], cnt * 16, hipMemcpyDeviceToHost, c->stream));
+    if (c->utf8_out) {  // is_utf8 sniff of the same staged bytes
+        hipLaunchKernelGGL(oxh::utf8_prefix_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, c->stream, c->d_stage[s],
+                           c->d_desc[s], c->d_desc[s] + M, cnt, c->d_utf8[s]);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(c->h_utf8[s], c->d_utf8[s], cnt * 4, hipMemcpyDeviceToHost, c->stream));
+    }
     HIP_TRY(hipEventRecord(c->ev_done[s], c->stream));
     STEP("submitted s=%d", s);
     return OXH_OK;
@@ -343,6 +353,8 @@ int drain_slot(oxh_ctx* c, int s, Pending& p, uint64_t* out, uint64_t* counts = 
             counts[2 * p.ids[j]] = c->h_cnt[s][2 * j];
             counts[2 * p.ids[j] + 1] = c->h_cnt[s][2 * j + 1];
         }
+    if (c->utf8_out)
+        for (size_t j = 0; j < p.ids.size(); ++j) c->utf8_out[p.ids[j]] = c->h_utf8[s][j];
     p.busy = false;
     if (sink) {
         // hand the slot to the consumer pool; the caller refills it only after join_consumer()
@@ -367,7 +379,8 @@ int drain_slot(oxh_ctx* c, int s, Pending& p, uint64_t* out, uint64_t* counts = 
 
 // Hash one oversize host item (> a staging slot) through a temporary device buffer; with `cnt2`,
 // also its text counts (num_lines, num_chars).
-int oversize_item(oxh_ctx* c, const uint8_t* src, uint64_t len, uint64_t* out2, uint64_t* cnt2 = nullptr) {
+int oversize_item(oxh_ctx* c, const uint8_t* src, uint64_t len, uint64_t* out2, uint64_t* cnt2 = nullptr,
+                  int32_t* utf8_1 = nullptr) {
     uint8_t* d = nullptr;
     if (hipMalloc(&d, len) != hipSuccess) return fail(OXH_ERR_NOMEM, "oversize hipMalloc failed");
     int rc = OXH_OK;
@@ -388,6 +401,21 @@ int oversize_item(oxh_ctx* c, const uint8_t* src, uint64_t len, uint64_t* out2, 
         if (rc == OXH_OK && hipMemcpyAsync(c->h_cnt[0], c->d_cnt[0], 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
             rc = fail(OXH_ERR_HIP, "oversize counts D2H failed");
     }
+    if (rc == OXH_OK && utf8_1) {
+        // one item: offset 0, length len, through the slot-0 descriptor arrays
+        c->h_desc[0][0] = 0;
+        c->h_desc[0][c->max_items] = len;
+        if (hipMemcpyAsync(c->d_desc[0], c->h_desc[0], 8, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+            hipMemcpyAsync(c->d_desc[0] + c->max_items, c->h_desc[0] + c->max_items, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+            rc = fail(OXH_ERR_HIP, "oversize utf8 descriptors");
+        if (rc == OXH_OK) {
+            hipLaunchKernelGGL(oxh::utf8_prefix_kernel, dim3(1), dim3(64), 0, c->stream, d, c->d_desc[0], c->d_desc[0] + c->max_items,
+                               (uint64_t)1, c->d_utf8[0]);
+            if (hipGetLastError() != hipSuccess) rc = fail(OXH_ERR_HIP, "utf8_prefix_kernel launch");
+        }
+        if (rc == OXH_OK && hipMemcpyAsync(c->h_utf8[0], c->d_utf8[0], 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+            rc = fail(OXH_ERR_HIP, "oversize utf8 D2H failed");
+    }
     if (rc == OXH_OK && hipMemcpyAsync(c->h_out[0], c->d_out[0], 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
         rc = fail(OXH_ERR_HIP, "oversize D2H failed");
     if (rc == OXH_OK && hipStreamSynchronize(c->stream) != hipSuccess) rc = fail(OXH_ERR_HIP, "oversize sync failed");
@@ -398,6 +426,7 @@ int oversize_item(oxh_ctx* c, const uint8_t* src, uint64_t len, uint64_t* out2, 
             cnt2[0] = 1 + c->h_cnt[0][0];
             cnt2[1] = len - c->h_cnt[0][1];
         }
+        if (utf8_1) *utf8_1 = c->h_utf8[0][0];
     }
     (void)hipFree(d);
     return rc;
@@ -442,6 +471,8 @@ int oxh_ctx_create(int device, uint64_t staging_bytes, oxh_ctx** out) {
         if (hipMalloc(&c->d_out[s], c->max_items * 16) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "device out");
         if (hipHostMalloc(&c->h_cnt[s], c->max_items * 16, hipHostMallocDefault) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "pinned counts");
         if (hipMalloc(&c->d_cnt[s], c->max_items * 16) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "device counts");
+        if (hipHostMalloc(&c->h_utf8[s], c->max_items * 4, hipHostMallocDefault) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "pinned utf8");
+        if (hipMalloc(&c->d_utf8[s], c->max_items * 4) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "device utf8");
         if (hipEventCreateWithFlags(&c->ev_copied[s], hipEventDisableTiming) != hipSuccess) return cleanup(OXH_ERR_HIP, "event");
         if (hipEventCreateWithFlags(&c->ev_done[s], hipEventDisableTiming) != hipSuccess) return cleanup(OXH_ERR_HIP, "event");
     }
@@ -464,6 +495,8 @@ int oxh_ctx_destroy(oxh_ctx* c) {
         if (c->d_out[s]) (void)hipFree(c->d_out[s]);
         if (c->h_cnt[s]) (void)hipHostFree(c->h_cnt[s]);
         if (c->d_cnt[s]) (void)hipFree(c->d_cnt[s]);
+        if (c->h_utf8[s]) (void)hipHostFree(c->h_utf8[s]);
+        if (c->d_utf8[s]) (void)hipFree(c->d_utf8[s]);
         if (c->ev_copied[s]) (void)hipEventDestroy(c->ev_copied[s]);
         if (c->ev_done[s]) (void)hipEventDestroy(c->ev_done[s]);
     }
@@ -911,7 +944,8 @@ static int stream_files(oxh_ctx* c, const char* const* paths, uint64_t n, uint64
             fs.st[i] = OXH_ERR_IO;
             continue;
         }
-        rc = oversize_item(c, tmp.data(), fs.lens[i], out + 2 * i, counts ? counts + 2 * i : nullptr);
+        rc = oversize_item(c, tmp.data(), fs.lens[i], out + 2 * i, counts ? counts + 2 * i : nullptr,
+                           c->utf8_out ? c->utf8_out + i : nullptr);
         if (rc) return rc;
         if (sink) (*sink)(i, tmp.data(), fs.lens[i], out[2 * i], out[2 * i + 1]);
     }
@@ -922,6 +956,7 @@ static int stream_files(oxh_ctx* c, const char* const* paths, uint64_t n, uint64
         if (fs.st[i] != OXH_OK) {
             out[2 * i] = out[2 * i + 1] = 0;
             if (counts) counts[2 * i] = counts[2 * i + 1] = 0;
+            if (c->utf8_out) c->utf8_out[i] = 0;  // read_first_n_bytes failed -> is_utf8 false (fs.rs:655-658)
         }
         if (lens_out) lens_out[i] = fs.lens[i];
         if (st_out) st_out[i] = fs.st[i];
@@ -930,9 +965,14 @@ static int stream_files(oxh_ctx* c, const char* const* paths, uint64_t n, uint64
 }
 
 static int hash_files_impl(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* sizes, int32_t* status,
-                           uint64_t* counts, const ItemSink* sink = nullptr) {
+                           uint64_t* counts, const ItemSink* sink = nullptr, int32_t* utf8 = nullptr) {
     if (!c || (n && (!paths || !out))) return fail(OXH_ERR_INVALID, "bad arguments");
     std::lock_guard<std::mutex> g(c->mu);
+    struct Utf8Out {  // the context's per-call is_utf8 destination, cleared before the lock is released
+        oxh_ctx* c;
+        ~Utf8Out() { c->utf8_out = nullptr; }
+    } u8{c};
+    c->utf8_out = utf8;
     HIP_TRY(hipSetDevice(c->device));
     if (n == 0) return OXH_OK;
     return stream_files(c, paths, n, out, sizes, status, counts, sink);
@@ -946,6 +986,13 @@ int oxh_hash_files_text(oxh_ctx* c, const char* const* paths, uint64_t n, uint64
                         uint64_t* counts) {
     if (n && !counts) return fail(OXH_ERR_INVALID, "counts is NULL");
     return hash_files_impl(c, paths, n, out, sizes, status, counts);
+}
+
+int oxh_hash_files_text_utf8(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* sizes,
+                             int32_t* status, uint64_t* counts, int32_t* is_utf8) {
+    if (n && (!counts || !is_utf8)) return fail(OXH_ERR_INVALID, "counts / is_utf8 is NULL");
+    for (uint64_t i = 0; i < n; ++i) is_utf8[i] = 0;
+    return hash_files_impl(c, paths, n, out, sizes, status, counts, nullptr, is_utf8);
 }
 
 // Publish `data` as the version blob of digest (lo, hi): {root}/{hex[..2]}/{hex[2..]}/data
@@ -1120,6 +1167,16 @@ int oxh_xxh3_128_text_batch_device(const void* d_arena, const uint64_t* d_offset
     if (n == 0) return OXH_OK;
     if (!d_arena || !d_offsets || !d_lens || !d_out || !d_counts) return fail(OXH_ERR_INVALID, "NULL device pointer");
     return launch_text((const uint8_t*)d_arena, d_offsets, d_lens, n, d_out, d_counts, (hipStream_t)stream);
+}
+
+int oxh_utf8_prefix_device(const void* d_arena, const uint64_t* d_offsets, const uint64_t* d_lens, uint64_t n,
+                           int32_t* d_flags, void* stream) {
+    if (n == 0) return OXH_OK;
+    if (!d_arena || !d_offsets || !d_lens || !d_flags) return fail(OXH_ERR_INVALID, "NULL device pointer");
+    hipLaunchKernelGGL(oxh::utf8_prefix_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const uint8_t*)d_arena, d_offsets, d_lens, n, d_flags);
+    HIP_TRY(hipGetLastError());
+    return OXH_OK;
 }
 
 int oxh_fill_splitmix(void* d_buf, uint64_t nbytes, uint64_t seed, void* stream) {

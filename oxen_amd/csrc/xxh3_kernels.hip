@@ -599,6 +599,69 @@ __global__ __launch_bounds__(64) void xxh3_chain_kernel(ChainBatch batch) {
     }
 }
 
+// util::fs::is_utf8 (util/fs.rs:652-668): the first min(len, 4096) bytes are valid UTF-8, or the
+// first error is a multi-byte sequence cut off by the end of that prefix (Utf8Error::error_len() ==
+// None); an empty file is UTF-8. Restates core::str::from_utf8's validation (ASCII, C2-DF + 1,
+// E0 A0-BF, E1-EC/EE-EF 80-BF, ED 80-9F, F0 90-BF, F1-F3 80-BF, F4 80-8F, then 80-BF continuations).
+// One lane per item, 16-byte loads; runs beside K1T on the staged bytes, so the data-type sniff
+// add.rs:809-810 makes (file_mime_type -> is_utf8) needs no third read of the file.
+__device__ __forceinline__ bool utf8_second_ok(uint32_t lead, uint32_t b) {
+    if (lead == 0xE0) return b >= 0xA0 && b <= 0xBF;
+    if (lead == 0xED) return b >= 0x80 && b <= 0x9F;
+    if (lead == 0xF0) return b >= 0x90 && b <= 0xBF;
+    if (lead == 0xF4) return b >= 0x80 && b <= 0x8F;
+    return (b & 0xC0) == 0x80;
+}
+
+__device__ int32_t utf8_prefix_ok(const uint8_t* __restrict__ p, uint64_t len) {
+    const uint32_t n = (uint32_t)(len < 4096 ? len : 4096);
+    uint32_t need = 0, width = 0, lead = 0;  // continuation bytes still expected for the open sequence
+    for (uint32_t base = 0; base < n; base += 16) {
+        uint32_t w[4] = {0, 0, 0, 0};
+        if (base + 16 <= n) {
+            uint4 v;
+            __builtin_memcpy(&v, p + base, 16);
+            w[0] = v.x;
+            w[1] = v.y;
+            w[2] = v.z;
+            w[3] = v.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                if (base + j < n) w[j >> 2] |= (uint32_t)p[base + j] << (8 * (j & 3));
+        }
+        const uint32_t m = n - base < 16 ? n - base : 16;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if ((uint32_t)j >= m) break;
+            const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xFF;
+            if (need) {
+                const bool ok = (need == width - 1) ? utf8_second_ok(lead, b) : ((b & 0xC0) == 0x80);
+                if (!ok) return 0;
+                --need;
+                continue;
+            }
+            if (b < 0x80) continue;
+            if (b >= 0xC2 && b <= 0xDF) width = 2;
+            else if (b >= 0xE0 && b <= 0xEF) width = 3;
+            else if (b >= 0xF0 && b <= 0xF4) width = 4;
+            else return 0;  // continuation byte, C0, C1 or F5-FF: error_len Some(1)
+            lead = b;
+            need = width - 1;
+        }
+    }
+    return 1;  // valid, or a sequence still open at the end of the prefix (error_len None)
+}
+
+__global__ __launch_bounds__(256) void utf8_prefix_kernel(const uint8_t* __restrict__ arena,
+                                                          const uint64_t* __restrict__ offsets,
+                                                          const uint64_t* __restrict__ lens, uint64_t n,
+                                                          int32_t* __restrict__ flags) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    flags[i] = utf8_prefix_ok(arena + offsets[i], lens[i]);
+}
+
 // Text counts of one large buffer without hashing it (oversize text files, whose digest comes from
 // K1L): counts[0] += newlines, counts[1] += UTF-8 continuation bytes (caller zeroes counts first).
 __global__ __launch_bounds__(256) void text_count_kernel(const uint8_t* __restrict__ p, uint64_t len,

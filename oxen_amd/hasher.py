@@ -163,6 +163,35 @@ def hash_files_text_128bit(paths: Sequence[str], ctx: Optional[_capi.Context] = 
     return digests, [int(s) for s in sizes], [int(s) for s in status], meta
 
 
+def hash_files_text_utf8_128bit(paths: Sequence[str], ctx: Optional[_capi.Context] = None):
+    """hash_files_text_128bit plus util::fs::is_utf8 (util/fs.rs:652-668) of every file, all from one
+    read of each file: returns (digests, sizes, status, metadata, is_utf8)."""
+    ctx = ctx or default_context()
+    n = len(paths)
+    if n == 0:
+        return [], [], [], [], []
+    arr = (ctypes.c_char_p * n)(*[os.fsencode(str(p)) for p in paths])
+    out = np.zeros((n, 2), dtype=np.uint64)
+    sizes = np.zeros(n, dtype=np.uint64)
+    status = np.zeros(n, dtype=np.int32)
+    counts = np.zeros((n, 2), dtype=np.uint64)
+    utf8 = np.zeros(n, dtype=np.int32)
+    _capi.check(_capi.lib().oxh_hash_files_text_utf8(ctx.handle, arr, n, out.ctypes.data_as(_capi._u64p),
+                                                     sizes.ctypes.data_as(_capi._u64p),
+                                                     status.ctypes.data_as(_capi._i32p),
+                                                     counts.ctypes.data_as(_capi._u64p),
+                                                     utf8.ctypes.data_as(_capi._i32p)), "oxh_hash_files_text_utf8")
+    digests = [(_to_u128(lo, hi) if st == 0 else None) for (lo, hi), st in zip(out, status)]
+    meta = [({"text": {"num_lines": int(c[0]), "num_chars": int(c[1])}} if st == 0 else None)
+            for c, st in zip(counts, status)]
+    return digests, [int(s) for s in sizes], [int(s) for s in status], meta, [bool(u) for u in utf8]
+
+
+def is_utf8(path) -> bool:
+    """util/fs.rs:652-668 (one file; the batched form is hash_files_text_utf8_128bit)."""
+    return hash_files_text_utf8_128bit([path])[4][0]
+
+
 def text_file_nodes(paths: Sequence[str], ctx: Optional[_capi.Context] = None):
     """The hashing half of add.rs:833-842 for text files, batched: content hash and text counts in one
     GPU pass (K1T), then metadata_hash = XXH3(serde_json(metadata)) and combined_hash =

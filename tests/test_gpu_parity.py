@@ -483,3 +483,71 @@ def test_commit_driver_image_repo_shape(ctx):
     rvn, rdh = commit_oracle.commit_tree(entries, {}, 10_000, _commit.salt)
     assert {d: [v.id.value for v in vn[d][0]] for d in vn} == {d: [i for i, _ in rvn[d]] for d in rvn}
     assert {d: h.value for d, h in dh.items()} == rdh
+
+
+def _utf8_cases():
+    import random
+
+    rng = random.Random(9)
+    pieces = [b"a", b"\xc3\xa9", b"\xe2\x82\xac", b"\xf0\x9f\x98\x80", b"\xed\x9f\xbf", b"\xf4\x8f\xbf\xbf", b"\xc0",
+              b"\xc1\x80", b"\xe0\x80\x80", b"\xed\xa0\x80", b"\xf4\x90\x80\x80", b"\xf5", b"\xff", b"\x80", b"\x0a"]
+    cases = [b"", b"hello", b"\xe2\x82", b"\xe2\x28", b"a" * 4096 + b"\xff", b"a" * 4095 + b"\xe2\x82\xac",
+             b"a" * 4094 + b"\xe2\x82\xac", b"a" * 4093 + b"\xf0\x9f\x98\x80", b"a" * 4095 + b"\xe0\x80",
+             "héllo wörld €".encode() * 500]
+    for _ in range(600):
+        s = b"".join(rng.choice(pieces) for _ in range(rng.randint(0, 60)))
+        if rng.random() < 0.3:
+            s = s[: rng.randint(0, len(s))]
+        if rng.random() < 0.3:
+            s = b"t" * rng.randint(4000, 4100) + s
+        cases.append(s)
+    return cases
+
+
+def test_utf8_sniff_device(cuda, oracle_lib):
+    """util::fs::is_utf8 (util/fs.rs:652-668) on the device, vs the oracle, at misaligned offsets."""
+    import torch
+
+    from oxen_amd import _capi
+
+    cases = _utf8_cases()
+    offs, pos = [], 0
+    for c in cases:
+        offs.append(pos)
+        pos += len(c) + 5
+    arena = np.zeros(max(pos, 1), dtype=np.uint8)
+    for o, c in zip(offs, cases):
+        arena[o:o + len(c)] = np.frombuffer(c, dtype=np.uint8)
+    d_arena = torch.from_numpy(arena).to(cuda)
+    d_offs = torch.tensor(offs, dtype=torch.int64, device=cuda)
+    d_lens = torch.tensor([len(c) for c in cases], dtype=torch.int64, device=cuda)
+    flags = torch.empty(len(cases), dtype=torch.int32, device=cuda)
+    _capi.check(_capi.lib().oxh_utf8_prefix_device(d_arena.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), len(cases),
+                                                   flags.data_ptr(), 0), "oxh_utf8_prefix_device")
+    torch.cuda.synchronize()
+    got = flags.cpu().numpy().tolist()
+    want = [int(oracle_lib.is_utf8_prefix(c)) for c in cases]
+    assert got == want
+
+
+def test_hash_files_text_utf8(ctx, oracle_lib, tmp_path):
+    """One read per file: digest, text counts and is_utf8, including oversize files (> staging) and
+    unreadable paths."""
+    from oxen_amd import _capi, hasher
+
+    cases = _utf8_cases()[:200] + [b"\xff" + b"a" * (3 << 20), "ü".encode() * (2 << 20)]
+    paths = []
+    for i, c in enumerate(cases):
+        p = tmp_path / f"f{i}.txt"
+        p.write_bytes(c)
+        paths.append(str(p))
+    paths.append(str(tmp_path / "missing.txt"))
+    with _capi.Context(0, staging_bytes=1 << 20) as c:
+        d, sizes, st, meta, utf8 = hasher.hash_files_text_utf8_128bit(paths, c)
+    assert st[-1] != 0 and utf8[-1] is False and d[-1] is None
+    out, _, _ = oracle_lib.hash_files(paths[:-1], threads=8)
+    assert [(int(hi) << 64) | int(lo) for lo, hi in out] == d[:-1]
+    assert utf8[:-1] == [oracle_lib.is_utf8_prefix(c) for c in cases]
+    for c, m in zip(cases, meta):
+        assert m["text"]["num_lines"] == 1 + c.count(b"\n")
+        assert m["text"]["num_chars"] == len(c) - sum(1 for x in c if (x & 0xC0) == 0x80)

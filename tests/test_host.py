@@ -133,3 +133,25 @@ def test_thread_pool_stress(tmp_path):
                     os.path.join(root, "tests", "native", "pool_stress.cpp"), "-o", exe], check=True)
     r = subprocess.run([exe, "100000"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "done" in r.stdout
+
+
+def test_utf8_oracles_agree():
+    """is_utf8 (util/fs.rs:652-668): Python's strict decoder and the from_utf8 walk restated agree."""
+    import random
+
+    from oracle import oracle
+
+    rng = random.Random(4)
+    pieces = [b"a", b"\xc3\xa9", b"\xe2\x82\xac", b"\xf0\x9f\x98\x80", b"\xed\x9f\xbf", b"\xf4\x8f\xbf\xbf",
+              b"\xc0", b"\xc1\x80", b"\xe0\x80\x80", b"\xed\xa0\x80", b"\xf4\x90\x80\x80", b"\xf5", b"\xff", b"\x80",
+              b"\xe2\x82", b"\xf0\x9f", b"\x0a"]
+    for _ in range(3000):
+        s = b"".join(rng.choice(pieces) for _ in range(rng.randint(0, 40)))
+        if rng.random() < 0.3:
+            s = s[: rng.randint(0, len(s))]
+        if rng.random() < 0.2:
+            s = b"x" * (4096 - rng.randint(0, 3)) + s
+        assert oracle.is_utf8_prefix(s) == oracle.is_utf8_prefix_dfa(s), s[-8:]
+    assert oracle.is_utf8_prefix(b"") and oracle.is_utf8_prefix(b"\xe2\x82")
+    assert not oracle.is_utf8_prefix(b"\xe2\x28")
+    assert oracle.is_utf8_prefix(b"a" * 4096 + b"\xff")  # only the first 4 KiB count
