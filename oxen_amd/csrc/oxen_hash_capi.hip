@@ -187,9 +187,14 @@ struct oxh_ctx {
     int32_t* h_utf8[NSLOT] = {};  // is_utf8 of each item's first 4 KiB (util/fs.rs:652-668)
     int32_t* d_utf8[NSLOT] = {};
     int32_t* utf8_out = nullptr;  // per call (calls on a context are serialised): where is_utf8 goes
+    // file-request coalescer (see hash_files_impl): requests queue here while a leader thread runs
+    std::mutex qmu;
+    std::vector<struct FileRequest*> queue;
+    bool leader = false;
     hipEvent_t ev_copied[NSLOT] = {}, ev_done[NSLOT] = {};
     oxh::Pool* pool = nullptr;   // readers / copiers (fill)
     oxh::Pool* wpool = nullptr;  // consumers of hashed bytes (fused publish), created on first use
+    oxh::Pool* rpool = nullptr;  // streaming-pipeline file readers (stream_files)
     std::mutex mu;
 };
 
@@ -477,6 +482,7 @@ int oxh_ctx_create(int device, uint64_t staging_bytes, oxh_ctx** out) {
         if (hipEventCreateWithFlags(&c->ev_done[s], hipEventDisableTiming) != hipSuccess) return cleanup(OXH_ERR_HIP, "event");
     }
     c->pool = new oxh::Pool(default_threads());
+    c->rpool = new oxh::Pool(default_threads());
     *out = c;
     return OXH_OK;
 }
@@ -504,6 +510,7 @@ int oxh_ctx_destroy(oxh_ctx* c) {
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     delete c->pool;
     delete c->wpool;
+    delete c->rpool;
     delete c;
     return OXH_OK;
 }
@@ -858,11 +865,12 @@ static int stream_files(oxh_ctx* c, const char* const* paths, uint64_t n, uint64
     fs.slot[0].word.store(1ull << kGenShift);
     Trace tr;
     const double t_start = Trace::now();
-    const int nreaders = (int)std::max<uint64_t>(1, std::min<uint64_t>(n, (uint64_t)c->pool->size()));
+    const int nreaders = (int)std::max<uint64_t>(1, std::min<uint64_t>(n, (uint64_t)c->rpool->size()));
     fs.readers_left.store(nreaders);
-    std::vector<std::thread> readers;
-    readers.reserve(nreaders);
-    for (int r = 0; r < nreaders; ++r) readers.emplace_back([&fs] { reader_loop(fs); });
+    // the readers run on the context's persistent reader pool (no thread start-up per call)
+    oxh::Pool::Group readers;
+    const std::function<void(int)> reader_fn = [&fs](int) { reader_loop(fs); };
+    c->rpool->start(nreaders, reader_fn, readers);
     Pending pend[NSLOT];
     int rc = OXH_OK;
     const uint64_t M = c->max_items;
@@ -920,7 +928,7 @@ static int stream_files(oxh_ctx* c, const char* const* paths, uint64_t n, uint64
         s = (s + 1) % NSLOT;
     }
     if (rc) fs.abort.store(true);
-    for (auto& th : readers) th.join();
+    readers.wait();
     const double t3 = Trace::now();
     for (int k = 0; k < NSLOT && rc == OXH_OK; ++k) rc = drain_slot(c, k, pend[k], out, counts, sink, fs.st.data());
     for (int k = 0; k < NSLOT; ++k) join_consumer(pend[k]);
@@ -964,18 +972,115 @@ static int stream_files(oxh_ctx* c, const char* const* paths, uint64_t n, uint64
     return OXH_OK;
 }
 
-static int hash_files_impl(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* sizes, int32_t* status,
-                           uint64_t* counts, const ItemSink* sink = nullptr, int32_t* utf8 = nullptr) {
-    if (!c || (n && (!paths || !out))) return fail(OXH_ERR_INVALID, "bad arguments");
+// ---------------------------------------------------------------- request coalescer
+// liboxen hashes 64-file batches from up to 2 x ncpu tokio tasks at once (add.rs:41, 422-425): a few
+// MB per call, far too small for one launch each. Concurrent file requests on a context therefore
+// coalesce ("group commit"): a caller that finds no leader becomes the leader and runs the streaming
+// pipeline over every request queued at that moment as ONE item list; callers arriving meanwhile
+// queue and sleep; when a run ends, the leader completes its batch and hands leadership to the
+// oldest queued caller. Outputs are scattered back per request; each request keeps its own sink
+// (fused add), text counts and is_utf8 destinations.
+struct FileRequest {
+    const char* const* paths;
+    uint64_t n;
+    uint64_t* out;
+    uint64_t* sizes;
+    int32_t* status;
+    uint64_t* counts;
+    int32_t* utf8;
+    const ItemSink* sink;
+    int rc = OXH_OK;
+    std::string msg;
+    bool done = false, lead = false;
+    std::condition_variable cv;
+};
+
+static int run_requests(oxh_ctx* c, const std::vector<FileRequest*>& batch) {
     std::lock_guard<std::mutex> g(c->mu);
-    struct Utf8Out {  // the context's per-call is_utf8 destination, cleared before the lock is released
+    struct Utf8Out {  // the context's per-run is_utf8 destination, cleared before the lock is released
         oxh_ctx* c;
         ~Utf8Out() { c->utf8_out = nullptr; }
     } u8{c};
-    c->utf8_out = utf8;
     HIP_TRY(hipSetDevice(c->device));
-    if (n == 0) return OXH_OK;
-    return stream_files(c, paths, n, out, sizes, status, counts, sink);
+    if (batch.size() == 1) {  // the common, uncontended case: no copies
+        FileRequest* r = batch[0];
+        c->utf8_out = r->utf8;
+        return r->n ? stream_files(c, r->paths, r->n, r->out, r->sizes, r->status, r->counts, r->sink) : OXH_OK;
+    }
+    std::vector<uint64_t> base(batch.size() + 1, 0);
+    bool want_counts = false, want_utf8 = false, want_sink = false;
+    for (size_t k = 0; k < batch.size(); ++k) {
+        base[k + 1] = base[k] + batch[k]->n;
+        want_counts |= batch[k]->counts != nullptr;
+        want_utf8 |= batch[k]->utf8 != nullptr;
+        want_sink |= batch[k]->sink != nullptr;
+    }
+    const uint64_t N = base.back();
+    if (N == 0) return OXH_OK;
+    std::vector<const char*> paths(N);
+    for (size_t k = 0; k < batch.size(); ++k)
+        for (uint64_t i = 0; i < batch[k]->n; ++i) paths[base[k] + i] = batch[k]->paths[i];
+    std::vector<uint64_t> out(2 * N), lens(N), counts(want_counts ? 2 * N : 0);
+    std::vector<int32_t> st(N), utf8(want_utf8 ? N : 0);
+    ItemSink sink = [&](uint64_t id, const uint8_t* bytes, uint64_t len, uint64_t lo, uint64_t hi) {
+        const size_t k = (size_t)(std::upper_bound(base.begin(), base.end(), id) - base.begin()) - 1;
+        if (batch[k]->sink) (*batch[k]->sink)(id - base[k], bytes, len, lo, hi);
+    };
+    c->utf8_out = want_utf8 ? utf8.data() : nullptr;
+    const int rc = stream_files(c, paths.data(), N, out.data(), lens.data(), st.data(),
+                                want_counts ? counts.data() : nullptr, want_sink ? &sink : nullptr);
+    if (rc) return rc;
+    for (size_t k = 0; k < batch.size(); ++k) {
+        FileRequest* r = batch[k];
+        const uint64_t b = base[k];
+        std::copy(out.begin() + 2 * b, out.begin() + 2 * (b + r->n), r->out);
+        if (r->sizes) std::copy(lens.begin() + b, lens.begin() + b + r->n, r->sizes);
+        if (r->status) std::copy(st.begin() + b, st.begin() + b + r->n, r->status);
+        if (r->counts) std::copy(counts.begin() + 2 * b, counts.begin() + 2 * (b + r->n), r->counts);
+        if (r->utf8) std::copy(utf8.begin() + b, utf8.begin() + b + r->n, r->utf8);
+    }
+    return OXH_OK;
+}
+
+static int hash_files_impl(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* sizes, int32_t* status,
+                           uint64_t* counts, const ItemSink* sink = nullptr, int32_t* utf8 = nullptr) {
+    if (!c || (n && (!paths || !out))) return fail(OXH_ERR_INVALID, "bad arguments");
+    FileRequest r;
+    r.paths = paths;
+    r.n = n;
+    r.out = out;
+    r.sizes = sizes;
+    r.status = status;
+    r.counts = counts;
+    r.utf8 = utf8;
+    r.sink = sink;
+    std::unique_lock<std::mutex> lk(c->qmu);
+    c->queue.push_back(&r);
+    if (c->leader) {
+        r.cv.wait(lk, [&] { return r.done || r.lead; });
+        if (r.done) return r.rc ? fail(r.rc, r.msg) : OXH_OK;
+    }
+    // leader: run everything queued now (this request included) as one pipeline
+    c->leader = true;
+    std::vector<FileRequest*> batch;
+    batch.swap(c->queue);
+    lk.unlock();
+    const int rc = run_requests(c, batch);
+    const std::string msg = rc ? g_err : std::string();
+    lk.lock();
+    for (FileRequest* q : batch) {
+        q->rc = rc;
+        q->msg = msg;
+        q->done = true;
+        if (q != &r) q->cv.notify_all();
+    }
+    if (!c->queue.empty()) {  // hand over to the oldest waiting caller
+        c->queue.front()->lead = true;
+        c->queue.front()->cv.notify_all();
+    } else {
+        c->leader = false;
+    }
+    return rc;
 }
 
 int oxh_hash_files(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* sizes, int32_t* status) {

@@ -54,6 +54,35 @@ class Pool {
         idle_cv_.wait(g, [&] { return busy_ == 0 && q_.empty(); });
     }
 
+    // Start fn(t) for t in [0, ntasks) on the pool WITHOUT waiting; wait() on the returned group
+    // blocks until all have returned. The caller keeps working meanwhile (the streaming pipeline's
+    // coordinator runs on the calling thread while the readers run here).
+    struct Group {
+        std::mutex mu;
+        std::condition_variable cv;
+        int left = 0;
+        void wait() {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return left == 0; });
+        }
+    };
+    void start(int ntasks, const std::function<void(int)>& fn, Group& grp) {
+        {
+            std::lock_guard<std::mutex> g(grp.mu);
+            grp.left = ntasks;
+        }
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            for (int t = 0; t < ntasks; ++t)
+                q_.push_back([&fn, &grp, t] {
+                    fn(t);
+                    std::lock_guard<std::mutex> g2(grp.mu);
+                    if (--grp.left == 0) grp.cv.notify_all();
+                });
+        }
+        cv_.notify_all();
+    }
+
    private:
     void run() {
         for (;;) {

@@ -551,3 +551,49 @@ def test_hash_files_text_utf8(ctx, oracle_lib, tmp_path):
     for c, m in zip(cases, meta):
         assert m["text"]["num_lines"] == 1 + c.count(b"\n")
         assert m["text"]["num_chars"] == len(c) - sum(1 for x in c if (x & 0xC0) == 0x80)
+
+
+def test_concurrent_callers_coalesce(oracle_lib, tmp_path, cuda):
+    """liboxen calls the hasher from many tokio tasks at once, 64 files per batch (add.rs:41,
+    422-425): concurrent oxh_hash_files / oxh_add_files / oxh_hash_files_text_utf8 calls on one
+    context coalesce into shared pipeline runs, and every caller gets exactly its own results."""
+    import threading
+
+    from oxen_amd import _capi, hasher
+    from oxen_amd.workloads import splitmix_bytes
+
+    rng = np.random.default_rng(21)
+    paths = []
+    for i in range(16 * 64):
+        p = tmp_path / f"f{i}.bin"
+        p.write_bytes(splitmix_bytes(500 + i, 0, int(rng.integers(0, 70_000))).tobytes())
+        paths.append(str(p))
+    want_out, _, _ = oracle_lib.hash_files(paths, threads=8)
+    want = [(int(hi) << 64) | int(lo) for lo, hi in want_out]
+    results, errors = {}, []
+    with _capi.Context(0, staging_bytes=4 << 20) as c:
+        def worker(t):
+            try:
+                batch = paths[t * 64:(t + 1) * 64] + ([str(tmp_path / "missing")] if t % 3 == 0 else [])
+                if t % 4 == 1:
+                    d, _, st, _ = hasher.add_files(batch, str(tmp_path / "store" / f"t{t}"), c)
+                elif t % 4 == 2:
+                    d, _, st, _, _ = hasher.hash_files_text_utf8_128bit(batch, c)
+                else:
+                    d, _, st = hasher.hash_files_128bit(batch, c)
+                results[t] = (d, st)
+            except Exception as e:  # pragma: no cover - reported below
+                errors.append(repr(e))
+
+        for _round in range(3):
+            th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            assert not errors, errors
+            for t in range(16):
+                d, st = results[t]
+                assert d[:64] == want[t * 64:(t + 1) * 64], t
+                if t % 3 == 0:
+                    assert st[64] != 0 and d[64] in (None, 0)
