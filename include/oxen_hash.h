@@ -14,8 +14,9 @@
  *   - every function returns an int status (OXH_OK == 0); batch calls also fill a per-item
  *     `status[]` so one unreadable file never fails the batch (add.rs:533-544 logs and skips);
  *   - the library never frees caller memory and retains no caller pointer after returning;
- *   - all entry points are thread-safe; concurrent file calls on one context coalesce into shared
- *     pipeline runs (group commit: one caller leads, the others queue), other calls serialise;
+ *   - all entry points are thread-safe; file calls on one context are requests to the context's
+ *     streaming engine, and concurrent ones share its live pipeline (each caller returns when its
+ *     own files are done); other calls on a context serialise;
  *   - there is no CPU fallback: without a usable gfx950 device, calls fail with OXH_ERR_NODEVICE.
  *
  * The Rust-side `extern "C"` block that binds these is in INTEGRATION.md.

@@ -186,11 +186,16 @@ struct oxh_ctx {
     uint64_t* d_cnt[NSLOT] = {};
     int32_t* h_utf8[NSLOT] = {};  // is_utf8 of each item's first 4 KiB (util/fs.rs:652-668)
     int32_t* d_utf8[NSLOT] = {};
-    int32_t* utf8_out = nullptr;  // per call (calls on a context are serialised): where is_utf8 goes
-    // file-request coalescer (see hash_files_impl): requests queue here while a leader thread runs
+    // streaming file engine (see run_stream): file calls queue requests here; the engine thread runs
+    // them, and requests arriving while it runs join the live pipeline
     std::mutex qmu;
+    std::condition_variable qcv;  // a request was queued (or the engine must stop)
     std::vector<struct FileRequest*> queue;
-    bool leader = false;
+    bool stop = false;
+    std::thread engine;
+    uint64_t flush_bytes = 0;  // seal a partly filled slot at this many bytes when the next slot is free
+    std::vector<struct FileRequest*> rq[NSLOT];  // per staged item: its request and index in it
+    std::vector<uint64_t> loc[NSLOT];
     hipEvent_t ev_copied[NSLOT] = {}, ev_done[NSLOT] = {};
     oxh::Pool* pool = nullptr;   // readers / copiers (fill)
     oxh::Pool* wpool = nullptr;  // consumers of hashed bytes (fused publish), created on first use
@@ -199,6 +204,8 @@ struct oxh_ctx {
 };
 
 namespace {
+
+void engine_main(oxh_ctx* c);  // the streaming file engine's thread (below)
 
 // K1L over n device buffers: block sums chip-wide (one launch per buffer; each fills the chip),
 // then the serial chains of up to kChainJobs buffers in one launch, one wave each, so the chains of
@@ -260,7 +267,8 @@ static const bool g_steps = getenv("OXH_DEBUG_STEPS") != nullptr;
     } while (0)
 
 // One staged batch: items [0, cnt) already in h_stage[s] at h_desc offsets; launch and queue D2H.
-int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_only, bool short_items, bool text) {
+int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_only, bool short_items, bool text,
+                bool utf8 = false) {
     const uint64_t M = c->max_items;
     STEP("submit s=%d bytes=%llu cnt=%llu lane=%d short=%d", s, (unsigned long long)bytes, (unsigned long long)cnt,
          (int)any_short_only, (int)short_items);
@@ -279,7 +287,7 @@ int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_
     STEP("launched s=%d", s);
     HIP_TRY(hipMemcpyAsync(c->h_out[s], c->d_out[s], cnt * 16, hipMemcpyDeviceToHost, c->stream));
     if (text) HIP_TRY(hipMemcpyAsync(c->h_cnt[s], c->d_cnt[s], cnt * 16, hipMemcpyDeviceToHost, c->stream));
-    if (c->utf8_out) {  // is_utf8 sniff of the same staged bytes
+    if (utf8) {  // is_utf8 sniff of the same staged bytes
         hipLaunchKernelGGL(oxh::utf8_prefix_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, c->stream, c->d_stage[s],
                            c->d_desc[s], c->d_desc[s] + M, cnt, c->d_utf8[s]);
         HIP_TRY(hipGetLastError());
@@ -358,8 +366,6 @@ int drain_slot(oxh_ctx* c, int s, Pending& p, uint64_t* out, uint64_t* counts = 
             counts[2 * p.ids[j]] = c->h_cnt[s][2 * j];
             counts[2 * p.ids[j] + 1] = c->h_cnt[s][2 * j + 1];
         }
-    if (c->utf8_out)
-        for (size_t j = 0; j < p.ids.size(); ++j) c->utf8_out[p.ids[j]] = c->h_utf8[s][j];
     p.busy = false;
     if (sink) {
         // hand the slot to the consumer pool; the caller refills it only after join_consumer()
@@ -382,56 +388,48 @@ int drain_slot(oxh_ctx* c, int s, Pending& p, uint64_t* out, uint64_t* counts = 
     return OXH_OK;
 }
 
-// Hash one oversize host item (> a staging slot) through a temporary device buffer; with `cnt2`,
-// also its text counts (num_lines, num_chars).
+// Hash one oversize host item (> a staging slot) through a device buffer of its own (the staging
+// slots may belong to a live pipeline); with `cnt2`, also its text counts (num_lines, num_chars),
+// with `utf8_1` its is_utf8 sniff.
 int oversize_item(oxh_ctx* c, const uint8_t* src, uint64_t len, uint64_t* out2, uint64_t* cnt2 = nullptr,
                   int32_t* utf8_1 = nullptr) {
+    const uint64_t tail = align_up(len);
     uint8_t* d = nullptr;
-    if (hipMalloc(&d, len) != hipSuccess) return fail(OXH_ERR_NOMEM, "oversize hipMalloc failed");
+    if (hipMalloc(&d, tail + 256) != hipSuccess) return fail(OXH_ERR_NOMEM, "oversize hipMalloc failed");
+    struct Res {  // mirrored at d + tail: digest, text counts, a one-item descriptor, is_utf8
+        uint64_t out[2], cnt[2], off, len;
+        int32_t utf8, pad;
+    } h{};
+    h.len = len;
+    uint64_t* d_res = reinterpret_cast<uint64_t*>(d + tail);
     int rc = OXH_OK;
-    // stream it through the pinned slot 0 in stage-sized pieces
-    for (uint64_t off = 0; off < len && rc == OXH_OK; off += c->stage_bytes) {
-        const uint64_t piece = std::min(c->stage_bytes, len - off);
-        memcpy(c->h_stage[0], src + off, piece);
-        if (hipMemcpy(d + off, c->h_stage[0], piece, hipMemcpyHostToDevice) != hipSuccess) rc = fail(OXH_ERR_HIP, "oversize H2D failed");
-    }
-    if (rc == OXH_OK) rc = large_device(c, d, len, c->d_out[0], c->stream);
+    auto ok = [&](hipError_t e, const char* what) {
+        if (rc == OXH_OK && e != hipSuccess) rc = fail(OXH_ERR_HIP, what);
+        return rc == OXH_OK;
+    };
+    ok(hipMemcpyAsync(d, src, len, hipMemcpyHostToDevice, c->stream), "oversize H2D failed");
+    ok(hipMemcpyAsync(d_res, &h, sizeof h, hipMemcpyHostToDevice, c->stream), "oversize descriptor H2D failed");
+    if (rc == OXH_OK) rc = large_device(c, d, len, d_res, c->stream);
     if (rc == OXH_OK && cnt2) {
-        if (hipMemsetAsync(c->d_cnt[0], 0, 16, c->stream) != hipSuccess) rc = fail(OXH_ERR_HIP, "memset counts");
-        if (rc == OXH_OK) {
-            hipLaunchKernelGGL(oxh::text_count_kernel, dim3(2048), dim3(256), 0, c->stream, d, len,
-                               (unsigned long long*)c->d_cnt[0]);
-            if (hipGetLastError() != hipSuccess) rc = fail(OXH_ERR_HIP, "text_count_kernel launch");
-        }
-        if (rc == OXH_OK && hipMemcpyAsync(c->h_cnt[0], c->d_cnt[0], 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
-            rc = fail(OXH_ERR_HIP, "oversize counts D2H failed");
+        hipLaunchKernelGGL(oxh::text_count_kernel, dim3(2048), dim3(256), 0, c->stream, d, len,
+                           (unsigned long long*)(d_res + 2));
+        ok(hipGetLastError(), "text_count_kernel launch");
     }
     if (rc == OXH_OK && utf8_1) {
-        // one item: offset 0, length len, through the slot-0 descriptor arrays
-        c->h_desc[0][0] = 0;
-        c->h_desc[0][c->max_items] = len;
-        if (hipMemcpyAsync(c->d_desc[0], c->h_desc[0], 8, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
-            hipMemcpyAsync(c->d_desc[0] + c->max_items, c->h_desc[0] + c->max_items, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess)
-            rc = fail(OXH_ERR_HIP, "oversize utf8 descriptors");
-        if (rc == OXH_OK) {
-            hipLaunchKernelGGL(oxh::utf8_prefix_kernel, dim3(1), dim3(64), 0, c->stream, d, c->d_desc[0], c->d_desc[0] + c->max_items,
-                               (uint64_t)1, c->d_utf8[0]);
-            if (hipGetLastError() != hipSuccess) rc = fail(OXH_ERR_HIP, "utf8_prefix_kernel launch");
-        }
-        if (rc == OXH_OK && hipMemcpyAsync(c->h_utf8[0], c->d_utf8[0], 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
-            rc = fail(OXH_ERR_HIP, "oversize utf8 D2H failed");
+        hipLaunchKernelGGL(oxh::utf8_prefix_kernel, dim3(1), dim3(64), 0, c->stream, d, d_res + 4, d_res + 5, (uint64_t)1,
+                           (int32_t*)(d_res + 6));
+        ok(hipGetLastError(), "utf8_prefix_kernel launch");
     }
-    if (rc == OXH_OK && hipMemcpyAsync(c->h_out[0], c->d_out[0], 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
-        rc = fail(OXH_ERR_HIP, "oversize D2H failed");
-    if (rc == OXH_OK && hipStreamSynchronize(c->stream) != hipSuccess) rc = fail(OXH_ERR_HIP, "oversize sync failed");
+    ok(hipMemcpyAsync(&h, d_res, sizeof h, hipMemcpyDeviceToHost, c->stream), "oversize D2H failed");
+    ok(hipStreamSynchronize(c->stream), "oversize sync failed");
     if (rc == OXH_OK) {
-        out2[0] = c->h_out[0][0];
-        out2[1] = c->h_out[0][1];
+        out2[0] = h.out[0];
+        out2[1] = h.out[1];
         if (cnt2) {
-            cnt2[0] = 1 + c->h_cnt[0][0];
-            cnt2[1] = len - c->h_cnt[0][1];
+            cnt2[0] = 1 + h.cnt[0];
+            cnt2[1] = len - h.cnt[1];
         }
-        if (utf8_1) *utf8_1 = c->h_utf8[0][0];
+        if (utf8_1) *utf8_1 = h.utf8;
     }
     (void)hipFree(d);
     return rc;
@@ -481,14 +479,29 @@ int oxh_ctx_create(int device, uint64_t staging_bytes, oxh_ctx** out) {
         if (hipEventCreateWithFlags(&c->ev_copied[s], hipEventDisableTiming) != hipSuccess) return cleanup(OXH_ERR_HIP, "event");
         if (hipEventCreateWithFlags(&c->ev_done[s], hipEventDisableTiming) != hipSuccess) return cleanup(OXH_ERR_HIP, "event");
     }
+    for (int s = 0; s < NSLOT; ++s) {
+        c->rq[s].resize(c->max_items);
+        c->loc[s].resize(c->max_items);
+    }
+    const char* fl = getenv("OXH_FLUSH_MIB");
+    c->flush_bytes = std::min<uint64_t>(c->stage_bytes, (fl ? (uint64_t)atoll(fl) : 16ull) << 20);
     c->pool = new oxh::Pool(default_threads());
     c->rpool = new oxh::Pool(default_threads());
+    c->engine = std::thread(engine_main, c);
     *out = c;
     return OXH_OK;
 }
 
 int oxh_ctx_destroy(oxh_ctx* c) {
     if (!c) return OXH_OK;
+    if (c->engine.joinable()) {  // finishes what is queued, then exits
+        {
+            std::lock_guard<std::mutex> g(c->qmu);
+            c->stop = true;
+        }
+        c->qcv.notify_all();
+        c->engine.join();
+    }
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
@@ -701,16 +714,25 @@ int oxh_hash_streams(oxh_ctx* c, const uint8_t* streams, const uint64_t* offsets
     }, out, nullptr, true);
 }
 
-// ---------------------------------------------------------------- streaming file pipeline
+// ---------------------------------------------------------------- streaming file engine
 // The reference reads, stats and hashes each file inside one per-file closure (add.rs:462-539 ->
-// hasher.rs:126-148). Here T reader threads run the whole list without barriers or locks: each
-// claims the next files, opens + fstats one (one path walk), reserves its bytes in the slot being
-// filled with ONE atomic add (item count in the high bits, 256-B-rounded bytes in the low bits),
+// hasher.rs:126-148), and liboxen calls it for 64-file batches from up to 2 x ncpu tokio tasks at
+// once (add.rs:41, 422-425): a few MB per call, far too small for one launch each. Here every file
+// call on a context becomes a REQUEST on the context's queue, and one engine thread per context
+// runs a continuous pipeline over all queued requests: requests that arrive while it runs join the
+// live pipeline (their files go into the slot being filled), and each request completes, and its
+// caller returns, as soon as its own last file is drained.
+//
+// Inside the pipeline T reader threads run without barriers or per-file locks: each claims the next
+// 8 files of the current request, opens + fstats one (one path walk), reserves its bytes in the slot
+// being filled with ONE CAS (item count in the high bits, 256-B-rounded bytes in the low bits),
 // preads straight into the pinned slot and closes it. Reservations are monotone, so the first one
 // that does not fit seals the slot: every earlier one fits and every later one fails. The reader
-// that seals opens the next slot of the ring once the calling thread has freed it; the calling
-// thread submits a sealed slot when all its writers are done (H2D on the copy stream, K1/K1T, D2H)
-// and drains the previous slot while the readers fill the next one.
+// that seals opens the next slot of the ring once the engine has freed it. The engine also seals a
+// partly filled slot when it holds OXH_FLUSH_MIB (default 16 MiB) and the next slot is free, or
+// when every reader is idle, so small requests never wait for a full 256 MiB slot. It submits a
+// sealed slot when all its writers are done (H2D on the copy stream, K1/K1T (+ is_utf8), D2H) and
+// drains submitted slots, oldest first, as their events complete.
 namespace {
 
 // One 64-bit word per slot: bytes (31 bits) | items (19) | sealed (1) | generation (13). Every
@@ -729,22 +751,57 @@ struct SlotFill {
     std::atomic<uint64_t> done{0};     // writers finished
 };
 
+struct SlotRun {  // a submitted slot
+    uint64_t cnt = 0;
+    bool text = false, utf8 = false;
+};
+
+}  // namespace
+
+// One file call (oxh_hash_files / _text / _text_utf8 / oxh_add_files / fsck). Lives on its caller's
+// stack; the engine writes its outputs in place and wakes the caller when the last item is done.
+struct FileRequest {
+    const char* const* paths = nullptr;
+    uint64_t n = 0;
+    uint64_t* out = nullptr;
+    uint64_t* sizes = nullptr;
+    int32_t* status = nullptr;
+    uint64_t* counts = nullptr;
+    int32_t* utf8 = nullptr;
+    const ItemSink* sink = nullptr;
+    std::vector<uint64_t> lens;
+    std::vector<int32_t> st;
+    uint64_t next = 0;                   // claim cursor (under ctx->qmu)
+    size_t idx = 0;                      // index in the run's request table
+    std::atomic<uint64_t> remaining{0};  // items not yet accounted for
+    int rc = OXH_OK;
+    std::string msg;
+    bool done = false;  // under mu
+    std::mutex mu;
+    std::condition_variable cv;
+};
+
+namespace {
+
 struct FileStream {
     oxh_ctx* c;
-    const char* const* paths;
-    uint64_t n;
     SlotFill slot[NSLOT];
     std::atomic<int> cur{0};
     std::atomic<int> readers_left{0};
+    std::atomic<int> idle{0};            // readers waiting for new requests (changed under c->qmu)
+    int nreaders = 0;
     std::atomic<bool> abort{false};
-    std::atomic<uint64_t> next{0};
-    std::vector<uint64_t> lens;
-    std::vector<int32_t> st;
-    std::vector<uint64_t> ids[NSLOT];
+    bool closing = false;                // under c->qmu
+    std::vector<FileRequest*> reqs;      // joined requests; nullptr once complete (under c->qmu)
+    size_t cur_req = 0;                  // under c->qmu
+    std::atomic<bool> want_text{false}, want_utf8{false};
+    std::atomic<int> claimed_out{0};     // requests with every file claimed, not yet complete
     std::mutex omu;
-    std::vector<uint64_t> oversize;
-    std::mutex cmu;  // the calling thread sleeps on ccv until a slot is complete
+    std::vector<std::pair<FileRequest*, uint64_t>> oversize;
+    std::atomic<uint64_t> n_oversize{0};
+    std::mutex cmu;  // the engine sleeps on ccv between events
     std::condition_variable ccv;
+    uint64_t files = 0, slots = 0;
     void wake() {
         std::lock_guard<std::mutex> g(cmu);
         ccv.notify_all();
@@ -753,7 +810,70 @@ struct FileStream {
 
 inline void pause_us(int us) { std::this_thread::sleep_for(std::chrono::microseconds(us)); }
 
-// Open slot t for filling (generation + 1, empty, unsealed) once the calling thread has freed it.
+// Request r is complete: zero the outputs of failed items (add.rs:533-544 skips them), report sizes
+// and statuses, retire it from the run and wake its caller.
+void finish_request(FileStream& fs, FileRequest* r) {
+    for (uint64_t i = 0; i < r->n; ++i) {
+        if (r->st[i] != OXH_OK) {
+            r->out[2 * i] = r->out[2 * i + 1] = 0;
+            if (r->counts) r->counts[2 * i] = r->counts[2 * i + 1] = 0;
+            if (r->utf8) r->utf8[i] = 0;  // read_first_n_bytes failed -> is_utf8 false (fs.rs:655-658)
+        }
+        if (r->sizes) r->sizes[i] = r->lens[i];
+        if (r->status) r->status[i] = r->st[i];
+    }
+    {
+        std::lock_guard<std::mutex> g(fs.c->qmu);
+        fs.reqs[r->idx] = nullptr;
+    }
+    fs.claimed_out.fetch_sub(1);
+    std::lock_guard<std::mutex> g(r->mu);  // notify under the lock: the caller frees r once it sees done
+    r->done = true;
+    r->cv.notify_all();
+}
+
+// k more items of r are fully written; the thread that accounts the last one completes r.
+inline void account(FileStream& fs, FileRequest* r, uint64_t k) {
+    if (k && r->remaining.fetch_sub(k, std::memory_order_acq_rel) == k) finish_request(fs, r);
+}
+
+// Next files to read: [i0, i1) of request *r. Moves queued requests into the run; an idle reader
+// sleeps until a request arrives or the engine closes the run. False = stop.
+bool claim(FileStream& fs, FileRequest*& r, uint64_t& i0, uint64_t& i1) {
+    constexpr uint64_t kClaim = 8;
+    oxh_ctx* c = fs.c;
+    std::unique_lock<std::mutex> lk(c->qmu);
+    for (;;) {
+        if (fs.abort.load(std::memory_order_relaxed) || fs.closing) return false;
+        for (; fs.cur_req < fs.reqs.size(); ++fs.cur_req) {
+            FileRequest* q = fs.reqs[fs.cur_req];
+            if (q && q->next < q->n) {
+                r = q;
+                i0 = q->next;
+                i1 = std::min(q->n, i0 + kClaim);
+                q->next = i1;
+                if (i1 == q->n) fs.claimed_out.fetch_add(1);  // its caller may be waiting on a partial slot
+                return true;
+            }
+        }
+        if (!c->queue.empty()) {
+            for (FileRequest* q : c->queue) {
+                q->idx = fs.reqs.size();
+                fs.reqs.push_back(q);
+                fs.files += q->n;
+                if (q->counts) fs.want_text.store(true);
+                if (q->utf8) fs.want_utf8.store(true);
+            }
+            c->queue.clear();
+            continue;
+        }
+        if (fs.idle.fetch_add(1) + 1 == fs.nreaders) fs.wake();  // the engine may flush or close now
+        c->qcv.wait(lk, [&] { return fs.abort.load() || fs.closing || !c->queue.empty(); });
+        fs.idle.fetch_sub(1);
+    }
+}
+
+// Open slot t for filling (generation + 1, empty, unsealed) once the engine has freed it.
 bool open_slot(FileStream& fs, int t) {
     SlotFill& nx = fs.slot[t];
     while (nx.state.load(std::memory_order_acquire) != 0) {
@@ -768,8 +888,8 @@ bool open_slot(FileStream& fs, int t) {
     return true;
 }
 
-// Reserve L bytes for item i; returns the slot (and offset), or -1 on abort.
-int reserve(FileStream& fs, uint64_t i, uint64_t L, uint64_t& off) {
+// Reserve L bytes for item i of r; returns the slot (and offset), or -1 on abort.
+int reserve(FileStream& fs, FileRequest* r, uint64_t i, uint64_t L, uint64_t& off) {
     oxh_ctx* c = fs.c;
     const uint64_t M = c->max_items, cap = c->stage_bytes;
     const uint64_t need = align_up(L);
@@ -788,7 +908,8 @@ int reserve(FileStream& fs, uint64_t i, uint64_t L, uint64_t& off) {
             off = o;
             c->h_desc[s][j] = o;
             c->h_desc[s][M + j] = L;
-            fs.ids[s][j] = i;
+            c->rq[s][j] = r;
+            c->loc[s][j] = i;
             return s;
         }
         // does not fit: seal it (one reader wins) and open the next slot of the ring
@@ -800,34 +921,42 @@ int reserve(FileStream& fs, uint64_t i, uint64_t L, uint64_t& off) {
 
 void reader_loop(FileStream& fs) {
     oxh_ctx* c = fs.c;
-    constexpr uint64_t kClaim = 8;
-    for (;;) {
-        const uint64_t i0 = fs.next.fetch_add(kClaim);
-        if (i0 >= fs.n || fs.abort.load(std::memory_order_relaxed)) break;
-        for (uint64_t i = i0; i < std::min(fs.n, i0 + kClaim); ++i) {
+    FileRequest* r = nullptr;
+    uint64_t i0 = 0, i1 = 0;
+    bool stop = false;
+    while (!stop && claim(fs, r, i0, i1)) {
+        uint64_t failed = 0;  // items of this claim that never reach a slot
+        for (uint64_t i = i0; i < i1; ++i) {
             struct stat sb;
-            const int fd = fs.paths[i] ? open(fs.paths[i], O_RDONLY | O_CLOEXEC | O_NONBLOCK) : -1;
+            const int fd = r->paths[i] ? open(r->paths[i], O_RDONLY | O_CLOEXEC | O_NONBLOCK) : -1;
             if (fd < 0) {
-                fs.st[i] = OXH_ERR_IO;
+                r->st[i] = OXH_ERR_IO;
+                ++failed;
                 continue;
             }
             if (fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode)) {
                 close(fd);
-                fs.st[i] = OXH_ERR_IO;
+                r->st[i] = OXH_ERR_IO;
+                ++failed;
                 continue;
             }
             const uint64_t L = (uint64_t)sb.st_size;
-            fs.lens[i] = L;
-            if (L > c->stage_bytes) {  // read later through the oversize path
+            r->lens[i] = L;
+            if (L > c->stage_bytes) {  // the engine reads it through the oversize path
                 close(fd);
-                std::lock_guard<std::mutex> g(fs.omu);
-                fs.oversize.push_back(i);
+                {
+                    std::lock_guard<std::mutex> g(fs.omu);
+                    fs.oversize.push_back({r, i});
+                }
+                fs.n_oversize.fetch_add(1);
+                fs.wake();
                 continue;
             }
             uint64_t off = 0;
-            const int s = reserve(fs, i, L, off);
+            const int s = reserve(fs, r, i, L, off);
             if (s < 0) {
                 close(fd);
+                stop = true;  // aborted: the engine fails every open request
                 break;
             }
             uint8_t* dst = c->h_stage[s] + off;
@@ -835,216 +964,251 @@ void reader_loop(FileStream& fs) {
             while (got < L) {
                 const ssize_t k = pread(fd, dst + got, L - got, (off_t)got);
                 if (k <= 0) {
-                    fs.st[i] = OXH_ERR_IO;
+                    r->st[i] = OXH_ERR_IO;
                     break;
                 }
                 got += (uint64_t)k;
             }
             close(fd);
-            // the last writer of a sealed slot wakes the calling thread
+            // the last writer of a sealed slot wakes the engine
             const uint64_t d = fs.slot[s].done.fetch_add(1, std::memory_order_acq_rel) + 1;
             const uint64_t w = fs.slot[s].word.load(std::memory_order_acquire);
             if ((w & kSealedBit) && d == w_items(w)) fs.wake();
         }
+        if (!stop) account(fs, r, failed);
     }
     if (fs.readers_left.fetch_sub(1, std::memory_order_acq_rel) == 1) fs.wake();
 }
 
-}  // namespace
+// Scatter a completed slot's digests (+ counts, is_utf8) into the requests, run the sinks over the
+// staged bytes (fused publish), then account the items.
+void drain_files(FileStream& fs, int s, const SlotRun& p) {
+    oxh_ctx* c = fs.c;
+    const uint64_t M = c->max_items, cnt = p.cnt;
+    FileRequest* const* rq = c->rq[s].data();
+    const uint64_t* loc = c->loc[s].data();
+    bool any_sink = false;
+    for (uint64_t j = 0; j < cnt; ++j) {
+        FileRequest* r = rq[j];
+        const uint64_t i = loc[j];
+        r->out[2 * i] = c->h_out[s][2 * j];
+        r->out[2 * i + 1] = c->h_out[s][2 * j + 1];
+        if (r->counts && p.text) {
+            r->counts[2 * i] = c->h_cnt[s][2 * j];
+            r->counts[2 * i + 1] = c->h_cnt[s][2 * j + 1];
+        }
+        if (r->utf8 && p.utf8) r->utf8[i] = c->h_utf8[s][j];
+        any_sink |= r->sink != nullptr;
+    }
+    if (any_sink) {
+        if (!c->wpool) c->wpool = new oxh::Pool(c->pool->size());
+        const int ntasks = (int)std::min<uint64_t>(cnt, (uint64_t)c->wpool->size() * 4);
+        c->wpool->parallel_for(ntasks, [&](int t) {
+            for (uint64_t j = (uint64_t)t; j < cnt; j += (uint64_t)ntasks) {
+                FileRequest* r = rq[j];
+                const uint64_t i = loc[j];
+                if (!r->sink || r->st[i] != OXH_OK) continue;
+                (*r->sink)(i, c->h_stage[s] + c->h_desc[s][j], c->h_desc[s][M + j], c->h_out[s][2 * j], c->h_out[s][2 * j + 1]);
+            }
+        });
+    }
+    for (uint64_t j = 0; j < cnt;) {  // one atomic per run of items of the same request
+        uint64_t k = j + 1;
+        while (k < cnt && rq[k] == rq[j]) ++k;
+        account(fs, rq[j], k - j);
+        j = k;
+    }
+}
 
-static int stream_files(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* lens_out,
-                        int32_t* st_out, uint64_t* counts, const ItemSink* sink) {
+// One file read through the oversize path (files larger than a staging slot, K1L).
+int oversize_file(FileStream& fs, FileRequest* r, uint64_t i) {
+    oxh_ctx* c = fs.c;
+    const uint64_t L = r->lens[i];
+    std::vector<uint8_t> tmp(L);
+    const int fd = open(r->paths[i], O_RDONLY | O_CLOEXEC | O_NONBLOCK);
+    uint64_t got = 0;
+    if (fd >= 0) {
+        while (got < L) {
+            const ssize_t k = pread(fd, tmp.data() + got, L - got, (off_t)got);
+            if (k <= 0) break;
+            got += (uint64_t)k;
+        }
+        close(fd);
+    }
+    if (got != L) {
+        r->st[i] = OXH_ERR_IO;
+    } else {
+        int32_t u8 = 0;
+        const int rc = oversize_item(c, tmp.data(), L, r->out + 2 * i, r->counts ? r->counts + 2 * i : nullptr,
+                                     r->utf8 ? &u8 : nullptr);
+        if (rc) return rc;
+        if (r->utf8) r->utf8[i] = u8;
+        if (r->sink) (*r->sink)(i, tmp.data(), L, r->out[2 * i], r->out[2 * i + 1]);
+    }
+    account(fs, r, 1);
+    return OXH_OK;
+}
+
+// One run of the engine: from the first queued request until the readers are idle, the queue is
+// empty and every submitted slot is drained.
+void run_stream(oxh_ctx* c) {
     FileStream fs;
     fs.c = c;
-    fs.paths = paths;
-    fs.n = n;
-    fs.lens.assign(n, 0);
-    fs.st.assign(n, OXH_OK);
-    for (int s = 0; s < NSLOT; ++s) fs.ids[s].resize(c->max_items);
     fs.slot[0].state.store(1);
     fs.slot[0].word.store(1ull << kGenShift);
+    fs.nreaders = c->rpool->size();
+    fs.readers_left.store(fs.nreaders);
     Trace tr;
     const double t_start = Trace::now();
-    const int nreaders = (int)std::max<uint64_t>(1, std::min<uint64_t>(n, (uint64_t)c->rpool->size()));
-    fs.readers_left.store(nreaders);
-    // the readers run on the context's persistent reader pool (no thread start-up per call)
-    oxh::Pool::Group readers;
+    oxh::Pool::Group readers;  // the readers run on the context's persistent reader pool
     const std::function<void(int)> reader_fn = [&fs](int) { reader_loop(fs); };
-    c->rpool->start(nreaders, reader_fn, readers);
-    Pending pend[NSLOT];
-    int rc = OXH_OK;
+    c->rpool->start(fs.nreaders, reader_fn, readers);
+    SlotRun pend[NSLOT];
     const uint64_t M = c->max_items;
-    int s = 0;  // next slot to submit (slots are filled and submitted in ring order)
-    for (;;) {
-        // wait until slot s is sealed (or the readers are done) and its writers have finished
-        SlotFill& sl = fs.slot[s];
-        const double tw = Trace::now();
-        uint64_t cnt = 0;
-        bool last = false;  // set when this is the final, partial slot
-        for (;;) {
-            const bool finished = fs.readers_left.load(std::memory_order_acquire) == 0;
-            uint64_t w = sl.word.load(std::memory_order_acquire);
-            if (finished && sl.state.load(std::memory_order_acquire) == 1 && !(w & kSealedBit)) {
-                // the readers are done: seal the last, partial slot ourselves
-                sl.word.fetch_or(kSealedBit, std::memory_order_acq_rel);
-                w |= kSealedBit;
-                last = true;
+    int rc = hipSetDevice(c->device) == hipSuccess ? OXH_OK : fail(OXH_ERR_HIP, "hipSetDevice failed");
+    int s = 0, nbusy = 0;  // s: the slot being filled; the nbusy slots before it are submitted
+    static const double wait_limit = getenv("OXH_WAIT_LIMIT_S") ? atof(getenv("OXH_WAIT_LIMIT_S")) : 60.0;
+    double last_progress = Trace::now();
+    while (rc == OXH_OK) {
+        // 1. drain submitted slots whose digests are back, oldest first, and free them
+        bool progressed = false;
+        while (nbusy) {
+            const int t = (s + NSLOT - nbusy) % NSLOT;
+            const hipError_t q = hipEventQuery(c->ev_done[t]);
+            if (q == hipErrorNotReady) break;
+            if (q != hipSuccess) {
+                rc = fail(OXH_ERR_HIP, std::string("slot event: ") + hipGetErrorString(q));
+                break;
             }
-            if ((w & kSealedBit) || (finished && sl.state.load(std::memory_order_acquire) != 1)) {
-                cnt = (w & kSealedBit) && sl.state.load(std::memory_order_acquire) == 1 ? w_items(w) : 0;
-                if (cnt == 0 && finished) break;
-                if (cnt && sl.done.load(std::memory_order_acquire) == cnt) break;
-            }
-            // sleep until a reader reports a completed slot (bounded: a missed wake-up costs 1 ms)
-            std::unique_lock<std::mutex> lk(fs.cmu);
-            fs.ccv.wait_for(lk, std::chrono::milliseconds(1), [&] {
-                const uint64_t x = sl.word.load(std::memory_order_acquire);
-                return fs.readers_left.load(std::memory_order_acquire) == 0 ||
-                       ((x & kSealedBit) && sl.done.load(std::memory_order_acquire) == w_items(x));
-            });
+            drain_files(fs, t, pend[t]);
+            fs.slot[t].state.store(0, std::memory_order_release);
+            --nbusy;
+            progressed = true;
         }
-        tr.fill += Trace::now() - tw;
-        if (cnt == 0) break;  // only possible for the last, empty slot
-        uint64_t bytes = 0;
-        for (uint64_t j = 0; j < cnt; ++j) bytes = std::max(bytes, c->h_desc[s][j] + c->h_desc[s][M + j]);
-        const double t0 = Trace::now();
-        sl.state.store(2, std::memory_order_release);
-        rc = submit_slot(c, s, bytes, cnt, false, bytes / cnt <= kShortItemBytes, counts != nullptr);
         if (rc) break;
-        pend[s].busy = true;
-        pend[s].ids.assign(fs.ids[s].begin(), fs.ids[s].begin() + (ptrdiff_t)cnt);
-        tr.submit += Trace::now() - t0;
-        tr.batches++;
-        // drain the slot submitted in the previous round while the readers fill the next one: it is
-        // the slot they move into after that, so it is free well before they get there
-        const int t = (s + NSLOT - 1) % NSLOT;
-        const double t1 = Trace::now();
-        rc = drain_slot(c, t, pend[t], out, counts, sink, fs.st.data());
-        if (rc) break;
-        join_consumer(pend[t]);
-        tr.drain += Trace::now() - t1;
-        if (fs.slot[t].state.load(std::memory_order_acquire) == 2) fs.slot[t].state.store(0, std::memory_order_release);
-        if (last) break;
-        s = (s + 1) % NSLOT;
-    }
-    if (rc) fs.abort.store(true);
-    readers.wait();
-    const double t3 = Trace::now();
-    for (int k = 0; k < NSLOT && rc == OXH_OK; ++k) rc = drain_slot(c, k, pend[k], out, counts, sink, fs.st.data());
-    for (int k = 0; k < NSLOT; ++k) join_consumer(pend[k]);
-    tr.drain += Trace::now() - t3;
-    if (rc) return rc;
-    // files larger than a staging slot, one at a time through the oversize path (K1L)
-    std::sort(fs.oversize.begin(), fs.oversize.end());
-    for (uint64_t i : fs.oversize) {
-        std::vector<uint8_t> tmp(fs.lens[i]);
-        const int fd = open(paths[i], O_RDONLY | O_CLOEXEC | O_NONBLOCK);
-        uint64_t got = 0;
-        if (fd >= 0) {
-            while (got < fs.lens[i]) {
-                const ssize_t k = pread(fd, tmp.data() + got, fs.lens[i] - got, (off_t)got);
-                if (k <= 0) break;
-                got += (uint64_t)k;
+        // 2. files larger than a slot, one at a time
+        if (fs.n_oversize.load(std::memory_order_acquire)) {
+            std::pair<FileRequest*, uint64_t> it;
+            {
+                std::lock_guard<std::mutex> g(fs.omu);
+                it = fs.oversize.back();
+                fs.oversize.pop_back();
             }
-            close(fd);
-        }
-        if (got != fs.lens[i]) {
-            fs.st[i] = OXH_ERR_IO;
+            fs.n_oversize.fetch_sub(1);
+            rc = oversize_file(fs, it.first, it.second);
             continue;
         }
-        rc = oversize_item(c, tmp.data(), fs.lens[i], out + 2 * i, counts ? counts + 2 * i : nullptr,
-                           c->utf8_out ? c->utf8_out + i : nullptr);
-        if (rc) return rc;
-        if (sink) (*sink)(i, tmp.data(), fs.lens[i], out[2 * i], out[2 * i + 1]);
+        // 3. the slot being filled: seal it early (flush) when it holds enough bytes or every reader
+        //    is idle and the next slot is free; submit it once sealed and its writers are done
+        SlotFill& sl = fs.slot[s];
+        // state before word: a slot seen open (state 1) shows its current generation's word
+        const int sst = sl.state.load(std::memory_order_acquire);
+        uint64_t w = sl.word.load(std::memory_order_acquire);
+        const bool all_idle = fs.idle.load(std::memory_order_acquire) == fs.nreaders;
+        // (early flushes only help while some caller is waiting on a partial slot: a request whose
+        // files are all claimed; a lone whole-list call keeps full slots until its last files)
+        if (sst == 1 && !(w & kSealedBit) && w_items(w) > 0 &&
+            (all_idle || (w_bytes(w) >= c->flush_bytes && fs.claimed_out.load(std::memory_order_relaxed) > 0)) &&
+            fs.slot[(s + 1) % NSLOT].state.load(std::memory_order_acquire) == 0) {
+            if (!sl.word.compare_exchange_strong(w, w | kSealedBit, std::memory_order_acq_rel)) continue;
+            w |= kSealedBit;
+            open_slot(fs, (s + 1) % NSLOT);
+        }
+        if (sst == 1 && (w & kSealedBit) && sl.done.load(std::memory_order_acquire) == w_items(w) &&
+            sl.word.load(std::memory_order_acquire) == w) {
+            const uint64_t cnt = w_items(w);
+            uint64_t bytes = 0;
+            for (uint64_t j = 0; j < cnt; ++j) bytes = std::max(bytes, c->h_desc[s][j] + c->h_desc[s][M + j]);
+            const double t0 = Trace::now();
+            pend[s].cnt = cnt;
+            pend[s].text = fs.want_text.load();
+            pend[s].utf8 = fs.want_utf8.load();
+            sl.state.store(2, std::memory_order_release);
+            rc = submit_slot(c, s, bytes, cnt, false, bytes / cnt <= kShortItemBytes, pend[s].text, pend[s].utf8);
+            if (nbusy == 0) last_progress = Trace::now();
+            tr.submit += Trace::now() - t0;
+            tr.batches++;
+            ++nbusy;
+            s = (s + 1) % NSLOT;
+            continue;
+        }
+        // 4. nothing left: close the run (requests arriving later start the next one)
+        if (all_idle && sst == 1 && !(w & kSealedBit) && w_items(w) == 0 && nbusy == 0 && fs.n_oversize.load() == 0) {
+            std::lock_guard<std::mutex> g(c->qmu);
+            if (c->queue.empty() && fs.idle.load() == fs.nreaders) {
+                fs.closing = true;
+                c->qcv.notify_all();
+                break;
+            }
+            continue;
+        }
+        if (progressed) {
+            last_progress = Trace::now();
+            continue;
+        }
+        if (nbusy && Trace::now() - last_progress > wait_limit) {  // report a stalled GPU instead of hanging
+            fprintf(stderr, "[oxh] slot %d stalled: copy_stream=%s stream=%s\n", (s + NSLOT - nbusy) % NSLOT,
+                    hipGetErrorName(hipStreamQuery(c->copy_stream)), hipGetErrorName(hipStreamQuery(c->stream)));
+            rc = fail(OXH_ERR_HIP, "timed out waiting for a staged batch (see stderr)");
+            break;
+        }
+        // 5. sleep until a reader reports an event; poll the GPU while slots are in flight
+        std::unique_lock<std::mutex> lk(fs.cmu);
+        fs.ccv.wait_for(lk, std::chrono::microseconds(nbusy ? 20 : 100));
+    }
+    if (rc) {
+        const std::string msg = g_err;
+        {
+            std::lock_guard<std::mutex> g(c->qmu);
+            fs.abort.store(true);
+            c->qcv.notify_all();
+        }
+        readers.wait();
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamSynchronize(c->copy_stream);
+        std::vector<FileRequest*> open;
+        {
+            std::lock_guard<std::mutex> g(c->qmu);
+            for (FileRequest*& r : fs.reqs)
+                if (r) open.push_back(r), r = nullptr;
+        }
+        for (FileRequest* r : open) {
+            std::lock_guard<std::mutex> g(r->mu);
+            r->rc = rc;
+            r->msg = msg;
+            r->done = true;
+            r->cv.notify_all();
+        }
+    } else {
+        readers.wait();
     }
     if (tr.on)
-        fprintf(stderr, "[oxh] files=%llu batches=%d total=%.3fs coord-wait-fill=%.3fs drain-wait=%.3fs submit=%.3fs readers=%d\n",
-                (unsigned long long)n, tr.batches, Trace::now() - t_start, tr.fill, tr.drain, tr.submit, nreaders);
-    for (uint64_t i = 0; i < n; ++i) {
-        if (fs.st[i] != OXH_OK) {
-            out[2 * i] = out[2 * i + 1] = 0;
-            if (counts) counts[2 * i] = counts[2 * i + 1] = 0;
-            if (c->utf8_out) c->utf8_out[i] = 0;  // read_first_n_bytes failed -> is_utf8 false (fs.rs:655-658)
+        fprintf(stderr, "[oxh] run: requests=%zu files=%llu slots=%d total=%.3fs submit=%.3fs readers=%d rc=%d\n",
+                fs.reqs.size(), (unsigned long long)fs.files, tr.batches, Trace::now() - t_start, tr.submit,
+                fs.nreaders, rc);
+}
+
+// The context's engine thread: one run per burst of requests.
+void engine_main(oxh_ctx* c) {
+    std::unique_lock<std::mutex> lk(c->qmu);
+    for (;;) {
+        c->qcv.wait(lk, [&] { return c->stop || !c->queue.empty(); });
+        if (c->queue.empty()) return;  // stopping, nothing left
+        lk.unlock();
+        {
+            std::lock_guard<std::mutex> g(c->mu);  // the staging slots are the run's
+            run_stream(c);
         }
-        if (lens_out) lens_out[i] = fs.lens[i];
-        if (st_out) st_out[i] = fs.st[i];
+        lk.lock();
     }
-    return OXH_OK;
 }
 
-// ---------------------------------------------------------------- request coalescer
-// liboxen hashes 64-file batches from up to 2 x ncpu tokio tasks at once (add.rs:41, 422-425): a few
-// MB per call, far too small for one launch each. Concurrent file requests on a context therefore
-// coalesce ("group commit"): a caller that finds no leader becomes the leader and runs the streaming
-// pipeline over every request queued at that moment as ONE item list; callers arriving meanwhile
-// queue and sleep; when a run ends, the leader completes its batch and hands leadership to the
-// oldest queued caller. Outputs are scattered back per request; each request keeps its own sink
-// (fused add), text counts and is_utf8 destinations.
-struct FileRequest {
-    const char* const* paths;
-    uint64_t n;
-    uint64_t* out;
-    uint64_t* sizes;
-    int32_t* status;
-    uint64_t* counts;
-    int32_t* utf8;
-    const ItemSink* sink;
-    int rc = OXH_OK;
-    std::string msg;
-    bool done = false, lead = false;
-    std::condition_variable cv;
-};
-
-static int run_requests(oxh_ctx* c, const std::vector<FileRequest*>& batch) {
-    std::lock_guard<std::mutex> g(c->mu);
-    struct Utf8Out {  // the context's per-run is_utf8 destination, cleared before the lock is released
-        oxh_ctx* c;
-        ~Utf8Out() { c->utf8_out = nullptr; }
-    } u8{c};
-    HIP_TRY(hipSetDevice(c->device));
-    if (batch.size() == 1) {  // the common, uncontended case: no copies
-        FileRequest* r = batch[0];
-        c->utf8_out = r->utf8;
-        return r->n ? stream_files(c, r->paths, r->n, r->out, r->sizes, r->status, r->counts, r->sink) : OXH_OK;
-    }
-    std::vector<uint64_t> base(batch.size() + 1, 0);
-    bool want_counts = false, want_utf8 = false, want_sink = false;
-    for (size_t k = 0; k < batch.size(); ++k) {
-        base[k + 1] = base[k] + batch[k]->n;
-        want_counts |= batch[k]->counts != nullptr;
-        want_utf8 |= batch[k]->utf8 != nullptr;
-        want_sink |= batch[k]->sink != nullptr;
-    }
-    const uint64_t N = base.back();
-    if (N == 0) return OXH_OK;
-    std::vector<const char*> paths(N);
-    for (size_t k = 0; k < batch.size(); ++k)
-        for (uint64_t i = 0; i < batch[k]->n; ++i) paths[base[k] + i] = batch[k]->paths[i];
-    std::vector<uint64_t> out(2 * N), lens(N), counts(want_counts ? 2 * N : 0);
-    std::vector<int32_t> st(N), utf8(want_utf8 ? N : 0);
-    ItemSink sink = [&](uint64_t id, const uint8_t* bytes, uint64_t len, uint64_t lo, uint64_t hi) {
-        const size_t k = (size_t)(std::upper_bound(base.begin(), base.end(), id) - base.begin()) - 1;
-        if (batch[k]->sink) (*batch[k]->sink)(id - base[k], bytes, len, lo, hi);
-    };
-    c->utf8_out = want_utf8 ? utf8.data() : nullptr;
-    const int rc = stream_files(c, paths.data(), N, out.data(), lens.data(), st.data(),
-                                want_counts ? counts.data() : nullptr, want_sink ? &sink : nullptr);
-    if (rc) return rc;
-    for (size_t k = 0; k < batch.size(); ++k) {
-        FileRequest* r = batch[k];
-        const uint64_t b = base[k];
-        std::copy(out.begin() + 2 * b, out.begin() + 2 * (b + r->n), r->out);
-        if (r->sizes) std::copy(lens.begin() + b, lens.begin() + b + r->n, r->sizes);
-        if (r->status) std::copy(st.begin() + b, st.begin() + b + r->n, r->status);
-        if (r->counts) std::copy(counts.begin() + 2 * b, counts.begin() + 2 * (b + r->n), r->counts);
-        if (r->utf8) std::copy(utf8.begin() + b, utf8.begin() + b + r->n, r->utf8);
-    }
-    return OXH_OK;
-}
+}  // namespace
 
 static int hash_files_impl(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* sizes, int32_t* status,
                            uint64_t* counts, const ItemSink* sink = nullptr, int32_t* utf8 = nullptr) {
     if (!c || (n && (!paths || !out))) return fail(OXH_ERR_INVALID, "bad arguments");
+    if (n == 0) return OXH_OK;
     FileRequest r;
     r.paths = paths;
     r.n = n;
@@ -1054,33 +1218,17 @@ static int hash_files_impl(oxh_ctx* c, const char* const* paths, uint64_t n, uin
     r.counts = counts;
     r.utf8 = utf8;
     r.sink = sink;
-    std::unique_lock<std::mutex> lk(c->qmu);
-    c->queue.push_back(&r);
-    if (c->leader) {
-        r.cv.wait(lk, [&] { return r.done || r.lead; });
-        if (r.done) return r.rc ? fail(r.rc, r.msg) : OXH_OK;
+    r.lens.assign(n, 0);
+    r.st.assign(n, OXH_OK);
+    r.remaining.store(n);
+    {
+        std::lock_guard<std::mutex> g(c->qmu);
+        c->queue.push_back(&r);
+        c->qcv.notify_all();  // the engine (idle) or the live run's idle readers
     }
-    // leader: run everything queued now (this request included) as one pipeline
-    c->leader = true;
-    std::vector<FileRequest*> batch;
-    batch.swap(c->queue);
-    lk.unlock();
-    const int rc = run_requests(c, batch);
-    const std::string msg = rc ? g_err : std::string();
-    lk.lock();
-    for (FileRequest* q : batch) {
-        q->rc = rc;
-        q->msg = msg;
-        q->done = true;
-        if (q != &r) q->cv.notify_all();
-    }
-    if (!c->queue.empty()) {  // hand over to the oldest waiting caller
-        c->queue.front()->lead = true;
-        c->queue.front()->cv.notify_all();
-    } else {
-        c->leader = false;
-    }
-    return rc;
+    std::unique_lock<std::mutex> lk(r.mu);
+    r.cv.wait(lk, [&] { return r.done; });
+    return r.rc ? fail(r.rc, r.msg) : OXH_OK;
 }
 
 int oxh_hash_files(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* sizes, int32_t* status) {
