@@ -233,7 +233,7 @@ def main() -> None:
             "data": "synthetic (splitmix64 byte stream, seed %d+rank), device-resident in HBM" % args.seed,
             "config": {"workload": desc, "items_per_gpu": n_items, "item_bytes": item_len,
                        "bytes_per_gpu": bytes_per_rank, "parallelism": f"files sharded x{world}, RCCL all-gather of digests" if world > 1 else "single GPU",
-                       "kernel_variant": args.variant},
+                       "kernel_variant": args.variant or "auto (8: 2-round ring, items > 16 KiB)"},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

@@ -102,15 +102,18 @@ WaveKernel wave_kernel_for(int variant) {
 
 // K1 register/pipeline shape by item size (measured): items of a few KiB want many
 // resident waves (2-round ring, keys in LDS: 77 VGPRs, 6 waves/SIMD, every load issued up front);
-// large items want 4 rounds in flight per wave (201 VGPRs, 2 waves/SIMD). An explicit
+// larger items a 2-round ring with the keys in registers (variant 8). The 4-round ring (variant 0,
+// 201 VGPRs, 2 waves/SIMD) matches it on equal 64 KiB items but loses 13 % on ragged, packed items
+// (FastCDC chunks: tools/k1_align_probe.py) and 4 % of the C2 step rate. An explicit
 // oxh_set_kernel_variant() overrides the choice.
 constexpr uint64_t kShortItemBytes = 16384;
 constexpr int kVariantShort = 72;  // Cfg: depth 2, keys in LDS
+constexpr int kVariantLong = 8;    // Cfg: depth 2, keys from the constant table
 
 int pick_variant(bool short_items) {
     const int v = g_variant.load();
     if (v != 0) return v;
-    return short_items ? kVariantShort : 0;
+    return short_items ? kVariantShort : kVariantLong;
 }
 
 // K1 over a descriptor table: one 64-lane wave per item, 4 waves per 256-thread workgroup.

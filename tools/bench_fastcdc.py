@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=65536)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--check-mib", type=int, default=256)
+    ap.add_argument("--variant", type=int, default=0, help="force a K1 variant (0 = the library's choice)")
     args = ap.parse_args()
 
     import torch
@@ -37,6 +38,8 @@ def main():
     from oxen_amd.device import fastcdc_device, fill_splitmix, to_numpy_u64
 
     dev = torch.device("cuda:0")
+    from oxen_amd import _capi
+    _capi.lib().oxh_set_kernel_variant(args.variant)
     size = int(args.gib * 2**30)
     pitch = (size + 4095) // 4096 * 4096
     arena = torch.empty(pitch * args.files, dtype=torch.uint8, device=dev)

@@ -7,6 +7,9 @@ Cases (each ~6.5 GB device-resident, K1 = oxh_xxh3_128_batch_device, HIP-event t
   c2_shift3      the same items starting 3 bytes later (every load misaligned)
   ragged_256     lengths uniform in [4 KiB, 128 KiB), packed at 256-B alignment
   ragged_packed  the same lengths packed back to back (arbitrary alignment, like FastCDC chunks)
+  ragged_4       the same lengths packed at 4-B alignment (no item takes the byte-shift path)
+  ragged_4p1     ragged_4 shifted by 1 B (every item takes the byte-shift path)
+  ragged_packed_vN  ragged_packed with K1 variant N forced (oxh_set_kernel_variant)
 """
 from __future__ import annotations
 
@@ -28,7 +31,7 @@ def main():
     dev = torch.device("cuda:0")
     rng = np.random.default_rng(0)
     total = 100_000 * 65536
-    arena = torch.empty(total + 4096, dtype=torch.uint8, device=dev)
+    arena = torch.empty(total + (1 << 20), dtype=torch.uint8, device=dev)
     fill_splitmix(arena, 5)
 
     def case(offs, lens):
@@ -61,6 +64,17 @@ def main():
     lens2 = lens[: np.searchsorted(np.cumsum(lens), total)]
     offs_packed = np.concatenate([[0], np.cumsum(lens2)[:-1]])
     res["ragged_packed"] = case(offs_packed, lens2)
+    offs4 = np.concatenate([[0], np.cumsum((lens2 + 3) // 4 * 4)[:-1]])
+    res["ragged_4"] = case(offs4, lens2)
+    res["ragged_4p1"] = case(offs4 + 1, lens2)
+    from oxen_amd import _capi
+    layouts = {"c2_aligned": (np.arange(n) * 65536, np.full(n, 65536)), "ragged_256": (offs256, lens),
+               "ragged_packed": (offs_packed, lens2), "ragged_4p1": (offs4 + 1, lens2)}
+    for v in (64, 65, 66, 68, 72, 76, 8):
+        _capi.lib().oxh_set_kernel_variant(v)
+        for name, (o, ln) in layouts.items():
+            res[f"{name}_v{v}"] = case(o, ln)
+    _capi.lib().oxh_set_kernel_variant(0)
     print(json.dumps(res), flush=True)
 
 
