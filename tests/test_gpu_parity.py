@@ -597,3 +597,74 @@ def test_concurrent_callers_coalesce(oracle_lib, tmp_path, cuda):
                 assert d[:64] == want[t * 64:(t + 1) * 64], t
                 if t % 3 == 0:
                     assert st[64] != 0 and d[64] in (None, 0)
+
+
+@pytest.mark.gpu
+def test_concurrent_mixed_requests_join_live_run(oracle_lib, tmp_path, cuda):
+    """Requests of every kind join one live engine run: text/UTF-8 requests arriving while plain hash
+    requests stream (the slots switch to K1T + is_utf8 mid-run), files larger than the staging slot
+    (oversize path inside the live run), missing files, and empty requests -- each caller gets
+    exactly the reference's digests, text counts and is_utf8 for its own files."""
+    import threading
+
+    from oracle import oracle
+    from oxen_amd import _capi, hasher
+    from oxen_amd.workloads import splitmix_bytes
+
+    rng = np.random.default_rng(33)
+    paths, blobs = [], []
+    for i in range(12 * 48):
+        kind = i % 3
+        if kind == 0:
+            b = splitmix_bytes(900 + i, 0, int(rng.integers(0, 40_000))).tobytes()
+        elif kind == 1:
+            b = ("line %d é ü\n" % i * int(rng.integers(1, 3000))).encode()
+        else:
+            # a 2-byte sequence cut off by the end (still UTF-8 for is_utf8), or broken mid-file
+            b = ("x" * int(rng.integers(0, 5000))).encode() + (b"\xc3x" if i % 2 else b"\xc3")
+        if i == 60:
+            b = splitmix_bytes(77, 0, (3 << 20) + 12345).tobytes()  # > the 2 MiB staging slot
+        p = tmp_path / f"m{i}.dat"
+        p.write_bytes(b)
+        paths.append(str(p))
+        blobs.append(b)
+    want = [oracle.xxh3_128_int(b) for b in blobs]
+    want_counts = [(1 + b.count(b"\n"), len(b) - sum(1 for x in b if (x & 0xC0) == 0x80)) for b in blobs]
+    want_utf8 = [oracle.is_utf8_prefix(b[:4096]) for b in blobs]
+    results, errors = {}, []
+    with _capi.Context(0, staging_bytes=2 << 20) as c:
+        def worker(t):
+            try:
+                batch = paths[t * 48:(t + 1) * 48]
+                if t % 5 == 4:
+                    batch = batch + [str(tmp_path / "nope")]
+                if t == 7:
+                    results[("empty", t)] = hasher.hash_files_128bit([], c)
+                if t % 2 == 1:
+                    d, sz, st, meta, u8 = hasher.hash_files_text_utf8_128bit(batch, c)
+                    results[t] = (d, st, meta, u8)
+                else:
+                    d, sz, st = hasher.hash_files_128bit(batch, c)
+                    results[t] = (d, st, None, None)
+            except Exception as e:  # pragma: no cover - reported below
+                errors.append(repr(e))
+
+        for _round in range(2):
+            results.clear()
+            th = [threading.Thread(target=worker, args=(t,)) for t in range(12)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            assert not errors, errors
+            for t in range(12):
+                d, st, meta, u8 = results[t]
+                lo = t * 48
+                assert d[:48] == want[lo:lo + 48], t
+                assert all(s == 0 for s in st[:48]), t
+                if meta is not None:
+                    got = [(m["text"]["num_lines"], m["text"]["num_chars"]) for m in meta[:48]]
+                    assert got == want_counts[lo:lo + 48], t
+                    assert u8[:48] == want_utf8[lo:lo + 48], t
+                if t % 5 == 4:
+                    assert st[48] != 0 and d[48] is None
