@@ -33,7 +33,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <map>
+#include <mutex>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -620,6 +624,21 @@ __global__ void cdc_first_kernel(const uint64_t* __restrict__ sec_base, const ui
     if (i <= n_files) first[i] = out_base[sec_base[i]];
 }
 
+// File of every section (sec_base is the exclusive prefix of per-file section counts): built on the
+// device so no section-sized table is copied from pageable host memory.
+__global__ void cdc_sec_file_kernel(const uint64_t* __restrict__ sec_base, uint64_t n_files, uint64_t n_sec,
+                                    uint32_t* __restrict__ sec_file) {
+    const uint64_t sec = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (sec >= n_sec) return;
+    uint64_t lo = 0, hi = n_files;  // last file with sec_base[file] <= sec
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (sec_base[mid] <= sec) lo = mid;
+        else hi = mid;
+    }
+    sec_file[sec] = (uint32_t)lo;
+}
+
 }  // namespace oxh
 
 // ---------------------------------------------------------------- host side
@@ -640,21 +659,74 @@ uint32_t log2_round(uint32_t v) {
 }
 
 // stream-ordered scratch, freed on every exit path
+// Scratch (candidate lists, speculative starts, stitch tables: ~8 GB for C5) lives in one device
+// buffer per device that is kept between calls, up to OXH_SCRATCH_KEEP_MIB (default 16 GiB), and
+// calls on a device take it in turn (each call fills the GPU anyway). Per-call stream-ordered
+// allocations of that size occasionally stalled the host for 0.5-1.2 s before the first launch
+// (tools/bench_fastcdc.py, OXH_TRACE=1), with the default pool and with a private one alike.
+struct ScratchCache {
+    std::mutex mu;
+    void* base = nullptr;
+    uint64_t size = 0;
+};
+
+ScratchCache& scratch_cache(int dev) {
+    static std::mutex mu;
+    static std::map<int, ScratchCache*> caches;  // one per device, never freed (process lifetime)
+    std::lock_guard<std::mutex> g(mu);
+    ScratchCache*& c = caches[dev];
+    if (!c) c = new ScratchCache();
+    return *c;
+}
+
 struct Scratch {
     hipStream_t st;
-    std::vector<void*> ptrs;
-    explicit Scratch(hipStream_t s) : st(s) {}
+    ScratchCache* cache = nullptr;
+    std::unique_lock<std::mutex> lk;
+    std::vector<std::pair<void**, uint64_t>> parts;
+    explicit Scratch(hipStream_t s) : st(s) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        cache = &scratch_cache(dev);
+        lk = std::unique_lock<std::mutex>(cache->mu);
+    }
     ~Scratch() {
-        // host vectors fed stream-ordered copies: on an error path they must be done before the
-        // caller's frames unwind
+        // host vectors fed stream-ordered copies and the kernels use the buffer: finish first
         (void)hipStreamSynchronize(st);
-        for (void* p : ptrs) (void)hipFreeAsync(p, st);
+        static const uint64_t keep = (getenv("OXH_SCRATCH_KEEP_MIB") ? strtoull(getenv("OXH_SCRATCH_KEEP_MIB"), nullptr, 10)
+                                                                     : 16384ull) << 20;
+        if (cache->size > keep) {
+            (void)hipFree(cache->base);
+            cache->base = nullptr;
+            cache->size = 0;
+        }
     }
     template <class T>
-    hipError_t alloc(T** p, uint64_t count) {
-        const hipError_t e = hipMallocAsync((void**)p, std::max<uint64_t>(count, 1) * sizeof(T), st);
-        if (e == hipSuccess) ptrs.push_back(*p);
-        return e;
+    void want(T** p, uint64_t count) {
+        parts.push_back({(void**)p, (std::max<uint64_t>(count, 1) * sizeof(T) + 255) & ~255ull});
+    }
+    // carve every wanted part out of the cached buffer, growing it first if needed
+    hipError_t commit() {
+        uint64_t total = 0;
+        for (auto& q : parts) total += q.second;
+        if (cache->size < total) {
+            if (cache->base) {
+                hipError_t e = hipDeviceSynchronize();  // an earlier call's work may still read it
+                if (e != hipSuccess) return e;
+                (void)hipFree(cache->base);
+                cache->base = nullptr;
+                cache->size = 0;
+            }
+            hipError_t e = hipMalloc(&cache->base, total);
+            if (e != hipSuccess) return e;
+            cache->size = total;
+        }
+        uint64_t off = 0;
+        for (auto& q : parts) {
+            *q.first = (uint8_t*)cache->base + off;
+            off += q.second;
+        }
+        return hipSuccess;
     }
 };
 
@@ -729,37 +801,45 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     sec_base[0] = 0;
     for (uint64_t i = 0; i < n; ++i) sec_base[i + 1] = sec_base[i] + (lens[i] + prm.sec - 1) / prm.sec;
     const uint64_t n_sec = sec_base[n];
-    std::vector<uint32_t> sec_file(std::max<uint64_t>(n_sec, 1));
-    for (uint64_t i = 0; i < n; ++i)
-        for (uint64_t s = sec_base[i]; s < sec_base[i + 1]; ++s) sec_file[s] = (uint32_t)i;
 
+    // OXH_TRACE=1: host-side stage times of this call on stderr
+    static const bool trace = getenv("OXH_TRACE") != nullptr;
+    const auto t_start = std::chrono::steady_clock::now();
+    auto since = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(); };
     Scratch sc(st);
     uint64_t *d_foff, *d_flen, *d_sec_base, *d_first, *d_exit, *d_out_base;
     uint32_t *d_sec_file, *d_cand, *d_cand_cnt, *d_spec, *d_spec_cnt, *d_status, *d_k0, *d_count, *d_fix;
     uint64_t* d_cand_h;
     uint4* d_cand_b;
-    CDC_HIP(sc.alloc(&d_foff, n));
-    CDC_HIP(sc.alloc(&d_flen, n));
-    CDC_HIP(sc.alloc(&d_sec_base, n + 1));
-    CDC_HIP(sc.alloc(&d_first, n + 1));
-    CDC_HIP(sc.alloc(&d_sec_file, n_sec));
-    CDC_HIP(sc.alloc(&d_cand, n_sec * prm.cap));
-    CDC_HIP(sc.alloc(&d_cand_h, n_sec * prm.cap));
-    CDC_HIP(sc.alloc(&d_cand_b, n_sec * prm.cap));
-    CDC_HIP(sc.alloc(&d_cand_cnt, n_sec));
-    CDC_HIP(sc.alloc(&d_spec, n_sec * prm.speccap));
-    CDC_HIP(sc.alloc(&d_spec_cnt, n_sec));
-    CDC_HIP(sc.alloc(&d_status, n_sec));
-    CDC_HIP(sc.alloc(&d_k0, n_sec));
-    CDC_HIP(sc.alloc(&d_count, n_sec));
-    CDC_HIP(sc.alloc(&d_exit, n_sec));
-    CDC_HIP(sc.alloc(&d_fix, n_sec * prm.speccap));
-    CDC_HIP(sc.alloc(&d_out_base, n_sec + 1));
+    sc.want(&d_foff, n);
+    sc.want(&d_flen, n);
+    sc.want(&d_sec_base, n + 1);
+    sc.want(&d_first, n + 1);
+    sc.want(&d_sec_file, n_sec);
+    sc.want(&d_cand, n_sec * prm.cap);
+    sc.want(&d_cand_h, n_sec * prm.cap);
+    sc.want(&d_cand_b, n_sec * prm.cap);
+    sc.want(&d_cand_cnt, n_sec);
+    sc.want(&d_spec, n_sec * prm.speccap);
+    sc.want(&d_spec_cnt, n_sec);
+    sc.want(&d_status, n_sec);
+    sc.want(&d_k0, n_sec);
+    sc.want(&d_count, n_sec);
+    sc.want(&d_exit, n_sec);
+    sc.want(&d_fix, n_sec * prm.speccap);
+    sc.want(&d_out_base, n_sec + 1);
+    CDC_HIP(sc.commit());
+    const double t_malloc = since();
     CDC_HIP(hipMemcpyAsync(d_foff, offsets, n * 8, hipMemcpyHostToDevice, st));
     CDC_HIP(hipMemcpyAsync(d_flen, lens, n * 8, hipMemcpyHostToDevice, st));
     CDC_HIP(hipMemcpyAsync(d_sec_base, sec_base.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
-    if (n_sec) CDC_HIP(hipMemcpyAsync(d_sec_file, sec_file.data(), n_sec * 4, hipMemcpyHostToDevice, st));
+    if (n_sec) {
+        hipLaunchKernelGGL(oxh::cdc_sec_file_kernel, dim3((unsigned)((n_sec + 255) / 256)), dim3(256), 0, st, d_sec_base, n,
+                           n_sec, d_sec_file);
+        CDC_HIP(hipGetLastError());
+    }
 
+    const double t_alloc = since();
     oxh::CdcFiles f{(const uint8_t*)d_arena, d_foff, d_flen, d_sec_base, d_sec_file, d_cand, d_cand_h, d_cand_b, d_cand_cnt, d_spec, d_spec_cnt};
     oxh::CdcStitch sti{d_status, d_k0, d_count, d_exit, d_fix, d_out_base};
     if (n_sec) {
@@ -795,7 +875,11 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
                        d_first);
     CDC_HIP(hipGetLastError());
     CDC_HIP(hipMemcpyAsync(first_chunk, d_first, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+    const double t_launch = since();
     CDC_HIP(hipStreamSynchronize(st));
+    if (trace)
+        fprintf(stderr, "[oxh] fastcdc: sections=%llu malloc=%.4fs copy=%.4fs launch=%.4fs chunking=%.4fs scratch=%.2fGiB\n",
+                (unsigned long long)n_sec, t_malloc, t_alloc - t_malloc, t_launch - t_alloc, since(), sc.cache->size / 1073741824.0);
     const uint64_t total = first_chunk[n];
     if (total > capacity)
         return cdc_fail(OXH_ERR_INVALID, "chunk capacity too small: need " + std::to_string(total) + " entries");

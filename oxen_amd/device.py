@@ -118,11 +118,12 @@ def fill_splitmix(buf: torch.Tensor, seed: int, nbytes: Optional[int] = None, st
 
 
 def fastcdc_device(arena: torch.Tensor, offsets, lens, min_size: int, avg_size: int, max_size: int,
-                   level: int = 1, digests: bool = True, stream=None):
+                   level: int = 1, digests: bool = True, stream=None, out=None):
     """FastCDC v2020 chunks (+ XXH3-128 of every chunk) of device-resident files
     arena[offsets[i] : offsets[i] + lens[i]] (offsets/lens are host sequences).
     Returns (chunk_offsets, chunk_lens, chunk_digests or None) as int64 device tensors and
-    first_chunk (numpy uint64, n+1): file i's chunks are rows first_chunk[i] .. first_chunk[i+1]."""
+    first_chunk (numpy uint64, n+1): file i's chunks are rows first_chunk[i] .. first_chunk[i+1].
+    `out` = (c_off, c_len, dig) from fastcdc_outputs() reuses preallocated chunk tables."""
     _require_cuda(arena)
     offs = np.ascontiguousarray(offsets, dtype=np.uint64)
     ln = np.ascontiguousarray(lens, dtype=np.uint64)
@@ -132,10 +133,15 @@ def fastcdc_device(arena: torch.Tensor, offsets, lens, min_size: int, avg_size: 
     if n and int((offs + ln).max()) > arena.numel() * arena.element_size():
         raise _capi.OxenError("a file extends past the arena", _capi.OXH_ERR_INVALID)
     L = _capi.lib()
-    cap = max(1, int(L.oxh_fastcdc_max_chunks(ln.ctypes.data_as(_capi._u64p), n, max(1, int(min_size)))))
-    c_off = torch.empty(cap, dtype=torch.int64, device=arena.device)
-    c_len = torch.empty(cap, dtype=torch.int64, device=arena.device)
-    dig = torch.empty((cap, 2), dtype=torch.int64, device=arena.device) if digests else None
+    if out is None:
+        out = fastcdc_outputs(arena, ln, min_size, digests)
+    c_off, c_len, dig = out
+    if not digests:
+        dig = None
+    cap = c_off.numel()
+    need = max(1, int(L.oxh_fastcdc_max_chunks(ln.ctypes.data_as(_capi._u64p), n, max(1, int(min_size)))))
+    if cap < need or c_len.numel() < need or (dig is not None and dig.shape[0] < need):
+        raise _capi.OxenError(f"chunk tables hold {cap} rows, need {need}", _capi.OXH_ERR_INVALID)
     first = np.zeros(n + 1, dtype=np.uint64)
     _capi.check(L.oxh_fastcdc_device(arena.data_ptr(), offs.ctypes.data_as(_capi._u64p), ln.ctypes.data_as(_capi._u64p),
                                      n, int(min_size), int(avg_size), int(max_size), int(level), c_off.data_ptr(),
@@ -143,6 +149,16 @@ def fastcdc_device(arena: torch.Tensor, offsets, lens, min_size: int, avg_size: 
                                      first.ctypes.data_as(_capi._u64p), _stream(stream)), "oxh_fastcdc_device")
     total = int(first[n])
     return c_off[:total], c_len[:total], (dig[:total] if dig is not None else None), first
+
+
+def fastcdc_outputs(arena: torch.Tensor, lens, min_size: int, digests: bool = True):
+    """Chunk tables sized for fastcdc_device over files of these lengths: (c_off, c_len, dig)."""
+    ln = np.ascontiguousarray(lens, dtype=np.uint64)
+    cap = max(1, int(_capi.lib().oxh_fastcdc_max_chunks(ln.ctypes.data_as(_capi._u64p), len(ln), max(1, int(min_size)))))
+    c_off = torch.empty(cap, dtype=torch.int64, device=arena.device)
+    c_len = torch.empty(cap, dtype=torch.int64, device=arena.device)
+    dig = torch.empty((cap, 2), dtype=torch.int64, device=arena.device) if digests else None
+    return c_off, c_len, dig
 
 
 def to_numpy_u64(t: torch.Tensor) -> np.ndarray:
