@@ -9,7 +9,7 @@
 //
 // The walk is serial per file (each cut decides where the next chunk's hash starts). The GPU
 // formulation splits it into three kernels:
-//   F1 cdc_scan_kernel    chip-wide, one wave per 256 KiB section, HBM-bound: the FULL-window gear
+//   F1 cdc_scan_kernel    chip-wide, one wave per section (>= 512 KiB): the FULL-window gear
 //                         hash at every byte (all mask bits are below bit 48, so only the last 48
 //                         bytes matter and the hash of position p is a function of b[p-47 .. p]) and
 //                         a compact, position-ordered list of candidate positions per section
@@ -60,7 +60,7 @@ static constexpr uint64_t kCdcMasks[26] = {
     0x0000db3777577000ULL,
 };
 
-constexpr uint32_t kSecDefault = 256 * 1024;  // section bytes (F1 wave / F2 lane unit)
+constexpr uint32_t kSecDefault = 512 * 1024;  // minimum section bytes (F1 wave / F2 lane unit)
 constexpr int kHashSpan = 47;          // positions after a chunk's start index with a truncated window
 
 struct CdcParams {
@@ -573,7 +573,7 @@ __global__ __launch_bounds__(64) void cdc_fixup_kernel(CdcFiles f, CdcParams prm
     }
 }
 
-// F3c: exclusive prefix of the per-section counts (one block; n_sec is ~ bytes / 256 KiB).
+// F3c: exclusive prefix of the per-section counts (one block; n_sec is ~ bytes / 512 KiB).
 __global__ __launch_bounds__(1024) void cdc_prefix_kernel(CdcStitch s, uint64_t n_sec) {
     __shared__ uint64_t part[1024];
     const uint64_t per = (n_sec + 1023) / 1024;
@@ -787,12 +787,15 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     }
     // sections of at least `max` bytes: a chunk never spans a whole section (F3's invariant)
     // Speculative walks meet the true walk after ~1.5 chunks (median) and within 6 chunks in 99 % of
-    // random starts (measured with the oracle): 4 max-sized chunks of warm-up, sections of at least
-    // 4 max-sized chunks so the warm-up costs at most as much as the section itself.
+    // random starts (measured with the oracle). Warm-up: 4 max-sized chunks, at least 128 KiB;
+    // sections: at least 8 max-sized chunks and 512 KiB. Every section whose walk has not met the
+    // true one is re-walked serially by F3, so at small chunk sizes the longer warm-up pays for itself
+    // (C5 at 8 KiB: 57.2 ms vs 63.8 ms with 256 KiB sections and 64 KiB of warm-up; at 64 KiB: 53.8
+    // vs 54.9 ms with 1 MiB sections; tools/bench_fastcdc.py sweeps).
     const uint64_t max_rounded = ((uint64_t)max_size + 1023) / 1024 * 1024;
-    prm.warmup = 4 * (uint64_t)max_size;
+    prm.warmup = std::max<uint64_t>(4 * (uint64_t)max_size, 128 * 1024);
     if (prm.sec < max_rounded) prm.sec = max_rounded;
-    if (!getenv("OXH_CDC_SECTION_BYTES") && prm.sec < 4 * max_rounded) prm.sec = 4 * max_rounded;
+    if (!getenv("OXH_CDC_SECTION_BYTES") && prm.sec < 8 * max_rounded) prm.sec = 8 * max_rounded;
     if (const char* e = getenv("OXH_CDC_WARMUP_BYTES")) prm.warmup = strtoull(e, nullptr, 10);  // tests
     prm.cap = (uint32_t)std::min<double>(prm.sec / 16, 8.0 * dens * prm.sec + 64);
     prm.speccap = (uint32_t)(prm.sec / min_size + 2 + (max_size + min_size - 1) / min_size);
