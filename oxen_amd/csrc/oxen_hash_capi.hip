@@ -10,6 +10,7 @@
 // There is no CPU hashing path here: every digest this library returns was computed on the GPU.
 #include <hip/hip_runtime.h>
 #include <dirent.h>
+#include <sched.h>
 #include <errno.h>
 #include <fcntl.h>
 #include <ftw.h>
@@ -160,12 +161,32 @@ int launch_lane(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens
     return OXH_OK;
 }
 
+// CPUs this process may use: the affinity mask, capped by a cgroup-v2 CPU quota (a container's
+// cpu.max, e.g. "1600000 100000" = 16 CPUs); hardware_concurrency() sees the whole machine.
+int usable_cpus() {
+    unsigned n = std::thread::hardware_concurrency();
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0) n = (unsigned)CPU_COUNT(&set);
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char quota[32] = {0};
+        unsigned long long period = 0;
+        if (fscanf(f, "%31s %llu", quota, &period) == 2 && strcmp(quota, "max") != 0 && period > 0) {
+            const unsigned long long q = strtoull(quota, nullptr, 10);
+            const unsigned cap = (unsigned)std::max<unsigned long long>(1, (q + period - 1) / period);
+            n = n ? std::min(n, cap) : cap;
+        }
+        fclose(f);
+    }
+    return (int)(n ? n : 4);
+}
+
 int default_threads() {
     const char* e = getenv("OXH_NUM_THREADS");  // cf. OXEN_NUM_THREADS (util/concurrency.rs:1-45)
     if (e && atoi(e) > 0) return atoi(e);
-    unsigned hc = std::thread::hardware_concurrency();
-    return (int)std::max(1u, std::min(hc ? hc : 4u, 16u));
+    return std::max(1, std::min(usable_cpus(), 16));
 }
+
+
 
 }  // namespace
 
