@@ -133,8 +133,17 @@ int launch_text(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens
                 uint64_t* counts, hipStream_t st, bool short_items = false) {
     if (n == 0) return OXH_OK;
     const uint64_t blocks = (n + 3) / 4;
-    if (pick_variant(short_items) == kVariantShort)
+    // K1T keeps the 2-round ring with the keys in LDS at every item size: the counting needs the
+    // registers (tools/k1t_probe.py: 6.41 TB/s on C2 and 5.55 on ragged items, against 5.42 / 4.40
+    // with variant 8 and 4.32 / 2.56 with the 4-round ring)
+    (void)short_items;
+    const int forced = g_variant.load();
+    const int v = forced ? forced : kVariantShort;
+    if (v == kVariantShort)
         hipLaunchKernelGGL(oxh::xxh3_text_wave_kernel<kVariantShort>, dim3((unsigned)blocks), dim3(256), 0, st, arena, offs, lens,
+                           n, out, counts);
+    else if (v == kVariantLong)
+        hipLaunchKernelGGL(oxh::xxh3_text_wave_kernel<kVariantLong>, dim3((unsigned)blocks), dim3(256), 0, st, arena, offs, lens,
                            n, out, counts);
     else
         hipLaunchKernelGGL(oxh::xxh3_text_wave_kernel<0>, dim3((unsigned)blocks), dim3(256), 0, st, arena, offs, lens, n, out,

@@ -728,6 +728,7 @@ template __global__ void xxh3_wave_kernel<true, 72>(const uint8_t*, const uint64
 template __global__ void xxh3_wave_kernel<false, 72>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 template __global__ void xxh3_text_wave_kernel<0>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t*, uint64_t*);
 template __global__ void xxh3_text_wave_kernel<72>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t*, uint64_t*);
+template __global__ void xxh3_text_wave_kernel<8>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t*, uint64_t*);
 template __global__ void xxh3_blocksum_kernel<true>(const uint8_t*, uint64_t, uint64_t*);
 template __global__ void xxh3_blocksum_kernel<false>(const uint8_t*, uint64_t, uint64_t*);
 

@@ -344,12 +344,23 @@ def _text_counts(b: bytes):
     return 1 + b.count(b"\n"), sum(1 for x in b if (x & 0xC0) != 0x80)
 
 
-def test_text_counts_fused_every_length(cuda, oracle_lib):
-    """K1T: digests identical to K1 and text counts exact for every length class, aligned and not."""
+@pytest.mark.parametrize("variant", [0, 8, 72, 4])
+def test_text_counts_fused_every_length(cuda, oracle_lib, variant):
+    """K1T: digests identical to K1 and text counts exact for every length class, aligned and not,
+    for the default dispatch and every K1T instantiation (<8>, <72>, <0> via a forced variant)."""
     import torch
 
+    from oxen_amd import _capi
     from oxen_amd.device import xxh3_128_text_batch_device
 
+    _capi.lib().oxh_set_kernel_variant(variant)
+    try:
+        _check_text_counts(cuda, oracle_lib, torch, xxh3_128_text_batch_device)
+    finally:
+        _capi.lib().oxh_set_kernel_variant(0)
+
+
+def _check_text_counts(cuda, oracle_lib, torch, xxh3_128_text_batch_device):
     rng = np.random.default_rng(9)
     alphabet = np.frombuffer("ab\nc é漢\n🐂 z\n".encode(), dtype=np.uint8)
     lens = list(range(0, 300)) + [1023, 1024, 1025, 4095, 4096, 4097, 8191, 8192, 49_292, 65_536, 100_003]
