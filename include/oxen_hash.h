@@ -83,7 +83,9 @@ int oxh_xxh3_128_large_device(oxh_ctx* ctx, const void* d_buf, uint64_t len, uin
 
 /* K1L over n large device-resident buffers (e.g. the 16 x 8 GiB files of the dedup experiment):
  * d_bufs and lens are HOST arrays of n device pointers / lengths; d_out (device) gets 2n u64.
- * Block sums run chip-wide per buffer, then up to 32 serial chains run concurrently in one launch. */
+ * Block sums run chip-wide per buffer, then up to 32 serial chains run concurrently in one launch.
+ * The block sums live in the device's cached scratch buffer, so both K1L calls return only after
+ * `stream` has finished them (calls on one device take the scratch in turn). */
 int oxh_xxh3_128_large_batch_device(const void* const* d_bufs, const uint64_t* lens, uint64_t n,
                                     uint64_t* d_out, void* stream);
 

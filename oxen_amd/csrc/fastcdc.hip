@@ -44,6 +44,7 @@
 
 #include "../../include/oxen_hash.h"
 #include "fastcdc_gear.h"
+#include "scratch.hpp"
 
 namespace oxh {
 
@@ -659,71 +660,25 @@ uint32_t log2_round(uint32_t v) {
 }
 
 // stream-ordered scratch, freed on every exit path
-// Scratch (candidate lists, speculative starts, stitch tables: ~8 GB for C5) lives in one device
-// buffer per device that is kept between calls, up to OXH_SCRATCH_KEEP_MIB (default 16 GiB), and
-// calls on a device take it in turn (each call fills the GPU anyway). Per-call stream-ordered
-// allocations of that size occasionally stalled the host for 0.5-1.2 s before the first launch
-// (tools/bench_fastcdc.py, OXH_TRACE=1), with the default pool and with a private one alike.
-struct ScratchCache {
-    std::mutex mu;
-    void* base = nullptr;
-    uint64_t size = 0;
-};
-
-ScratchCache& scratch_cache(int dev) {
-    static std::mutex mu;
-    static std::map<int, ScratchCache*> caches;  // one per device, never freed (process lifetime)
-    std::lock_guard<std::mutex> g(mu);
-    ScratchCache*& c = caches[dev];
-    if (!c) c = new ScratchCache();
-    return *c;
-}
-
+// Per-call scratch (candidate lists, speculative starts, stitch tables) carved out of the device's
+// cached scratch buffer (scratch.hpp).
 struct Scratch {
-    hipStream_t st;
-    ScratchCache* cache = nullptr;
-    std::unique_lock<std::mutex> lk;
+    oxh::ScratchLease lease;
     std::vector<std::pair<void**, uint64_t>> parts;
-    explicit Scratch(hipStream_t s) : st(s) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        cache = &scratch_cache(dev);
-        lk = std::unique_lock<std::mutex>(cache->mu);
-    }
-    ~Scratch() {
-        // host vectors fed stream-ordered copies and the kernels use the buffer: finish first
-        (void)hipStreamSynchronize(st);
-        static const uint64_t keep = (getenv("OXH_SCRATCH_KEEP_MIB") ? strtoull(getenv("OXH_SCRATCH_KEEP_MIB"), nullptr, 10)
-                                                                     : 16384ull) << 20;
-        if (cache->size > keep) {
-            (void)hipFree(cache->base);
-            cache->base = nullptr;
-            cache->size = 0;
-        }
-    }
+    explicit Scratch(hipStream_t s) : lease(s) {}
     template <class T>
     void want(T** p, uint64_t count) {
         parts.push_back({(void**)p, (std::max<uint64_t>(count, 1) * sizeof(T) + 255) & ~255ull});
     }
-    // carve every wanted part out of the cached buffer, growing it first if needed
     hipError_t commit() {
         uint64_t total = 0;
         for (auto& q : parts) total += q.second;
-        if (cache->size < total) {
-            if (cache->base) {
-                hipError_t e = hipDeviceSynchronize();  // an earlier call's work may still read it
-                if (e != hipSuccess) return e;
-                (void)hipFree(cache->base);
-                cache->base = nullptr;
-                cache->size = 0;
-            }
-            hipError_t e = hipMalloc(&cache->base, total);
-            if (e != hipSuccess) return e;
-            cache->size = total;
-        }
+        void* base = nullptr;
+        const hipError_t e = lease.get(total, &base);
+        if (e != hipSuccess) return e;
         uint64_t off = 0;
         for (auto& q : parts) {
-            *q.first = (uint8_t*)cache->base + off;
+            *q.first = (uint8_t*)base + off;
             off += q.second;
         }
         return hipSuccess;
@@ -882,7 +837,7 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     CDC_HIP(hipStreamSynchronize(st));
     if (trace)
         fprintf(stderr, "[oxh] fastcdc: sections=%llu malloc=%.4fs copy=%.4fs launch=%.4fs chunking=%.4fs scratch=%.2fGiB\n",
-                (unsigned long long)n_sec, t_malloc, t_alloc - t_malloc, t_launch - t_alloc, since(), sc.cache->size / 1073741824.0);
+                (unsigned long long)n_sec, t_malloc, t_alloc - t_malloc, t_launch - t_alloc, since(), sc.lease.size() / 1073741824.0);
     const uint64_t total = first_chunk[n];
     if (total > capacity)
         return cdc_fail(OXH_ERR_INVALID, "chunk capacity too small: need " + std::to_string(total) + " entries");

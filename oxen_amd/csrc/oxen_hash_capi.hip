@@ -34,6 +34,7 @@
 
 #include "../../include/oxen_hash.h"
 #include "pool.hpp"
+#include "scratch.hpp"
 #include "xxh3_device.hpp"
 
 namespace oxh {
@@ -240,6 +241,11 @@ namespace {
 
 void engine_main(oxh_ctx* c);  // the streaming file engine's thread (below)
 
+// The chain kernel is VALU-issue-bound per wave (every wave64 instruction takes 4 cycles whatever
+// the exec mask), so two chains on one SIMD run at half speed each. Unused dynamic LDS on top of the
+// kernel's 32 KiB makes every chain workgroup need more than half a CU's 160 KiB: one chain per CU.
+constexpr size_t kChainLdsPad = 50 * 1024;
+
 // K1L over n device buffers: block sums chip-wide (one launch per buffer; each fills the chip),
 // then the serial chains of up to kChainJobs buffers in one launch, one wave each, so the chains of
 // many large files run concurrently. Buffers below ~1 MiB take one K1 wave instead.
@@ -250,7 +256,8 @@ int large_batch_device(const uint8_t* const* bufs, const uint64_t* lens, uint64_
         if (nb >= 1024) total_nb += nb;
     }
     uint64_t* sums = nullptr;
-    if (total_nb) HIP_TRY(hipMallocAsync((void**)&sums, total_nb * 64, st));  // stream-ordered scratch
+    oxh::ScratchLease lease(st);  // the device's cached scratch (scratch.hpp); synchronises st at the end
+    if (total_nb) HIP_TRY(lease.get(total_nb * 64, (void**)&sums));
     oxh::ChainBatch batch;
     int nj = 0;
     uint64_t off = 0;
@@ -272,16 +279,15 @@ int large_batch_device(const uint8_t* const* bufs, const uint64_t* lens, uint64_
         batch.job[nj++] = {bufs[i], len, sums + off, d_out + 2 * i};
         off += nb * 8;
         if (nj == oxh::kChainJobs) {
-            hipLaunchKernelGGL(oxh::xxh3_chain_kernel, dim3(nj), dim3(64), 0, st, batch);
+            hipLaunchKernelGGL(oxh::xxh3_chain_kernel, dim3(nj), dim3(64), kChainLdsPad, st, batch);
             HIP_TRY(hipGetLastError());
             nj = 0;
         }
     }
     if (nj) {
-        hipLaunchKernelGGL(oxh::xxh3_chain_kernel, dim3(nj), dim3(64), 0, st, batch);
+        hipLaunchKernelGGL(oxh::xxh3_chain_kernel, dim3(nj), dim3(64), kChainLdsPad, st, batch);
         HIP_TRY(hipGetLastError());
     }
-    if (sums) HIP_TRY(hipFreeAsync(sums, st));
     return OXH_OK;
 }
 

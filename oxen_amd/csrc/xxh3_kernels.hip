@@ -512,7 +512,7 @@ __global__ __launch_bounds__(256) void xxh3_blocksum_kernel(const uint8_t* __res
 // different CUs). Lanes 0..7 each own one accumulator; block sums stream in GROUP steps at a time
 // with the next group's loads in flight while the current group is chained.
 __global__ __launch_bounds__(64) void xxh3_chain_kernel(ChainBatch batch) {
-    constexpr int GROUP = 128;
+    constexpr int GROUP = 256;
     const ChainJob job = batch.job[blockIdx.x];
     const uint8_t* __restrict__ p = job.p;
     const uint64_t len = job.len;
@@ -528,7 +528,8 @@ __global__ __launch_bounds__(64) void xxh3_chain_kernel(ChainBatch batch) {
     const uint32_t kl = (uint32_t)sk, kh = (uint32_t)(sk >> 32);
     uint64_t acc = kInitW[i];
     auto step = [&](uint32_t& xl, uint32_t& xh, uint64_t s_next) {
-        const uint32_t yl = (xl ^ kl) ^ (xh >> 15);
+        uint32_t yl;  // one 3-input xor (bitop3 0x96) on the critical path; hipcc emits two xors
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(yl) : "v"(xl), "v"(kl), "v"(xh >> 15));
         const uint32_t yh = xh ^ kh;
         uint32_t t = yh * P32_1;  // v_mul_lo_u32, in parallel with the mad below
         asm("" : "+v"(t));        // keep hipcc from folding it into a second, dependent v_mad_u64_u32
@@ -540,20 +541,56 @@ __global__ __launch_bounds__(64) void xxh3_chain_kernel(ChainBatch batch) {
         uint64_t x0 = acc + sums[i];
         uint32_t xl = (uint32_t)x0, xh = (uint32_t)(x0 >> 32);
         uint64_t b = 1;  // x holds acc + S_0; each step scrambles and adds the next block's sum
-        if (nb > GROUP) {
-            uint64_t cur[GROUP];
+        // Block sums reach the chain through LDS: all 64 lanes load the next group of GROUP steps
+        // (GROUP x 64 B) while lanes 0-7 run the current group's chain from LDS. Loading the sums in
+        // the chain lanes themselves let hipcc re-load each one from memory right before its step
+        // (the values are invariant), which put an L1 round trip on every step of the chain.
+        __shared__ uint64_t buf[2][GROUP * 8];
+        constexpr int PER = GROUP * 8 / 64;  // sums per lane per group
+        const uint64_t ngroups = (nb - 1) / GROUP;
+        uint64_t r[PER];
+        auto issue = [&](uint64_t g) {
 #pragma unroll
-            for (int t = 0; t < GROUP; ++t) cur[t] = sums[(1 + (uint64_t)t) * 8 + i];
-            const uint64_t ngroups = (nb - 1) / GROUP;
+            for (int k = 0; k < PER; ++k) {
+                const uint64_t e = (uint64_t)k * 64 + (uint64_t)lane;  // element of the group
+                r[k] = sums[(1 + g * GROUP + e / 8) * 8 + (e & 7)];
+            }
+        };
+        auto commit = [&](int sb) {
+#pragma unroll
+            for (int k = 0; k < PER; ++k) buf[sb][k * 64 + lane] = r[k];
+            __syncthreads();
+        };
+        if (ngroups > 0) {
+            issue(0);
+            commit(0);
             for (uint64_t gi = 0; gi < ngroups; ++gi) {
-                const uint64_t gn = (gi + 1 < ngroups) ? gi + 1 : gi;
-                uint64_t nxt[GROUP];
+                const int sb = (int)(gi & 1);
+                if (gi + 1 < ngroups) issue(gi + 1);
+                if (lane < 8) {
+                    // LDS reads a batch of B steps ahead of the chain (sched_barrier keeps hipcc from
+                    // sinking them to their use, which exposed the LDS latency every other step)
+                    constexpr int B = 32;
+                    uint64_t va[B], vb[B];
 #pragma unroll
-                for (int t = 0; t < GROUP; ++t) nxt[t] = sums[(1 + gn * GROUP + t) * 8 + i];
+                    for (int t = 0; t < B; ++t) va[t] = buf[sb][t * 8 + i];
 #pragma unroll
-                for (int t = 0; t < GROUP; ++t) step(xl, xh, cur[t]);
+                    for (int t0 = 0; t0 < GROUP; t0 += 2 * B) {
 #pragma unroll
-                for (int t = 0; t < GROUP; ++t) cur[t] = nxt[t];
+                        for (int t = 0; t < B; ++t) vb[t] = buf[sb][(t0 + B + t) * 8 + i];
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int t = 0; t < B; ++t) step(xl, xh, va[t]);
+                        if (t0 + 2 * B < GROUP) {
+#pragma unroll
+                            for (int t = 0; t < B; ++t) va[t] = buf[sb][(t0 + 2 * B + t) * 8 + i];
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int t = 0; t < B; ++t) step(xl, xh, vb[t]);
+                    }
+                }
+                if (gi + 1 < ngroups) commit(sb ^ 1);
             }
             b = 1 + ngroups * GROUP;
         }
