@@ -340,7 +340,7 @@ int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_
 // OXH_TRACE=1: per-call stage times on stderr (host-side wall clock)
 struct Trace {
     bool on = getenv("OXH_TRACE") != nullptr;
-    double fill = 0, drain = 0, submit = 0, stat = 0;
+    double fill = 0, drain = 0, submit = 0;
     int batches = 0;
     static double now() {
         return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -354,16 +354,7 @@ using ItemSink = std::function<void(uint64_t id, const uint8_t* bytes, uint64_t 
 struct Pending {
     bool busy = false;
     std::vector<uint64_t> ids;  // caller indices of the staged items
-    std::thread consumer;       // runs the ItemSink over the slot's items while the next slot fills
-    ~Pending() {
-        if (consumer.joinable()) consumer.join();
-    }
 };
-
-// The slot's bytes are still being consumed by the sink: wait before the slot is refilled.
-void join_consumer(Pending& p) {
-    if (p.consumer.joinable()) p.consumer.join();
-}
 
 // Wait for slot s's digests. Polls (a slot is at most a few hundred MiB: milliseconds of work) and,
 // after OXH_WAIT_LIMIT_S seconds (default 60), reports which stage never finished instead of
@@ -390,39 +381,16 @@ int wait_slot(oxh_ctx* c, int s, const Pending& p) {
     }
 }
 
-int drain_slot(oxh_ctx* c, int s, Pending& p, uint64_t* out, uint64_t* counts = nullptr,
-               const ItemSink* sink = nullptr, const int32_t* status = nullptr) {
+// Scatter slot s's digests to the caller's table (host-buffer batches: oxh_hash_buffers/_streams).
+int drain_slot(oxh_ctx* c, int s, Pending& p, uint64_t* out) {
     if (!p.busy) return OXH_OK;
     STEP("drain s=%d", s);
     if (int rc = wait_slot(c, s, p)) return rc;
-    STEP("drained s=%d", s);
     for (size_t j = 0; j < p.ids.size(); ++j) {
         out[2 * p.ids[j]] = c->h_out[s][2 * j];
         out[2 * p.ids[j] + 1] = c->h_out[s][2 * j + 1];
     }
-    if (counts)
-        for (size_t j = 0; j < p.ids.size(); ++j) {
-            counts[2 * p.ids[j]] = c->h_cnt[s][2 * j];
-            counts[2 * p.ids[j] + 1] = c->h_cnt[s][2 * j + 1];
-        }
     p.busy = false;
-    if (sink) {
-        // hand the slot to the consumer pool; the caller refills it only after join_consumer()
-        if (!c->wpool) c->wpool = new oxh::Pool(c->pool->size());
-        p.consumer = std::thread([c, s, sink, status, ids = std::move(p.ids)] {
-            const uint64_t M = c->max_items;
-            const size_t cnt = ids.size();
-            const int ntasks = (int)std::min<size_t>(cnt, (size_t)c->wpool->size() * 4);
-            c->wpool->parallel_for(ntasks, [&](int t) {
-                for (size_t j = (size_t)t; j < cnt; j += (size_t)ntasks) {
-                    const uint64_t id = ids[j];
-                    if (status && status[id] != OXH_OK) continue;
-                    (*sink)(id, c->h_stage[s] + c->h_desc[s][j], c->h_desc[s][M + j], c->h_out[s][2 * j],
-                            c->h_out[s][2 * j + 1]);
-                }
-            });
-        });
-    }
     p.ids.clear();
     return OXH_OK;
 }
@@ -614,42 +582,26 @@ int oxh_combined_hash_device(const uint64_t* d_content, const uint64_t* d_metada
     return OXH_OK;
 }
 
-// Shared packer for host-resident items: item i's bytes come from `src(i)` (a pointer) or are read by
-// `reader(i, dst)` directly into the pinned slot; lens[i] is known up front.
+// Host-resident buffers (oxh_hash_buffers / oxh_hash_streams): item i (lens[i] bytes) is copied by
+// copy(i, dst) straight into a pinned slot; slots are packed greedily in order, hashed on the GPU
+// while the next one fills, and items larger than a slot go through the oversize path.
 static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
-                           const std::function<int(uint64_t, uint8_t*)>& fill, uint64_t* out, int32_t* status,
-                           bool short_only_lane, Trace* tr = nullptr, uint64_t* counts = nullptr,
-                           const ItemSink* sink = nullptr) {
-    Trace local;
-    if (!tr) tr = &local;
+                           const std::function<void(uint64_t, uint8_t*)>& copy, uint64_t* out, bool short_only_lane) {
+    Trace tr;
     Pending pend[NSLOT];
     int slot = 0;
     uint64_t i = 0;
     std::vector<uint64_t> batch;
     while (i < n) {
-        // gather the next batch (greedy, in order), routing oversize items individually
         batch.clear();
         uint64_t bytes = 0;
         while (i < n && batch.size() < c->max_items) {
             const uint64_t L = lens[i];
             if (L > c->stage_bytes) {
                 if (!batch.empty()) break;
-                // oversize item: read it fully into a host buffer, then stream through slot 0
-                for (int s = 0; s < NSLOT; ++s) {
-                    int rc = drain_slot(c, s, pend[s], out, counts, sink, status);
-                    if (rc) return rc;
-                    join_consumer(pend[s]);
-                }
                 std::vector<uint8_t> tmp(L);
-                int st = fill(i, tmp.data());
-                if (status) status[i] = st;
-                if (st == OXH_OK) {
-                    int rc = oversize_item(c, tmp.data(), L, out + 2 * i, counts ? counts + 2 * i : nullptr);
-                    if (rc) return rc;
-                    if (sink) (*sink)(i, tmp.data(), L, out[2 * i], out[2 * i + 1]);
-                } else {
-                    out[2 * i] = out[2 * i + 1] = 0;
-                }
+                copy(i, tmp.data());
+                if (int rc = oversize_item(c, tmp.data(), L, out + 2 * i)) return rc;
                 ++i;
                 continue;
             }
@@ -661,13 +613,10 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
         if (batch.empty()) continue;
         const int s = slot;
         slot = (slot + 1) % NSLOT;
-        double t0 = Trace::now();
-        int rc = drain_slot(c, s, pend[s], out, counts, sink, status);
-        join_consumer(pend[s]);  // this slot's previous bytes were consumed before it is refilled
-        if (rc) return rc;
-        double t1 = Trace::now();
-        tr->drain += t1 - t0;
-        // lay out the slot
+        const double t0 = Trace::now();
+        if (int rc = drain_slot(c, s, pend[s], out)) return rc;  // the slot's previous batch
+        const double t1 = Trace::now();
+        tr.drain += t1 - t0;
         const uint64_t M = c->max_items;
         uint64_t* hoff = c->h_desc[s];
         uint64_t* hlen = c->h_desc[s] + M;
@@ -680,53 +629,29 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
             if (hlen[j] > 240) all_short = false;
             off += hlen[j];
         }
-        // fill it: parallel readers / copiers write straight into pinned memory
         STEP("fill s=%d items=%zu", s, batch.size());
-        std::vector<int32_t> st(batch.size(), OXH_OK);
         const int ntasks = (int)std::min<size_t>(batch.size(), (size_t)c->pool->size() * 4);
         c->pool->parallel_for(ntasks, [&](int t) {
-            for (size_t j = (size_t)t; j < batch.size(); j += (size_t)ntasks)
-                st[j] = fill(batch[j], c->h_stage[s] + hoff[j]);
+            for (size_t j = (size_t)t; j < batch.size(); j += (size_t)ntasks) copy(batch[j], c->h_stage[s] + hoff[j]);
         });
-        for (size_t j = 0; j < batch.size(); ++j) {
-            if (status) status[batch[j]] = st[j];
-            if (st[j] != OXH_OK) hlen[j] = 0;  // keep the batch alive; digest is zeroed below
-        }
-        double t2 = Trace::now();
-        tr->fill += t2 - t1;
-        rc = submit_slot(c, s, off, batch.size(), short_only_lane && all_short,
-                         off / std::max<uint64_t>(1, batch.size()) <= kShortItemBytes, counts != nullptr);
-        if (rc) return rc;
-        tr->submit += Trace::now() - t2;
-        tr->batches++;
+        const double t2 = Trace::now();
+        tr.fill += t2 - t1;
+        if (int rc = submit_slot(c, s, off, batch.size(), short_only_lane && all_short,
+                                 off / std::max<uint64_t>(1, batch.size()) <= kShortItemBytes, false))
+            return rc;
+        tr.submit += Trace::now() - t2;
+        tr.batches++;
         pend[s].busy = true;
         pend[s].ids = batch;
-        if (sink) {
-            // publish the previous slot while the next one fills: its digests are due now
-            const int prev = (s + NSLOT - 1) % NSLOT;
-            const double t4 = Trace::now();
-            rc = drain_slot(c, prev, pend[prev], out, counts, sink, status);
-            tr->drain += Trace::now() - t4;
-            if (rc) return rc;
-        }
     }
-    double t3 = Trace::now();
+    const double t3 = Trace::now();
     STEP("final drain");
-    for (int s = 0; s < NSLOT; ++s) {
-        int rc = drain_slot(c, s, pend[s], out, counts, sink, status);
-        if (rc) return rc;
-    }
-    for (int s = 0; s < NSLOT; ++s) join_consumer(pend[s]);
-    tr->drain += Trace::now() - t3;
-    if (tr->on)
-        fprintf(stderr, "[oxh] items=%llu batches=%d stat=%.3fs fill=%.3fs drain-wait=%.3fs submit=%.3fs threads=%d\n",
-                (unsigned long long)n, tr->batches, tr->stat, tr->fill, tr->drain, tr->submit, c->pool->size());
-    if (status)
-        for (uint64_t k = 0; k < n; ++k)
-            if (status[k] != OXH_OK) {
-                out[2 * k] = out[2 * k + 1] = 0;
-                if (counts) counts[2 * k] = counts[2 * k + 1] = 0;
-            }
+    for (int s = 0; s < NSLOT; ++s)
+        if (int rc = drain_slot(c, s, pend[s], out)) return rc;
+    tr.drain += Trace::now() - t3;
+    if (tr.on)
+        fprintf(stderr, "[oxh] items=%llu batches=%d fill=%.3fs drain-wait=%.3fs submit=%.3fs threads=%d\n",
+                (unsigned long long)n, tr.batches, tr.fill, tr.drain, tr.submit, c->pool->size());
     return OXH_OK;
 }
 
@@ -736,8 +661,7 @@ int oxh_hash_buffers(oxh_ctx* c, const uint8_t* const* bufs, const uint64_t* len
     HIP_TRY(hipSetDevice(c->device));
     return hash_host_items(c, n, lens, [&](uint64_t i, uint8_t* dst) {
         if (lens[i]) memcpy(dst, bufs[i], lens[i]);
-        return OXH_OK;
-    }, out, nullptr, false);
+    }, out, false);
 }
 
 int oxh_hash_streams(oxh_ctx* c, const uint8_t* streams, const uint64_t* offsets, const uint64_t* lens, uint64_t n,
@@ -749,8 +673,7 @@ int oxh_hash_streams(oxh_ctx* c, const uint8_t* streams, const uint64_t* offsets
     STEP("hash_streams locked");
     return hash_host_items(c, n, lens, [&](uint64_t i, uint8_t* dst) {
         if (lens[i]) memcpy(dst, streams + offsets[i], lens[i]);
-        return OXH_OK;
-    }, out, nullptr, true);
+    }, out, true);
 }
 
 // ---------------------------------------------------------------- streaming file engine
