@@ -220,3 +220,15 @@ def test_fastcdc_small_sections(cuda, oracle_lib, monkeypatch, section, cfg, war
     files = [rng.integers(0, 256, s, dtype=np.uint8) for s in (5, 4097, 65_537, 300_001)]
     files += [text.copy(), np.full(70_000, 9, dtype=np.uint8), rng.integers(0, 3, 100_000, dtype=np.uint8)]
     _check(cuda, oracle_lib, files, *cfg)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("avg", [8192, 65536])
+def test_fastcdc_many_default_sections(cuda, oracle_lib, avg):
+    """Default section / warm-up sizing (sections >= 512 KiB or 8 max chunks, warm-up >= 128 KiB) over
+    files spanning many sections: random, text-like and a misaligned start, C5's min/avg/max shape."""
+    rng = np.random.default_rng(avg)
+    text = np.frombuffer(b"".join(b"row %d,label %d\n" % (i, i % 7) for i in range(600_000)), dtype=np.uint8)
+    files = [rng.integers(0, 256, 12_345_679, dtype=np.uint8), text[:9_000_001].copy(),
+             rng.integers(0, 256, 3 * (1 << 20) + 5, dtype=np.uint8)]
+    assert _check(cuda, oracle_lib, files, 4096, avg, 2 * avg) > 0
