@@ -44,6 +44,8 @@ def lib():
         L.oxo_xxh3_128_batch.restype = None
         L.oxo_hash_files.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_uint64, _u64p, _u64p, _i32p, ctypes.c_int]
         L.oxo_hash_files.restype = None
+        L.oxo_hash_files_stream4k.argtypes = L.oxo_hash_files.argtypes
+        L.oxo_hash_files_stream4k.restype = None
         L.oxo_add_files.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_uint64, ctypes.c_char_p, _u64p, _u64p,
                                     _i32p, _i32p, ctypes.c_int]
         L.oxo_add_files.restype = None

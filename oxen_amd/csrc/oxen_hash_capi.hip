@@ -228,6 +228,13 @@ struct oxh_ctx {
     bool stop = false;
     std::thread engine;
     uint64_t flush_bytes = 0;  // seal a partly filled slot at this many bytes when the next slot is free
+    // files larger than a staging slot (see big_file): a device buffer kept at the largest size seen
+    // and two pinned bounce buffers the file is read into in pieces
+    uint8_t* d_big = nullptr;
+    uint64_t d_big_size = 0;
+    uint8_t* h_bounce[2] = {};
+    hipEvent_t ev_bounce[2] = {};
+    bool bounce_used[2] = {};
     std::vector<struct FileRequest*> rq[NSLOT];  // per staged item: its request and index in it
     std::vector<uint64_t> loc[NSLOT];
     hipEvent_t ev_copied[NSLOT] = {}, ev_done[NSLOT] = {};
@@ -395,14 +402,10 @@ int drain_slot(oxh_ctx* c, int s, Pending& p, uint64_t* out) {
     return OXH_OK;
 }
 
-// Hash one oversize host item (> a staging slot) through a device buffer of its own (the staging
-// slots may belong to a live pipeline); with `cnt2`, also its text counts (num_lines, num_chars),
-// with `utf8_1` its is_utf8 sniff.
-int oversize_item(oxh_ctx* c, const uint8_t* src, uint64_t len, uint64_t* out2, uint64_t* cnt2 = nullptr,
-                  int32_t* utf8_1 = nullptr) {
+// Digest (+ text counts, + is_utf8) of one buffer already on the device (stream-ordered on
+// c->stream): d holds align_up(len) + 256 bytes, the tail is the results area. Synchronises c->stream.
+int device_item(oxh_ctx* c, uint8_t* d, uint64_t len, uint64_t* out2, uint64_t* cnt2, int32_t* utf8_1) {
     const uint64_t tail = align_up(len);
-    uint8_t* d = nullptr;
-    if (hipMalloc(&d, tail + 256) != hipSuccess) return fail(OXH_ERR_NOMEM, "oversize hipMalloc failed");
     struct Res {  // mirrored at d + tail: digest, text counts, a one-item descriptor, is_utf8
         uint64_t out[2], cnt[2], off, len;
         int32_t utf8, pad;
@@ -414,8 +417,7 @@ int oversize_item(oxh_ctx* c, const uint8_t* src, uint64_t len, uint64_t* out2, 
         if (rc == OXH_OK && e != hipSuccess) rc = fail(OXH_ERR_HIP, what);
         return rc == OXH_OK;
     };
-    ok(hipMemcpyAsync(d, src, len, hipMemcpyHostToDevice, c->stream), "oversize H2D failed");
-    ok(hipMemcpyAsync(d_res, &h, sizeof h, hipMemcpyHostToDevice, c->stream), "oversize descriptor H2D failed");
+    ok(hipMemcpyAsync(d_res, &h, sizeof h, hipMemcpyHostToDevice, c->stream), "results area H2D failed");
     if (rc == OXH_OK) rc = large_device(c, d, len, d_res, c->stream);
     if (rc == OXH_OK && cnt2) {
         hipLaunchKernelGGL(oxh::text_count_kernel, dim3(2048), dim3(256), 0, c->stream, d, len,
@@ -427,8 +429,8 @@ int oversize_item(oxh_ctx* c, const uint8_t* src, uint64_t len, uint64_t* out2, 
                            (int32_t*)(d_res + 6));
         ok(hipGetLastError(), "utf8_prefix_kernel launch");
     }
-    ok(hipMemcpyAsync(&h, d_res, sizeof h, hipMemcpyDeviceToHost, c->stream), "oversize D2H failed");
-    ok(hipStreamSynchronize(c->stream), "oversize sync failed");
+    ok(hipMemcpyAsync(&h, d_res, sizeof h, hipMemcpyDeviceToHost, c->stream), "results D2H failed");
+    ok(hipStreamSynchronize(c->stream), "sync failed");
     if (rc == OXH_OK) {
         out2[0] = h.out[0];
         out2[1] = h.out[1];
@@ -438,6 +440,19 @@ int oversize_item(oxh_ctx* c, const uint8_t* src, uint64_t len, uint64_t* out2, 
         }
         if (utf8_1) *utf8_1 = h.utf8;
     }
+    return rc;
+}
+
+// Hash one oversize host item (> a staging slot) through a device buffer of its own (the staging
+// slots may belong to a live pipeline); with `cnt2`, also its text counts (num_lines, num_chars),
+// with `utf8_1` its is_utf8 sniff.
+int oversize_item(oxh_ctx* c, const uint8_t* src, uint64_t len, uint64_t* out2, uint64_t* cnt2 = nullptr,
+                  int32_t* utf8_1 = nullptr) {
+    uint8_t* d = nullptr;
+    if (hipMalloc(&d, align_up(len) + 256) != hipSuccess) return fail(OXH_ERR_NOMEM, "oversize hipMalloc failed");
+    int rc = OXH_OK;
+    if (hipMemcpyAsync(d, src, len, hipMemcpyHostToDevice, c->stream) != hipSuccess) rc = fail(OXH_ERR_HIP, "oversize H2D failed");
+    if (rc == OXH_OK) rc = device_item(c, d, len, out2, cnt2, utf8_1);
     (void)hipFree(d);
     return rc;
 }
@@ -525,6 +540,11 @@ int oxh_ctx_destroy(oxh_ctx* c) {
         if (c->d_utf8[s]) (void)hipFree(c->d_utf8[s]);
         if (c->ev_copied[s]) (void)hipEventDestroy(c->ev_copied[s]);
         if (c->ev_done[s]) (void)hipEventDestroy(c->ev_done[s]);
+    }
+    if (c->d_big) (void)hipFree(c->d_big);
+    for (int b = 0; b < 2; ++b) {
+        if (c->h_bounce[b]) (void)hipHostFree(c->h_bounce[b]);
+        if (c->ev_bounce[b]) (void)hipEventDestroy(c->ev_bounce[b]);
     }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -983,8 +1003,77 @@ void drain_files(FileStream& fs, int s, const SlotRun& p) {
 }
 
 // One file read through the oversize path (files larger than a staging slot, K1L).
+// A file larger than a staging slot (the reference's streaming branch, hasher.rs:150-174): read in
+// 64 MiB pieces by the context's worker pool (parallel preads of 4 MiB each) into two pinned bounce
+// buffers, each piece copied to the device on the copy stream while the next one is read, into a
+// device buffer kept at the largest size seen; then K1L (+ text counts, + is_utf8) on the device.
+constexpr uint64_t kBigPiece = 64ull << 20, kBigRead = 4ull << 20;
+
+int big_file(FileStream& fs, FileRequest* r, uint64_t i) {
+    oxh_ctx* c = fs.c;
+    const uint64_t L = r->lens[i];
+    const uint64_t need = align_up(L) + 256;
+    if (c->d_big_size < need) {
+        if (c->d_big) {
+            HIP_TRY(hipDeviceSynchronize());
+            (void)hipFree(c->d_big);
+            c->d_big = nullptr;
+            c->d_big_size = 0;
+        }
+        if (hipMalloc(&c->d_big, need) != hipSuccess) return fail(OXH_ERR_NOMEM, "large-file device buffer");
+        c->d_big_size = need;
+    }
+    for (int b = 0; b < 2; ++b) {
+        if (!c->h_bounce[b] && hipHostMalloc(&c->h_bounce[b], kBigPiece, hipHostMallocDefault) != hipSuccess)
+            return fail(OXH_ERR_NOMEM, "large-file bounce buffer");
+        if (!c->ev_bounce[b]) HIP_TRY(hipEventCreateWithFlags(&c->ev_bounce[b], hipEventDisableTiming));
+    }
+    const int fd = open(r->paths[i], O_RDONLY | O_CLOEXEC | O_NONBLOCK);
+    bool io_ok = fd >= 0;
+    for (uint64_t off = 0, k = 0; io_ok && off < L; off += kBigPiece, ++k) {
+        const int b = (int)(k & 1);
+        if (c->bounce_used[b]) HIP_TRY(hipEventSynchronize(c->ev_bounce[b]));  // its last H2D is done
+        const uint64_t piece = std::min(kBigPiece, L - off);
+        const int parts = (int)((piece + kBigRead - 1) / kBigRead);
+        std::atomic<bool> bad{false};
+        c->pool->parallel_for(parts, [&](int t) {
+            const uint64_t lo = (uint64_t)t * kBigRead, hi = std::min(piece, lo + kBigRead);
+            for (uint64_t got = lo; got < hi;) {
+                const ssize_t n = pread(fd, c->h_bounce[b] + got, hi - got, (off_t)(off + got));
+                if (n <= 0) {
+                    bad.store(true);
+                    return;
+                }
+                got += (uint64_t)n;
+            }
+        });
+        if (bad.load()) {
+            io_ok = false;
+            break;
+        }
+        HIP_TRY(hipMemcpyAsync(c->d_big + off, c->h_bounce[b], piece, hipMemcpyHostToDevice, c->copy_stream));
+        HIP_TRY(hipEventRecord(c->ev_bounce[b], c->copy_stream));
+        c->bounce_used[b] = true;
+    }
+    if (fd >= 0) close(fd);
+    HIP_TRY(hipStreamSynchronize(c->copy_stream));  // every piece is on the device (or we stopped)
+    if (!io_ok) {
+        r->st[i] = OXH_ERR_IO;
+    } else {
+        int32_t u8 = 0;
+        if (int rc = device_item(c, c->d_big, L, r->out + 2 * i, r->counts ? r->counts + 2 * i : nullptr,
+                                 r->utf8 ? &u8 : nullptr))
+            return rc;
+        if (r->utf8) r->utf8[i] = u8;
+    }
+    account(fs, r, 1);
+    return OXH_OK;
+}
+
+// Oversize file of a request with a sink (fused add): the sink needs the whole file in host memory.
 int oversize_file(FileStream& fs, FileRequest* r, uint64_t i) {
     oxh_ctx* c = fs.c;
+    if (!r->sink) return big_file(fs, r, i);
     const uint64_t L = r->lens[i];
     std::vector<uint8_t> tmp(L);
     const int fd = open(r->paths[i], O_RDONLY | O_CLOEXEC | O_NONBLOCK);

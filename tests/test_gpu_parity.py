@@ -679,3 +679,33 @@ def test_concurrent_mixed_requests_join_live_run(oracle_lib, tmp_path, cuda):
                     assert u8[:48] == want_utf8[lo:lo + 48], t
                 if t % 5 == 4:
                     assert st[48] != 0 and d[48] is None
+
+
+def test_big_file_streamed_pieces(oracle_lib, tmp_path, cuda):
+    """Files above a staging slot stream through the large-file path in 64 MiB pieces (parallel
+    preads into two pinned bounce buffers, H2D, K1L on the device): several pieces, a ragged last
+    piece, an exact multiple, digests + text counts + is_utf8 against the oracle / numpy, and the
+    sink (fused add) variant that keeps the whole file on the host."""
+    from oracle import oracle
+    from oxen_amd import _capi, hasher
+    from oxen_amd.workloads import splitmix_bytes
+
+    sizes = [(150 << 20) + 17, 64 << 20, (5 << 20) + 3]
+    blobs = [splitmix_bytes(300 + k, 0, s).tobytes() for k, s in enumerate(sizes)]
+    paths = []
+    for k, b in enumerate(blobs):
+        p = tmp_path / f"big{k}.bin"
+        p.write_bytes(b)
+        paths.append(str(p))
+    want = [oracle.xxh3_128_int(b) for b in blobs]
+    arrs = [np.frombuffer(b, dtype=np.uint8) for b in blobs]
+    want_counts = [(1 + int(np.count_nonzero(a == 10)), len(a) - int(np.count_nonzero((a & 0xC0) == 0x80))) for a in arrs]
+    want_utf8 = [oracle.is_utf8_prefix(b[:4096]) for b in blobs]
+    with _capi.Context(0, staging_bytes=4 << 20) as c:
+        d, sz, st = hasher.hash_files_128bit(paths, c)
+        assert st == [0, 0, 0] and sz == sizes and d == want
+        d, sz, st, meta, u8 = hasher.hash_files_text_utf8_128bit(paths, c)
+        assert d == want and u8 == want_utf8
+        assert [(m["text"]["num_lines"], m["text"]["num_chars"]) for m in meta] == want_counts
+        d, sz, st, stored = hasher.add_files(paths, str(tmp_path / "store"), c)
+        assert d == want and all(s == 0 for s in st) and all(stored)
