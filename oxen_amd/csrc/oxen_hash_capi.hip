@@ -17,6 +17,7 @@
 #include <stdint.h>
 #include <string.h>
 #include <sys/resource.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -1003,10 +1004,11 @@ void drain_files(FileStream& fs, int s, const SlotRun& p) {
 }
 
 // One file read through the oversize path (files larger than a staging slot, K1L).
-// A file larger than a staging slot (the reference's streaming branch, hasher.rs:150-174): read in
-// 64 MiB pieces by the context's worker pool (parallel preads of 4 MiB each) into two pinned bounce
-// buffers, each piece copied to the device on the copy stream while the next one is read, into a
-// device buffer kept at the largest size seen; then K1L (+ text counts, + is_utf8) on the device.
+// A file larger than a staging slot (the reference's streaming branch, hasher.rs:150-174) lands in
+// a device buffer kept at the largest size seen -- straight from the page cache when its pages can
+// be pinned, else in 64 MiB pieces read by the context's worker pool (parallel preads of 4 MiB) into
+// two pinned bounce buffers, each piece's H2D overlapping the next piece's reads -- and is hashed
+// there by K1L (+ text counts, + is_utf8).
 constexpr uint64_t kBigPiece = 64ull << 20, kBigRead = 4ull << 20;
 
 int big_file(FileStream& fs, FileRequest* r, uint64_t i) {
@@ -1030,6 +1032,34 @@ int big_file(FileStream& fs, FileRequest* r, uint64_t i) {
     }
     const int fd = open(r->paths[i], O_RDONLY | O_CLOEXEC | O_NONBLOCK);
     bool io_ok = fd >= 0;
+    // Copy-free first: map the file and pin its page-cache pages for the DMA engine (~9 ms per
+    // 4 GiB), which then reads them at the PCIe rate (46-57 GB/s, tools/mmap_register_probe.hip)
+    // with no CPU copy. Any failure (a file system that cannot be pinned, an I/O error while
+    // faulting pages in) falls through to the bounce-buffer path, which reports I/O errors.
+    if (io_ok && L > 0) {
+        void* m = mmap(nullptr, L, PROT_READ, MAP_SHARED, fd, 0);
+        if (m != MAP_FAILED) {
+            (void)madvise(m, L, MADV_SEQUENTIAL);
+            bool copied = false;
+            if (hipHostRegister(m, L, hipHostRegisterReadOnly) == hipSuccess) {
+                copied = hipMemcpyAsync(c->d_big, m, L, hipMemcpyHostToDevice, c->copy_stream) == hipSuccess &&
+                         hipStreamSynchronize(c->copy_stream) == hipSuccess;
+                (void)hipHostUnregister(m);
+            }
+            munmap(m, L);
+            if (copied) {
+                close(fd);
+                int32_t u8 = 0;
+                if (int rc = device_item(c, c->d_big, L, r->out + 2 * i, r->counts ? r->counts + 2 * i : nullptr,
+                                         r->utf8 ? &u8 : nullptr))
+                    return rc;
+                if (r->utf8) r->utf8[i] = u8;
+                account(fs, r, 1);
+                return OXH_OK;
+            }
+            (void)hipGetLastError();  // clear a failed registration / copy before the fallback
+        }
+    }
     for (uint64_t off = 0, k = 0; io_ok && off < L; off += kBigPiece, ++k) {
         const int b = (int)(k & 1);
         if (c->bounce_used[b]) HIP_TRY(hipEventSynchronize(c->ev_bounce[b]));  // its last H2D is done
