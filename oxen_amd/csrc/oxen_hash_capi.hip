@@ -236,6 +236,7 @@ struct oxh_ctx {
     uint8_t* h_bounce[2] = {};
     hipEvent_t ev_bounce[2] = {};
     bool bounce_used[2] = {};
+    hipEvent_t ev_piece_free[2] = {};
     std::vector<struct FileRequest*> rq[NSLOT];  // per staged item: its request and index in it
     std::vector<uint64_t> loc[NSLOT];
     hipEvent_t ev_copied[NSLOT] = {}, ev_done[NSLOT] = {};
@@ -546,6 +547,7 @@ int oxh_ctx_destroy(oxh_ctx* c) {
     for (int b = 0; b < 2; ++b) {
         if (c->h_bounce[b]) (void)hipHostFree(c->h_bounce[b]);
         if (c->ev_bounce[b]) (void)hipEventDestroy(c->ev_bounce[b]);
+        if (c->ev_piece_free[b]) (void)hipEventDestroy(c->ev_piece_free[b]);
     }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -1004,97 +1006,151 @@ void drain_files(FileStream& fs, int s, const SlotRun& p) {
 }
 
 // One file read through the oversize path (files larger than a staging slot, K1L).
-// A file larger than a staging slot (the reference's streaming branch, hasher.rs:150-174) lands in
-// a device buffer kept at the largest size seen -- straight from the page cache when its pages can
-// be pinned, else in 64 MiB pieces read by the context's worker pool (parallel preads of 4 MiB) into
-// two pinned bounce buffers, each piece's H2D overlapping the next piece's reads -- and is hashed
-// there by K1L (+ text counts, + is_utf8).
-constexpr uint64_t kBigPiece = 64ull << 20, kBigRead = 4ull << 20;
+// A file larger than a staging slot (the reference's streaming branch, hasher.rs:150-174) is hashed
+// in device pieces of OXH_BIG_PIECE_MIB (default 1 GiB) through two piece buffers, so device memory
+// stays bounded whatever the file size and piece j+1's transfer overlaps piece j's K1L chain: each
+// piece's block sums are computed chip-wide and the serial chain continues from the previous piece's
+// accumulators (ChainJob kChainResume / kChainPartial); the last piece (> 1 KiB) takes the tail and
+// the merge. A piece reaches the device copy-free when the file's page-cache pages can be pinned
+// (mmap + hipHostRegister read-only, ~2 ms per GiB; the DMA engine then reads them at 46-57 GB/s,
+// tools/mmap_register_probe.hip), else through two pinned bounce buffers filled by the worker pool
+// (parallel 4 MiB preads, 64 MiB at a time). Text counts accumulate over the pieces; is_utf8 reads
+// the first 4 KiB of piece 0.
+constexpr uint64_t kBounce = 64ull << 20, kBigRead = 4ull << 20;
 
 int big_file(FileStream& fs, FileRequest* r, uint64_t i) {
     oxh_ctx* c = fs.c;
     const uint64_t L = r->lens[i];
-    const uint64_t need = align_up(L) + 256;
-    if (c->d_big_size < need) {
+    const uint64_t P = std::max<uint64_t>(
+        1, getenv("OXH_BIG_PIECE_MIB") ? strtoull(getenv("OXH_BIG_PIECE_MIB"), nullptr, 10) : 1024) << 20;
+    // pieces 0 .. k-1 hold P bytes each; the last one L - k*P bytes, in [1025, P + 1024]
+    const uint64_t k = L > P + 1024 ? (L - 1025) / P : 0;
+    const uint64_t cap = P + 1024;  // bytes per piece buffer
+    const uint64_t slot = align_up(cap) + 256;
+    if (c->d_big_size < 2 * slot + 4096) {
         if (c->d_big) {
             HIP_TRY(hipDeviceSynchronize());
             (void)hipFree(c->d_big);
             c->d_big = nullptr;
             c->d_big_size = 0;
         }
-        if (hipMalloc(&c->d_big, need) != hipSuccess) return fail(OXH_ERR_NOMEM, "large-file device buffer");
-        c->d_big_size = need;
+        if (hipMalloc(&c->d_big, 2 * slot + 4096) != hipSuccess) return fail(OXH_ERR_NOMEM, "large-file device buffers");
+        c->d_big_size = 2 * slot + 4096;
     }
+    uint8_t* dbuf[2] = {c->d_big, c->d_big + slot};
+    // results area: [digest 2 | counts 2 | desc off, len | utf8 | state 8]
+    uint64_t* d_res = reinterpret_cast<uint64_t*>(c->d_big + 2 * slot);
+    struct Res {
+        uint64_t out[2], cnt[2], off, len;
+        int32_t utf8, pad;
+    } h{};
+    h.len = L;
     for (int b = 0; b < 2; ++b) {
-        if (!c->h_bounce[b] && hipHostMalloc(&c->h_bounce[b], kBigPiece, hipHostMallocDefault) != hipSuccess)
+        if (!c->h_bounce[b] && hipHostMalloc(&c->h_bounce[b], kBounce, hipHostMallocDefault) != hipSuccess)
             return fail(OXH_ERR_NOMEM, "large-file bounce buffer");
         if (!c->ev_bounce[b]) HIP_TRY(hipEventCreateWithFlags(&c->ev_bounce[b], hipEventDisableTiming));
+        if (!c->ev_piece_free[b]) HIP_TRY(hipEventCreateWithFlags(&c->ev_piece_free[b], hipEventDisableTiming));
     }
+    uint64_t* sums = nullptr;
+    oxh::ScratchLease lease(c->stream);  // block sums of the two pieces in flight
+    const uint64_t sums_per = (cap >> 10) * 8;
+    HIP_TRY(lease.get(2 * sums_per * 8, (void**)&sums));
+    HIP_TRY(hipMemcpyAsync(d_res, &h, sizeof h, hipMemcpyHostToDevice, c->stream));
+
+    int rc = OXH_OK;
+    bool io_ok = true, piece_used[2] = {false, false};
     const int fd = open(r->paths[i], O_RDONLY | O_CLOEXEC | O_NONBLOCK);
-    bool io_ok = fd >= 0;
-    // Copy-free first: map the file and pin its page-cache pages for the DMA engine (~9 ms per
-    // 4 GiB), which then reads them at the PCIe rate (46-57 GB/s, tools/mmap_register_probe.hip)
-    // with no CPU copy. Any failure (a file system that cannot be pinned, an I/O error while
-    // faulting pages in) falls through to the bounce-buffer path, which reports I/O errors.
-    if (io_ok && L > 0) {
+    if (fd < 0) io_ok = false;
+    uint8_t* map = nullptr;
+    if (io_ok) {
         void* m = mmap(nullptr, L, PROT_READ, MAP_SHARED, fd, 0);
         if (m != MAP_FAILED) {
+            map = (uint8_t*)m;
             (void)madvise(m, L, MADV_SEQUENTIAL);
-            bool copied = false;
-            if (hipHostRegister(m, L, hipHostRegisterReadOnly) == hipSuccess) {
-                copied = hipMemcpyAsync(c->d_big, m, L, hipMemcpyHostToDevice, c->copy_stream) == hipSuccess &&
-                         hipStreamSynchronize(c->copy_stream) == hipSuccess;
-                (void)hipHostUnregister(m);
-            }
-            munmap(m, L);
-            if (copied) {
-                close(fd);
-                int32_t u8 = 0;
-                if (int rc = device_item(c, c->d_big, L, r->out + 2 * i, r->counts ? r->counts + 2 * i : nullptr,
-                                         r->utf8 ? &u8 : nullptr))
-                    return rc;
-                if (r->utf8) r->utf8[i] = u8;
-                account(fs, r, 1);
-                return OXH_OK;
-            }
-            (void)hipGetLastError();  // clear a failed registration / copy before the fallback
         }
     }
-    for (uint64_t off = 0, k = 0; io_ok && off < L; off += kBigPiece, ++k) {
-        const int b = (int)(k & 1);
-        if (c->bounce_used[b]) HIP_TRY(hipEventSynchronize(c->ev_bounce[b]));  // its last H2D is done
-        const uint64_t piece = std::min(kBigPiece, L - off);
-        const int parts = (int)((piece + kBigRead - 1) / kBigRead);
-        std::atomic<bool> bad{false};
-        c->pool->parallel_for(parts, [&](int t) {
-            const uint64_t lo = (uint64_t)t * kBigRead, hi = std::min(piece, lo + kBigRead);
-            for (uint64_t got = lo; got < hi;) {
-                const ssize_t n = pread(fd, c->h_bounce[b] + got, hi - got, (off_t)(off + got));
-                if (n <= 0) {
-                    bad.store(true);
-                    return;
+    // piece j of the file -> dbuf[b] on the copy stream; false on an I/O error
+    auto copy_piece = [&](uint64_t off, uint64_t plen, int b) -> bool {
+        if (map && hipHostRegister(map + off, plen, hipHostRegisterReadOnly) == hipSuccess) {
+            const bool ok = hipMemcpyAsync(dbuf[b], map + off, plen, hipMemcpyHostToDevice, c->copy_stream) == hipSuccess &&
+                            hipStreamSynchronize(c->copy_stream) == hipSuccess;
+            (void)hipHostUnregister(map + off);
+            if (ok) return true;
+        }
+        (void)hipGetLastError();
+        for (uint64_t o = 0, q = 0; o < plen; o += kBounce, ++q) {  // bounce-buffer path
+            const int bb = (int)(q & 1);
+            if (c->bounce_used[bb] && hipEventSynchronize(c->ev_bounce[bb]) != hipSuccess) return false;
+            const uint64_t n = std::min(kBounce, plen - o);
+            const int parts = (int)((n + kBigRead - 1) / kBigRead);
+            std::atomic<bool> bad{false};
+            c->pool->parallel_for(parts, [&](int t) {
+                const uint64_t lo = (uint64_t)t * kBigRead, hi = std::min(n, lo + kBigRead);
+                for (uint64_t got = lo; got < hi;) {
+                    const ssize_t x = pread(fd, c->h_bounce[bb] + got, hi - got, (off_t)(off + o + got));
+                    if (x <= 0) {
+                        bad.store(true);
+                        return;
+                    }
+                    got += (uint64_t)x;
                 }
-                got += (uint64_t)n;
-            }
-        });
-        if (bad.load()) {
+            });
+            if (bad.load()) return false;
+            if (hipMemcpyAsync(dbuf[b] + o, c->h_bounce[bb], n, hipMemcpyHostToDevice, c->copy_stream) != hipSuccess ||
+                hipEventRecord(c->ev_bounce[bb], c->copy_stream) != hipSuccess)
+                return false;
+            c->bounce_used[bb] = true;
+        }
+        return hipStreamSynchronize(c->copy_stream) == hipSuccess;
+    };
+    for (uint64_t j = 0; j <= k && io_ok && rc == OXH_OK; ++j) {
+        const int b = (int)(j & 1);
+        const uint64_t off = j * P, plen = j < k ? P : L - off;
+        // the chain of piece j-2 (which read dbuf[b] and its block sums) is done
+        if (piece_used[b] && hipEventSynchronize(c->ev_piece_free[b]) != hipSuccess) {
+            rc = fail(OXH_ERR_HIP, "large-file piece wait");
+            break;
+        }
+        if (!copy_piece(off, plen, b)) {
             io_ok = false;
             break;
         }
-        HIP_TRY(hipMemcpyAsync(c->d_big + off, c->h_bounce[b], piece, hipMemcpyHostToDevice, c->copy_stream));
-        HIP_TRY(hipEventRecord(c->ev_bounce[b], c->copy_stream));
-        c->bounce_used[b] = true;
+        piece_used[b] = true;
+        uint64_t* s_b = sums + (uint64_t)b * sums_per;
+        const bool last = j == k;
+        const uint64_t nb = last ? (plen - 1) >> 10 : plen >> 10;
+        const uint64_t nwaves = (nb + 3) / 4, blocks = (nwaves + 3) / 4;
+        hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, c->stream, dbuf[b], nb, s_b);
+        if (r->counts) {
+            hipLaunchKernelGGL(oxh::text_count_kernel, dim3(2048), dim3(256), 0, c->stream, dbuf[b], plen,
+                               (unsigned long long*)(d_res + 2));
+        }
+        if (j == 0 && r->utf8) {
+            hipLaunchKernelGGL(oxh::utf8_prefix_kernel, dim3(1), dim3(64), 0, c->stream, dbuf[b], d_res + 4, d_res + 5,
+                               (uint64_t)1, (int32_t*)(d_res + 6));
+        }
+        oxh::ChainBatch batch;
+        batch.job[0] = {dbuf[b], plen, s_b, d_res, L, d_res + 7, (j > 0 ? oxh::kChainResume : 0u) | (last ? 0u : oxh::kChainPartial)};
+        hipLaunchKernelGGL(oxh::xxh3_chain_kernel, dim3(1), dim3(64), kChainLdsPad, c->stream, batch);
+        if (hipGetLastError() != hipSuccess || hipEventRecord(c->ev_piece_free[b], c->stream) != hipSuccess)
+            rc = fail(OXH_ERR_HIP, "large-file piece launch");
     }
+    if (map) munmap(map, L);
     if (fd >= 0) close(fd);
-    HIP_TRY(hipStreamSynchronize(c->copy_stream));  // every piece is on the device (or we stopped)
+    if (rc == OXH_OK && hipMemcpyAsync(&h, d_res, sizeof h, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+        rc = fail(OXH_ERR_HIP, "large-file results D2H");
+    if (hipStreamSynchronize(c->stream) != hipSuccess && rc == OXH_OK) rc = fail(OXH_ERR_HIP, "large-file sync");
+    if (rc) return rc;
     if (!io_ok) {
         r->st[i] = OXH_ERR_IO;
     } else {
-        int32_t u8 = 0;
-        if (int rc = device_item(c, c->d_big, L, r->out + 2 * i, r->counts ? r->counts + 2 * i : nullptr,
-                                 r->utf8 ? &u8 : nullptr))
-            return rc;
-        if (r->utf8) r->utf8[i] = u8;
+        r->out[2 * i] = h.out[0];
+        r->out[2 * i + 1] = h.out[1];
+        if (r->counts) {
+            r->counts[2 * i] = 1 + h.cnt[0];
+            r->counts[2 * i + 1] = L - h.cnt[1];
+        }
+        if (r->utf8) r->utf8[i] = h.utf8;
     }
     account(fs, r, 1);
     return OXH_OK;

@@ -81,11 +81,20 @@ __device__ __forceinline__ uint32_t ld32u(const uint8_t* p) { uint32_t v; __buil
 struct U128 { uint64_t lo, hi; };
 
 // K1L chain launch: one job (one large buffer) per wave, passed by value as kernel arguments.
+// One buffer's K1L chain. Whole-buffer jobs: total_len == len, state == nullptr, flags == 0.
+// A huge file is chained in pieces of whole 1 KiB blocks: every piece but the last has
+// kChainPartial set (all its len / 1024 blocks are scrambled, the 8 accumulators go to `state`),
+// every piece but the first has kChainResume (the accumulators come from `state`); the last piece
+// (len > 1024) takes the tail and merges with total_len.
+constexpr uint32_t kChainResume = 1, kChainPartial = 2;
 struct ChainJob {
     const uint8_t* p;
     uint64_t len;
     const uint64_t* sums;  // 8 u64 block sums per scrambled block
     uint64_t* out;         // 2 u64 (lo, hi)
+    uint64_t total_len = 0;
+    uint64_t* state = nullptr;
+    uint32_t flags = 0;
 };
 constexpr int kChainJobs = 32;
 struct ChainBatch {

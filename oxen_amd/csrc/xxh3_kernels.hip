@@ -519,14 +519,15 @@ __global__ __launch_bounds__(64) void xxh3_chain_kernel(ChainBatch batch) {
     const uint64_t* __restrict__ sums = job.sums;
     const int lane = threadIdx.x;
     const int i = lane & 7;
-    const uint64_t nb = (len - 1) >> 10;
+    const bool partial = (job.flags & kChainPartial) != 0;
+    const uint64_t nb = partial ? len >> 10 : (len - 1) >> 10;
     // The chain acc <- scramble(acc + S_b) is carried as x = acc + S_b in 32-bit halves so that the
     // critical path per step is shift -> xor -> v_mad_u64_u32 (which also adds S_{b+1}) -> add:
     //   y = x ^ (x >> 47) ^ key;  x' = y * P32_1 + S_{b+1}
     //   lo(x') = lo(yl * P + S), hi(x') = hi(yl * P + S) + yh * P   (yh * P off the critical path)
     const uint64_t sk = kSecW[16 + i];
     const uint32_t kl = (uint32_t)sk, kh = (uint32_t)(sk >> 32);
-    uint64_t acc = kInitW[i];
+    uint64_t acc = (job.flags & kChainResume) ? job.state[i] : kInitW[i];
     auto step = [&](uint32_t& xl, uint32_t& xh, uint64_t s_next) {
         uint32_t yl;  // one 3-input xor (bitop3 0x96) on the critical path; hipcc emits two xors
         asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(yl) : "v"(xl), "v"(kl), "v"(xh >> 15));
@@ -598,6 +599,10 @@ __global__ __launch_bounds__(64) void xxh3_chain_kernel(ChainBatch batch) {
         step(xl, xh, 0);  // the last full block's scramble
         acc = ((uint64_t)xh << 32) | xl;
     }
+    if (partial) {  // a piece of a huge file: hand the accumulators to the next piece
+        if (lane < 8) job.state[i] = acc;
+        return;
+    }
     // partial block stripes + last stripe: lane i owns accumulator i here (scalar per lane)
     const uint64_t ns = ((len - 1) - (nb << 10)) >> 6;
     const uint8_t* pb = p + (nb << 10);
@@ -631,8 +636,9 @@ __global__ __launch_bounds__(64) void xxh3_chain_kernel(ChainBatch batch) {
         mhi += oh;
     }
     if (lane == 0) {
-        job.out[0] = avalanche_xxh3(len * P64_1 + mlo);
-        job.out[1] = avalanche_xxh3(~(len * P64_2) + mhi);
+        const uint64_t tl = job.total_len ? job.total_len : len;  // the whole file's length
+        job.out[0] = avalanche_xxh3(tl * P64_1 + mlo);
+        job.out[1] = avalanche_xxh3(~(tl * P64_2) + mhi);
     }
 }
 

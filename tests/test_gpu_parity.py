@@ -681,7 +681,8 @@ def test_concurrent_mixed_requests_join_live_run(oracle_lib, tmp_path, cuda):
                     assert st[48] != 0 and d[48] is None
 
 
-def test_big_file_streamed_pieces(oracle_lib, tmp_path, cuda):
+@pytest.mark.parametrize("piece_mib", [None, "32"], ids=["one-piece", "32MiB-pieces"])
+def test_big_file_streamed_pieces(oracle_lib, tmp_path, cuda, monkeypatch, piece_mib):
     """Files above a staging slot stream through the large-file path in 64 MiB pieces (parallel
     preads into two pinned bounce buffers, H2D, K1L on the device): several pieces, a ragged last
     piece, an exact multiple, digests + text counts + is_utf8 against the oracle / numpy, and the
@@ -690,7 +691,9 @@ def test_big_file_streamed_pieces(oracle_lib, tmp_path, cuda):
     from oxen_amd import _capi, hasher
     from oxen_amd.workloads import splitmix_bytes
 
-    sizes = [(150 << 20) + 17, 64 << 20, (5 << 20) + 3]
+    if piece_mib:  # device pieces of 32 MiB: resumed chains, a last piece of 32 MiB + 10 B
+        monkeypatch.setenv("OXH_BIG_PIECE_MIB", piece_mib)
+    sizes = [(150 << 20) + 17, 64 << 20, (5 << 20) + 3, (64 << 20) + 10]
     blobs = [splitmix_bytes(300 + k, 0, s).tobytes() for k, s in enumerate(sizes)]
     paths = []
     for k, b in enumerate(blobs):
@@ -703,7 +706,7 @@ def test_big_file_streamed_pieces(oracle_lib, tmp_path, cuda):
     want_utf8 = [oracle.is_utf8_prefix(b[:4096]) for b in blobs]
     with _capi.Context(0, staging_bytes=4 << 20) as c:
         d, sz, st = hasher.hash_files_128bit(paths, c)
-        assert st == [0, 0, 0] and sz == sizes and d == want
+        assert st == [0] * len(sizes) and sz == sizes and d == want
         d, sz, st, meta, u8 = hasher.hash_files_text_utf8_128bit(paths, c)
         assert d == want and u8 == want_utf8
         assert [(m["text"]["num_lines"], m["text"]["num_chars"]) for m in meta] == want_counts
