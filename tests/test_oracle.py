@@ -93,3 +93,30 @@ def test_clean_corrupted_versions_oracle(oracle_lib, tmp_path):
     assert oracle_lib.clean_corrupted_versions(root, dry_run=True, threads=4) == dry
     assert oracle_lib.clean_corrupted_versions(root, dry_run=False, threads=4) == real
     assert oracle_lib.clean_corrupted_versions(root, dry_run=False, threads=4) == again
+
+
+def test_large_file_branches_agree(oracle_lib, tmp_path):
+    """Files >= 1e9 B (hasher.rs:150-174): the mmap one-shot form and the 4 KiB read-loop form the
+    CPU baseline times (oxo_hash_files_stream4k) give the same digest (XXH3 streaming == one-shot).
+    A sparse file with a few written regions keeps this cheap."""
+    import ctypes
+
+    from oracle import oracle
+
+    p = tmp_path / "big.bin"
+    size = 1_000_000_007
+    with open(p, "wb") as fh:
+        fh.truncate(size)
+        for off in (0, 123_456_789, size - 5000):
+            fh.seek(off)
+            fh.write(splitmix_bytes(off, 0, 4096).tobytes())
+    arr = (ctypes.c_char_p * 1)(os.fsencode(str(p)))
+    outs = []
+    for fn in (oracle.lib().oxo_hash_files, oracle.lib().oxo_hash_files_stream4k):
+        out = np.zeros((1, 2), dtype=np.uint64)
+        sz = np.zeros(1, dtype=np.uint64)
+        st = np.zeros(1, dtype=np.int32)
+        fn(arr, 1, out.ctypes.data_as(oracle._u64p), sz.ctypes.data_as(oracle._u64p), st.ctypes.data_as(oracle._i32p), 1)
+        assert int(st[0]) == 0 and int(sz[0]) == size
+        outs.append((int(out[0, 0]), int(out[0, 1])))
+    assert outs[0] == outs[1]
