@@ -103,6 +103,13 @@ int oxh_hash_buffers(oxh_ctx* ctx, const uint8_t* const* bufs, const uint64_t* l
 int oxh_hash_files(oxh_ctx* ctx, const char* const* paths, uint64_t n, uint64_t* out,
                    uint64_t* sizes, int32_t* status);
 
+/* get_hash_given_metadata(path, &metadata) x n (hasher.rs:56-65) with the sizes the caller already
+ * holds from its directory walk (add.rs stats every entry): readers skip the fstat and read
+ * meta_sizes[i] + 1 bytes; a file whose size differs from meta_sizes[i] is re-read (fstat + whole
+ * read), so digests always cover the file's current content. `sizes` returns the sizes read. */
+int oxh_hash_files_meta(oxh_ctx* ctx, const char* const* paths, const uint64_t* meta_sizes, uint64_t n,
+                        uint64_t* out, uint64_t* sizes, int32_t* status);
+
 /* The add loop's hash and version-store copy, fused (add.rs:507-516, 718, 743;
  * storage/local.rs:104-121; util/fs/atomic_file.rs:363-463): each file is read ONCE into pinned
  * staging and hashed by K1; when its blob is not already in the store it is written from the same

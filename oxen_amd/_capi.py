@@ -45,6 +45,7 @@ SIGNATURES = {
     "oxh_xxh3_128_large_batch_device": (_int, [ctypes.POINTER(_vp), _u64p, _u64, _vp, _vp]),
     "oxh_hash_buffers": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64p, _u64, _u64p]),
     "oxh_hash_files": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64, _u64p, _u64p, _i32p]),
+    "oxh_hash_files_meta": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64p, _u64, _u64p, _u64p, _i32p]),
     "oxh_add_files": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64, ctypes.c_char_p, _u64p, _u64p, _i32p, _i32p]),
     "oxh_clean_corrupted_versions": (_int, [_vp, ctypes.c_char_p, _int, _u64p]),
     "oxh_hash_files_text": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64, _u64p, _u64p, _i32p, _u64p]),

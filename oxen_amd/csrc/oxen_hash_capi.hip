@@ -747,6 +747,7 @@ struct SlotRun {  // a submitted slot
 // stack; the engine writes its outputs in place and wakes the caller when the last item is done.
 struct FileRequest {
     const char* const* paths = nullptr;
+    const uint64_t* meta = nullptr;  // sizes the caller already has (get_hash_given_metadata), or null
     uint64_t n = 0;
     uint64_t* out = nullptr;
     uint64_t* sizes = nullptr;
@@ -784,6 +785,8 @@ struct FileStream {
     std::mutex omu;
     std::vector<std::pair<FileRequest*, uint64_t>> oversize;
     std::atomic<uint64_t> n_oversize{0};
+    std::vector<std::pair<FileRequest*, uint64_t>> changed;  // meta size != file size: re-read
+    std::atomic<uint64_t> n_changed{0};
     std::mutex cmu;  // the engine sleeps on ccv between events
     std::condition_variable ccv;
     uint64_t files = 0, slots = 0;
@@ -874,10 +877,10 @@ bool open_slot(FileStream& fs, int t) {
 }
 
 // Reserve L bytes for item i of r; returns the slot (and offset), or -1 on abort.
-int reserve(FileStream& fs, FileRequest* r, uint64_t i, uint64_t L, uint64_t& off) {
+int reserve(FileStream& fs, FileRequest* r, uint64_t i, uint64_t L, uint64_t room, uint64_t& off, uint64_t& jout) {
     oxh_ctx* c = fs.c;
     const uint64_t M = c->max_items, cap = c->stage_bytes;
-    const uint64_t need = align_up(L);
+    const uint64_t need = align_up(room);
     for (;;) {
         if (fs.abort.load(std::memory_order_relaxed)) return -1;
         const int s = fs.cur.load(std::memory_order_acquire);
@@ -888,9 +891,10 @@ int reserve(FileStream& fs, FileRequest* r, uint64_t i, uint64_t L, uint64_t& of
             continue;
         }
         const uint64_t o = w_bytes(w), j = w_items(w);
-        if (o + L <= cap && j < M) {
+        if (o + room <= cap && j < M) {
             if (!sl.word.compare_exchange_weak(w, w + (1ull << kWBytes) + need, std::memory_order_acq_rel)) continue;
             off = o;
+            jout = j;
             c->h_desc[s][j] = o;
             c->h_desc[s][M + j] = L;
             c->rq[s][j] = r;
@@ -919,13 +923,16 @@ void reader_loop(FileStream& fs) {
                 ++failed;
                 continue;
             }
-            if (fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode)) {
+            // with the caller's metadata size no fstat is needed: read one byte more than expected
+            // and re-read the file (fstat + whole read) if the size turns out different
+            const bool meta = r->meta != nullptr && r->meta[i] < c->stage_bytes;
+            if (!meta && (fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode))) {
                 close(fd);
                 r->st[i] = OXH_ERR_IO;
                 ++failed;
                 continue;
             }
-            const uint64_t L = (uint64_t)sb.st_size;
+            const uint64_t L = meta ? r->meta[i] : (uint64_t)sb.st_size;
             r->lens[i] = L;
             if (L > c->stage_bytes) {  // the engine reads it through the oversize path
                 close(fd);
@@ -937,24 +944,35 @@ void reader_loop(FileStream& fs) {
                 fs.wake();
                 continue;
             }
-            uint64_t off = 0;
-            const int s = reserve(fs, r, i, L, off);
+            uint64_t off = 0, j = 0;
+            const int s = reserve(fs, r, i, L, meta ? L + 1 : L, off, j);
             if (s < 0) {
                 close(fd);
                 stop = true;  // aborted: the engine fails every open request
                 break;
             }
             uint8_t* dst = c->h_stage[s] + off;
+            const uint64_t want = meta ? L + 1 : L;
             uint64_t got = 0;
-            while (got < L) {
-                const ssize_t k = pread(fd, dst + got, L - got, (off_t)got);
-                if (k <= 0) {
+            while (got < want) {
+                const ssize_t k = pread(fd, dst + got, want - got, (off_t)got);
+                if (k < 0 || (k == 0 && !meta)) {
                     r->st[i] = OXH_ERR_IO;
                     break;
                 }
+                if (k == 0) break;  // EOF
                 got += (uint64_t)k;
             }
             close(fd);
+            if (meta && r->st[i] == OXH_OK && got != L) {  // the file is not the size the caller saw
+                c->rq[s][j] = nullptr;                     // drain skips this slot entry
+                {
+                    std::lock_guard<std::mutex> g(fs.omu);
+                    fs.changed.push_back({r, i});
+                }
+                fs.n_changed.fetch_add(1);
+                fs.wake();
+            }
             // the last writer of a sealed slot wakes the engine
             const uint64_t d = fs.slot[s].done.fetch_add(1, std::memory_order_acq_rel) + 1;
             const uint64_t w = fs.slot[s].word.load(std::memory_order_acquire);
@@ -975,6 +993,7 @@ void drain_files(FileStream& fs, int s, const SlotRun& p) {
     bool any_sink = false;
     for (uint64_t j = 0; j < cnt; ++j) {
         FileRequest* r = rq[j];
+        if (!r) continue;  // re-read later (its size changed)
         const uint64_t i = loc[j];
         r->out[2 * i] = c->h_out[s][2 * j];
         r->out[2 * i + 1] = c->h_out[s][2 * j + 1];
@@ -991,6 +1010,7 @@ void drain_files(FileStream& fs, int s, const SlotRun& p) {
         c->wpool->parallel_for(ntasks, [&](int t) {
             for (uint64_t j = (uint64_t)t; j < cnt; j += (uint64_t)ntasks) {
                 FileRequest* r = rq[j];
+                if (!r) continue;
                 const uint64_t i = loc[j];
                 if (!r->sink || r->st[i] != OXH_OK) continue;
                 (*r->sink)(i, c->h_stage[s] + c->h_desc[s][j], c->h_desc[s][M + j], c->h_out[s][2 * j], c->h_out[s][2 * j + 1]);
@@ -1000,7 +1020,7 @@ void drain_files(FileStream& fs, int s, const SlotRun& p) {
     for (uint64_t j = 0; j < cnt;) {  // one atomic per run of items of the same request
         uint64_t k = j + 1;
         while (k < cnt && rq[k] == rq[j]) ++k;
-        account(fs, rq[j], k - j);
+        if (rq[j]) account(fs, rq[j], k - j);
         j = k;
     }
 }
@@ -1186,6 +1206,46 @@ int oversize_file(FileStream& fs, FileRequest* r, uint64_t i) {
     return OXH_OK;
 }
 
+// A file whose size differed from the caller's metadata: stat and read it afresh (the reference
+// reads whatever the file holds, hasher.rs:126-148).
+int refresh_file(FileStream& fs, FileRequest* r, uint64_t i) {
+    oxh_ctx* c = fs.c;
+    struct stat sb;
+    const int fd = open(r->paths[i], O_RDONLY | O_CLOEXEC | O_NONBLOCK);
+    if (fd < 0 || fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode)) {
+        if (fd >= 0) close(fd);
+        r->st[i] = OXH_ERR_IO;
+        account(fs, r, 1);
+        return OXH_OK;
+    }
+    const uint64_t L = (uint64_t)sb.st_size;
+    r->lens[i] = L;
+    if (L > c->stage_bytes) {
+        close(fd);
+        return oversize_file(fs, r, i);
+    }
+    std::vector<uint8_t> tmp(std::max<uint64_t>(L, 1));
+    uint64_t got = 0;
+    while (got < L) {
+        const ssize_t k = pread(fd, tmp.data() + got, L - got, (off_t)got);
+        if (k <= 0) break;
+        got += (uint64_t)k;
+    }
+    close(fd);
+    if (got != L) {
+        r->st[i] = OXH_ERR_IO;
+    } else {
+        int32_t u8 = 0;
+        if (int rc = oversize_item(c, tmp.data(), L, r->out + 2 * i, r->counts ? r->counts + 2 * i : nullptr,
+                                   r->utf8 ? &u8 : nullptr))
+            return rc;
+        if (r->utf8) r->utf8[i] = u8;
+        if (r->sink) (*r->sink)(i, tmp.data(), L, r->out[2 * i], r->out[2 * i + 1]);
+    }
+    account(fs, r, 1);
+    return OXH_OK;
+}
+
 // One run of the engine: from the first queued request until the readers are idle, the queue is
 // empty and every submitted slot is drained.
 void run_stream(oxh_ctx* c) {
@@ -1223,7 +1283,18 @@ void run_stream(oxh_ctx* c) {
             progressed = true;
         }
         if (rc) break;
-        // 2. files larger than a slot, one at a time
+        // 2. files larger than a slot, and files whose size changed, one at a time
+        if (fs.n_changed.load(std::memory_order_acquire)) {
+            std::pair<FileRequest*, uint64_t> it;
+            {
+                std::lock_guard<std::mutex> g(fs.omu);
+                it = fs.changed.back();
+                fs.changed.pop_back();
+            }
+            fs.n_changed.fetch_sub(1);
+            rc = refresh_file(fs, it.first, it.second);
+            continue;
+        }
         if (fs.n_oversize.load(std::memory_order_acquire)) {
             std::pair<FileRequest*, uint64_t> it;
             {
@@ -1270,7 +1341,8 @@ void run_stream(oxh_ctx* c) {
             continue;
         }
         // 4. nothing left: close the run (requests arriving later start the next one)
-        if (all_idle && sst == 1 && !(w & kSealedBit) && w_items(w) == 0 && nbusy == 0 && fs.n_oversize.load() == 0) {
+        if (all_idle && sst == 1 && !(w & kSealedBit) && w_items(w) == 0 && nbusy == 0 && fs.n_oversize.load() == 0 &&
+            fs.n_changed.load() == 0) {
             std::lock_guard<std::mutex> g(c->qmu);
             if (c->queue.empty() && fs.idle.load() == fs.nreaders) {
                 fs.closing = true;
@@ -1343,11 +1415,13 @@ void engine_main(oxh_ctx* c) {
 }  // namespace
 
 static int hash_files_impl(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* sizes, int32_t* status,
-                           uint64_t* counts, const ItemSink* sink = nullptr, int32_t* utf8 = nullptr) {
+                           uint64_t* counts, const ItemSink* sink = nullptr, int32_t* utf8 = nullptr,
+                           const uint64_t* meta = nullptr) {
     if (!c || (n && (!paths || !out))) return fail(OXH_ERR_INVALID, "bad arguments");
     if (n == 0) return OXH_OK;
     FileRequest r;
     r.paths = paths;
+    r.meta = meta;
     r.n = n;
     r.out = out;
     r.sizes = sizes;
@@ -1370,6 +1444,12 @@ static int hash_files_impl(oxh_ctx* c, const char* const* paths, uint64_t n, uin
 
 int oxh_hash_files(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* sizes, int32_t* status) {
     return hash_files_impl(c, paths, n, out, sizes, status, nullptr);
+}
+
+int oxh_hash_files_meta(oxh_ctx* c, const char* const* paths, const uint64_t* meta_sizes, uint64_t n, uint64_t* out,
+                        uint64_t* sizes, int32_t* status) {
+    if (n && !meta_sizes) return fail(OXH_ERR_INVALID, "meta_sizes is NULL");
+    return hash_files_impl(c, paths, n, out, sizes, status, nullptr, nullptr, nullptr, meta_sizes);
 }
 
 int oxh_hash_files_text(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* sizes, int32_t* status,

@@ -109,6 +109,28 @@ def hash_files_128bit(paths: Sequence[str], ctx: Optional[_capi.Context] = None)
     return digests, [int(s) for s in sizes], [int(s) for s in status]
 
 
+
+def hash_files_given_metadata_128bit(paths: Sequence[str], meta_sizes: Sequence[int],
+                                     ctx: Optional[_capi.Context] = None):
+    """`get_hash_given_metadata(path, &metadata)` over many files (hasher.rs:56-65) with the sizes
+    the caller's directory walk already has: no fstat per file; a file whose size changed since is
+    re-read. Returns (digests, sizes, status) like hash_files_128bit."""
+    ctx = ctx or default_context()
+    n = len(paths)
+    if n == 0:
+        return [], [], []
+    if len(meta_sizes) != n:
+        raise _capi.OxenError("paths and meta_sizes differ in length", _capi.OXH_ERR_INVALID)
+    arr = (ctypes.c_char_p * n)(*[os.fsencode(str(p)) for p in paths])
+    meta = np.ascontiguousarray(meta_sizes, dtype=np.uint64)
+    out = np.zeros((n, 2), dtype=np.uint64)
+    sizes = np.zeros(n, dtype=np.uint64)
+    status = np.zeros(n, dtype=np.int32)
+    _capi.check(_capi.lib().oxh_hash_files_meta(ctx.handle, arr, meta.ctypes.data_as(_capi._u64p), n,
+                                                out.ctypes.data_as(_capi._u64p), sizes.ctypes.data_as(_capi._u64p),
+                                                status.ctypes.data_as(_capi._i32p)), "oxh_hash_files_meta")
+    return _u128_list(out, status), [int(s) for s in sizes], [int(s) for s in status]
+
 def add_files(paths: Sequence[str], versions_root: str, ctx: Optional[_capi.Context] = None):
     """Fused hash + version-store publish (oxh_add_files): returns (digests, sizes, status, stored).
     stored[i] is True when the blob {versions_root}/{hex[:2]}/{hex[2:]}/data was written now."""

@@ -712,3 +712,35 @@ def test_big_file_streamed_pieces(oracle_lib, tmp_path, cuda, monkeypatch, piece
         assert [(m["text"]["num_lines"], m["text"]["num_chars"]) for m in meta] == want_counts
         d, sz, st, stored = hasher.add_files(paths, str(tmp_path / "store"), c)
         assert d == want and all(s == 0 for s in st) and all(stored)
+
+
+def test_hash_files_given_metadata(oracle_lib, tmp_path, cuda):
+    """oxh_hash_files_meta (get_hash_given_metadata with the walk's sizes, hasher.rs:56-65): no
+    fstat per file; sizes that are stale (file grew, shrank, emptied), a directory, a missing path and
+    an oversize file are all handled so that every digest covers the file's current content."""
+    from oxen_amd import _capi, hasher
+    from oxen_amd.workloads import splitmix_bytes
+
+    rng = np.random.default_rng(41)
+    blobs = [splitmix_bytes(900 + k, 0, int(s)).tobytes() for k, s in enumerate(rng.integers(0, 300_000, 400))]
+    blobs += [b"", b"x", splitmix_bytes(5, 0, (3 << 20) + 9).tobytes()]  # the last one is oversize
+    paths = []
+    for k, b in enumerate(blobs):
+        p = tmp_path / f"m{k}.bin"
+        p.write_bytes(b)
+        paths.append(str(p))
+    meta = [len(b) for b in blobs]
+    meta[3] += 1          # file shrank since the walk
+    meta[4] = max(0, meta[4] - 7)  # file grew
+    meta[5] = 0           # grew from empty
+    meta[-3] = 10         # now empty
+    os.mkdir(tmp_path / "adir")
+    paths += [str(tmp_path / "adir"), str(tmp_path / "missing")]
+    meta += [4096, 5]
+    want_out, want_sizes, want_st = oracle_lib.hash_files(paths, threads=8)
+    with _capi.Context(0, staging_bytes=1 << 20) as c:
+        d, sz, st = hasher.hash_files_given_metadata_128bit(paths, meta, c)
+    assert st[:-2] == [0] * len(blobs) and st[-2] != 0 and st[-1] != 0
+    assert sz[:-2] == [len(b) for b in blobs]
+    assert d[:-2] == [(int(hi) << 64) | int(lo) for lo, hi in want_out[:-2]]
+    assert d[-2] is None and d[-1] is None

@@ -4,6 +4,7 @@
 
 Writes the C3 image repo (benchmark/generate_image_repo.py layout: 200 000 noise TIFFs of
 49 292 B in 1 000 dirs + images.csv + README.md), then times, on the same files:
+  gpu_e2e_meta  oxh_hash_files_meta: the same with the caller's stat sizes (no fstat per file)
   gpu_e2e    oxh_hash_files: parallel pread into pinned staging -> H2D on a side stream (3-slot
              ring, overlapped with K1 on the compute stream) -> D2H digests
   cpu_ref    the reference's per-file loop restated in C (oracle/): stat, read whole file, one-shot
@@ -91,6 +92,19 @@ def main():
                     "oxh_hash_files")
         return time.perf_counter() - t0, out, st
 
+    # get_hash_given_metadata form: the sizes liboxen's walk already has (stat'ed outside the timing)
+    meta = np.array([os.stat(p).st_size for p in paths], dtype=np.uint64)
+
+    def gpu_meta_call():
+        out = np.zeros((n, 2), dtype=np.uint64)
+        sizes = np.zeros(n, dtype=np.uint64)
+        st = np.zeros(n, dtype=np.int32)
+        t0 = time.perf_counter()
+        _capi.check(L.oxh_hash_files_meta(ctx.handle, c_paths, meta.ctypes.data_as(_capi._u64p), n,
+                                          out.ctypes.data_as(_capi._u64p), sizes.ctypes.data_as(_capi._u64p),
+                                          st.ctypes.data_as(_capi._i32p)), "oxh_hash_files_meta")
+        return time.perf_counter() - t0, out, st
+
     def cpu_call():
         out = np.zeros((n, 2), dtype=np.uint64)
         sizes = np.zeros(n, dtype=np.uint64)
@@ -147,10 +161,11 @@ def main():
     runs = {}
     # warm: GPU and CPU alternate, 5 rounds (host timings on a shared box vary by +-20 % run to run)
     oracle.hash_files(paths[: min(len(paths), 1000)], a.threads)
-    wt = {"gpu_e2e": [], "cpu_ref": []}
+    wt = {"gpu_e2e": [], "gpu_e2e_meta": [], "cpu_ref": []}
+    calls = {"gpu_e2e": gpu_call, "gpu_e2e_meta": gpu_meta_call, "cpu_ref": cpu_call}
     for _ in range(5):
-        for who in ("gpu_e2e", "cpu_ref"):
-            dt, out, st = gpu_call() if who == "gpu_e2e" else cpu_call()
+        for who in ("gpu_e2e", "gpu_e2e_meta", "cpu_ref"):
+            dt, out, st = calls[who]()
             assert (st == 0).all(), "file errors"
             runs[(who, "warm")] = out
             wt[who].append(dt)
@@ -165,7 +180,8 @@ def main():
         runs[(who, "cold")] = out
         res[f"{who}_cold_s"] = round(dt, 3)
         res[f"{who}_cold_GiBs"] = round(nbytes / dt / 2**30, 2)
-    res["digests_bit_exact"] = all(np.array_equal(runs[("gpu_e2e", c)], runs[("cpu_ref", c)]) for c in ("warm", "cold"))
+    res["digests_bit_exact"] = (all(np.array_equal(runs[("gpu_e2e", c)], runs[("cpu_ref", c)]) for c in ("warm", "cold"))
+                                and np.array_equal(runs[("gpu_e2e_meta", "warm")], runs[("cpu_ref", "warm")]))
     # the Python mirror (hasher.hash_files_128bit) on warm cache, for its wrapper overhead
     t0 = time.perf_counter()
     d, _, _ = hasher.hash_files_128bit(paths, ctx)
