@@ -255,48 +255,82 @@ void engine_main(oxh_ctx* c);  // the streaming file engine's thread (below)
 // kernel's 32 KiB makes every chain workgroup need more than half a CU's 160 KiB: one chain per CU.
 constexpr size_t kChainLdsPad = 50 * 1024;
 
-// K1L over n device buffers: block sums chip-wide (one launch per buffer; each fills the chip),
-// then the serial chains of up to kChainJobs buffers in one launch, one wave each, so the chains of
-// many large files run concurrently. Buffers below ~1 MiB take one K1 wave instead.
+// K1L over n device buffers. Buffers below ~1 MiB take one K1 wave. The others are processed in
+// rounds of 1 GiB pieces (OXH_BIG_PIECE_MIB): round r computes the block sums of every buffer's
+// piece r chip-wide on `st` while the serial chains of round r-1 run on the scratch buffer's own
+// stream, up to kChainJobs chains per launch (ChainJob resume / partial flags carry each buffer's 8
+// accumulators from piece to piece), so a chain starts one piece's block sums after its buffer does
+// instead of after every buffer's, and the block-sum scratch is two rounds of pieces, not the whole
+// input. Returns after `st` has finished.
 int large_batch_device(const uint8_t* const* bufs, const uint64_t* lens, uint64_t n, uint64_t* d_out, hipStream_t st) {
-    uint64_t total_nb = 0;
-    for (uint64_t i = 0; i < n; ++i) {
-        const uint64_t nb = lens[i] > 0 ? (lens[i] - 1) >> 10 : 0;
-        if (nb >= 1024) total_nb += nb;
-    }
-    uint64_t* sums = nullptr;
-    oxh::ScratchLease lease(st);  // the device's cached scratch (scratch.hpp); synchronises st at the end
-    if (total_nb) HIP_TRY(lease.get(total_nb * 64, (void**)&sums));
-    oxh::ChainBatch batch;
-    int nj = 0;
-    uint64_t off = 0;
+    const char* pe = getenv("OXH_BIG_PIECE_MIB");
+    const uint64_t P = std::max<uint64_t>(1, pe ? strtoull(pe, nullptr, 10) : 1024) << 20;
+    std::vector<uint64_t> big;  // buffers on the chained path
+    uint64_t rounds = 0;
+    auto pieces_of = [&](uint64_t len) { return (len > P + 1024 ? (len - 1025) / P : 0) + 1; };
     for (uint64_t i = 0; i < n; ++i) {
         const uint64_t len = lens[i];
         const uint64_t nb = len > 0 ? (len - 1) >> 10 : 0;
         if (nb < 1024) {
-            int rc = launch_chunks(bufs[i], 1, len, len, d_out + 2 * i, st);
-            if (rc) return rc;
+            if (int rc = launch_chunks(bufs[i], 1, len, len, d_out + 2 * i, st)) return rc;
             continue;
         }
-        const bool aligned = (reinterpret_cast<uintptr_t>(bufs[i]) & 15) == 0;
-        const uint64_t nwaves = (nb + 3) / 4, blocks = (nwaves + 3) / 4;
-        if (aligned)
-            hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, bufs[i], nb, sums + off);
-        else
-            hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, bufs[i], nb, sums + off);
-        HIP_TRY(hipGetLastError());
-        batch.job[nj++] = {bufs[i], len, sums + off, d_out + 2 * i};
-        off += nb * 8;
-        if (nj == oxh::kChainJobs) {
-            hipLaunchKernelGGL(oxh::xxh3_chain_kernel, dim3(nj), dim3(64), kChainLdsPad, st, batch);
+        big.push_back(i);
+        rounds = std::max(rounds, pieces_of(len));
+    }
+    if (big.empty()) return OXH_OK;
+    oxh::ScratchLease lease(st);  // the device's cached scratch (scratch.hpp); synchronises st at the end
+    const uint64_t per_buf = ((P + 1024) >> 10) * 8;  // block-sum u64 per buffer per round
+    uint64_t* scratch = nullptr;
+    HIP_TRY(lease.get((2 * per_buf * big.size() + 8 * big.size()) * 8, (void**)&scratch));
+    uint64_t* state = scratch + 2 * per_buf * big.size();  // 8 accumulators per buffer
+    hipStream_t aux = nullptr;
+    hipEvent_t* ev = nullptr;
+    HIP_TRY(lease.aux(&aux, &ev));
+    hipEvent_t* ev_sums = ev;       // [2] block sums of round r (parity) are ready
+    hipEvent_t* ev_chain = ev + 2;  // [2] chains of round r (parity) are done with them
+    for (uint64_t r = 0; r < rounds; ++r) {
+        const int b = (int)(r & 1);
+        if (r >= 2) HIP_TRY(hipStreamWaitEvent(st, ev_chain[b], 0));  // round r-2 read these sums
+        oxh::ChainBatch batch;
+        int nj = 0;
+        auto flush = [&]() -> int {
+            if (!nj) return OXH_OK;
+            hipLaunchKernelGGL(oxh::xxh3_chain_kernel, dim3(nj), dim3(64), kChainLdsPad, aux, batch);
             HIP_TRY(hipGetLastError());
             nj = 0;
+            return OXH_OK;
+        };
+        std::vector<oxh::ChainJob> jobs;
+        for (uint64_t q = 0; q < big.size(); ++q) {
+            const uint64_t i = big[q], len = lens[i], k = pieces_of(len) - 1;
+            if (r > k) continue;
+            const uint64_t off = r * P, plen = r < k ? P : len - off;
+            const bool last = r == k;
+            const uint64_t nb = last ? (plen - 1) >> 10 : plen >> 10;
+            uint64_t* s_q = scratch + ((uint64_t)b * big.size() + q) * per_buf;
+            const uint8_t* p = bufs[i] + off;
+            const bool aligned = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+            const uint64_t nwaves = (nb + 3) / 4, blocks = (nwaves + 3) / 4;
+            if (aligned)
+                hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, p, nb, s_q);
+            else
+                hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, p, nb, s_q);
+            HIP_TRY(hipGetLastError());
+            jobs.push_back({p, plen, s_q, d_out + 2 * i, len, state + 8 * q,
+                            (r > 0 ? oxh::kChainResume : 0u) | (last ? 0u : oxh::kChainPartial)});
         }
+        HIP_TRY(hipEventRecord(ev_sums[b], st));
+        HIP_TRY(hipStreamWaitEvent(aux, ev_sums[b], 0));
+        for (const oxh::ChainJob& j : jobs) {
+            batch.job[nj++] = j;
+            if (nj == oxh::kChainJobs)
+                if (int rc = flush()) return rc;
+        }
+        if (int rc = flush()) return rc;
+        HIP_TRY(hipEventRecord(ev_chain[b], aux));
     }
-    if (nj) {
-        hipLaunchKernelGGL(oxh::xxh3_chain_kernel, dim3(nj), dim3(64), kChainLdsPad, st, batch);
-        HIP_TRY(hipGetLastError());
-    }
+    HIP_TRY(hipStreamWaitEvent(st, ev_chain[(rounds - 1) & 1], 0));  // st continues after every chain
     return OXH_OK;
 }
 

@@ -21,15 +21,21 @@ struct ScratchCache {
     std::mutex mu;
     void* base = nullptr;
     uint64_t size = 0;
+    hipStream_t aux = nullptr;  // a second stream for the lease holder (created on first use)
+    hipEvent_t ev[4] = {};
 };
 
-inline ScratchCache& scratch_cache(int dev) {
+// Two buffers per device, so two calls on different streams (say FastCDC chunking and the K1L
+// whole-file chains of the same blobs) can run concurrently; a third caller waits for the first.
+constexpr int kScratchPerDevice = 2;
+
+inline ScratchCache* scratch_caches(int dev) {
     static std::mutex mu;
-    static std::map<int, ScratchCache*> caches;  // one per device, for the process lifetime
+    static std::map<int, ScratchCache*> caches;  // kScratchPerDevice per device, process lifetime
     std::lock_guard<std::mutex> g(mu);
     ScratchCache*& c = caches[dev];
-    if (!c) c = new ScratchCache();
-    return *c;
+    if (!c) c = new ScratchCache[kScratchPerDevice];
+    return c;
 }
 
 class ScratchLease {
@@ -37,8 +43,18 @@ class ScratchLease {
     explicit ScratchLease(hipStream_t st) : st_(st) {
         int dev = 0;
         (void)hipGetDevice(&dev);
-        cache_ = &scratch_cache(dev);
-        lk_ = std::unique_lock<std::mutex>(cache_->mu);
+        ScratchCache* cs = scratch_caches(dev);
+        for (int k = 0; k < kScratchPerDevice && !lk_.owns_lock(); ++k) {
+            std::unique_lock<std::mutex> t(cs[k].mu, std::try_to_lock);
+            if (t.owns_lock()) {
+                cache_ = &cs[k];
+                lk_ = std::move(t);
+            }
+        }
+        if (!lk_.owns_lock()) {
+            cache_ = &cs[0];
+            lk_ = std::unique_lock<std::mutex>(cache_->mu);
+        }
     }
     ~ScratchLease() {
         (void)hipStreamSynchronize(st_);
@@ -55,9 +71,7 @@ class ScratchLease {
     // At least `bytes` of device memory, valid until the lease ends.
     hipError_t get(uint64_t bytes, void** out) {
         if (cache_->size < bytes) {
-            if (cache_->base) {
-                const hipError_t e = hipDeviceSynchronize();  // an earlier call may still read it
-                if (e != hipSuccess) return e;
+            if (cache_->base) {  // idle: the previous holder synchronised its stream before releasing
                 (void)hipFree(cache_->base);
                 cache_->base = nullptr;
                 cache_->size = 0;
@@ -70,6 +84,21 @@ class ScratchLease {
         return hipSuccess;
     }
     uint64_t size() const { return cache_->size; }
+    // A stream of this scratch buffer's own, for work the caller overlaps with its stream, and four
+    // events to order the two (created on first use, kept with the buffer).
+    hipError_t aux(hipStream_t* s, hipEvent_t** ev) {
+        if (!cache_->aux) {
+            const hipError_t e = hipStreamCreateWithFlags(&cache_->aux, hipStreamNonBlocking);
+            if (e != hipSuccess) return e;
+            for (hipEvent_t& x : cache_->ev) {
+                const hipError_t f = hipEventCreateWithFlags(&x, hipEventDisableTiming);
+                if (f != hipSuccess) return f;
+            }
+        }
+        *s = cache_->aux;
+        *ev = cache_->ev;
+        return hipSuccess;
+    }
 
    private:
     hipStream_t st_;

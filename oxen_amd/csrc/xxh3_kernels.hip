@@ -513,6 +513,9 @@ __global__ __launch_bounds__(256) void xxh3_blocksum_kernel(const uint8_t* __res
 // with the next group's loads in flight while the current group is chained.
 __global__ __launch_bounds__(64) void xxh3_chain_kernel(ChainBatch batch) {
     constexpr int GROUP = 256;
+    // the chain is one latency-bound wave per file: give it issue priority over any wave of a
+    // concurrent kernel (chunking, K1) that lands on the same SIMD
+    __builtin_amdgcn_s_setprio(3);
     const ChainJob job = batch.job[blockIdx.x];
     const uint8_t* __restrict__ p = job.p;
     const uint64_t len = job.len;

@@ -175,9 +175,14 @@ def test_chunk_digests(cuda, oracle_lib):
         assert np.array_equal(got, want), chunk
 
 
+@pytest.mark.parametrize("piece_mib", [None, "1", "3"], ids=["one-piece", "1MiB-pieces", "3MiB-pieces"])
 @pytest.mark.parametrize("n", [1 << 20, (1 << 20) + 1, (4 << 20) + 7, 64 << 20, (64 << 20) + 4097])
-def test_large_single_buffer_k1l(cuda, ctx, oracle_lib, n):
+def test_large_single_buffer_k1l(cuda, ctx, oracle_lib, n, piece_mib, monkeypatch):
+    """K1L, whole and in pieces (rounds of block sums + resumed chains, OXH_BIG_PIECE_MIB)."""
     import torch
+
+    if piece_mib:
+        monkeypatch.setenv("OXH_BIG_PIECE_MIB", piece_mib)
 
     from oxen_amd.device import fill_splitmix, large_digest_device
 
@@ -191,9 +196,14 @@ def test_large_single_buffer_k1l(cuda, ctx, oracle_lib, n):
         assert (int(got[0, 0]), int(got[0, 1])) == want, (n, start)
 
 
-def test_large_batch_k1l(cuda, oracle_lib):
-    """Several large buffers in one call (concurrent chains), mixed with small and misaligned ones."""
+@pytest.mark.parametrize("piece_mib", [None, "1"], ids=["one-piece", "1MiB-pieces"])
+def test_large_batch_k1l(cuda, oracle_lib, piece_mib, monkeypatch):
+    """Several large buffers in one call (concurrent chains), mixed with small and misaligned ones;
+    with 1 MiB pieces the buffers need different numbers of rounds."""
     import torch
+
+    if piece_mib:
+        monkeypatch.setenv("OXH_BIG_PIECE_MIB", piece_mib)
 
     from oxen_amd.device import fill_splitmix, large_digests_device
 
