@@ -1065,10 +1065,10 @@ void drain_files(FileStream& fs, int s, const SlotRun& p) {
 // stays bounded whatever the file size and piece j+1's transfer overlaps piece j's K1L chain: each
 // piece's block sums are computed chip-wide and the serial chain continues from the previous piece's
 // accumulators (ChainJob kChainResume / kChainPartial); the last piece (> 1 KiB) takes the tail and
-// the merge. A piece reaches the device copy-free when the file's page-cache pages can be pinned
-// (mmap + hipHostRegister read-only, ~2 ms per GiB; the DMA engine then reads them at 46-57 GB/s,
-// tools/mmap_register_probe.hip), else through two pinned bounce buffers filled by the worker pool
-// (parallel 4 MiB preads, 64 MiB at a time). Text counts accumulate over the pieces; is_utf8 reads
+// the merge. A piece reaches the device copy-free when its pages are in the page cache (mincore)
+// and can be pinned (mmap + hipHostRegister read-only, ~2 ms per GiB; the DMA engine then reads
+// them at 46-57 GB/s, tools/mmap_register_probe.hip), else through two pinned bounce buffers
+// filled by the worker pool (parallel 4 MiB preads, 64 MiB at a time). Text counts accumulate over the pieces; is_utf8 reads
 // the first 4 KiB of piece 0.
 constexpr uint64_t kBounce = 64ull << 20, kBigRead = 4ull << 20;
 
@@ -1124,8 +1124,19 @@ int big_file(FileStream& fs, FileRequest* r, uint64_t i) {
         }
     }
     // piece j of the file -> dbuf[b] on the copy stream; false on an I/O error
+    // pages of [off, off + plen) in the page cache: pinning faults missing pages in one thread,
+    // so a piece that is mostly on disk is read by the parallel preads instead
+    std::vector<unsigned char> resident;
+    auto mostly_resident = [&](uint64_t off, uint64_t plen) {
+        const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE), npg = (plen + pg - 1) / pg;
+        resident.resize(npg);
+        if (mincore(map + off, plen, resident.data()) != 0) return false;
+        uint64_t in = 0;
+        for (unsigned char v : resident) in += v & 1;
+        return in * 10 >= npg * 9;
+    };
     auto copy_piece = [&](uint64_t off, uint64_t plen, int b) -> bool {
-        if (map && hipHostRegister(map + off, plen, hipHostRegisterReadOnly) == hipSuccess) {
+        if (map && mostly_resident(off, plen) && hipHostRegister(map + off, plen, hipHostRegisterReadOnly) == hipSuccess) {
             const bool ok = hipMemcpyAsync(dbuf[b], map + off, plen, hipMemcpyHostToDevice, c->copy_stream) == hipSuccess &&
                             hipStreamSynchronize(c->copy_stream) == hipSuccess;
             (void)hipHostUnregister(map + off);
@@ -1136,6 +1147,8 @@ int big_file(FileStream& fs, FileRequest* r, uint64_t i) {
             const int bb = (int)(q & 1);
             if (c->bounce_used[bb] && hipEventSynchronize(c->ev_bounce[bb]) != hipSuccess) return false;
             const uint64_t n = std::min(kBounce, plen - o);
+            // the kernel reads the next two bounce pieces ahead while the pool reads this one
+            (void)posix_fadvise(fd, (off_t)(off + o + n), (off_t)(2 * kBounce), POSIX_FADV_WILLNEED);
             const int parts = (int)((n + kBigRead - 1) / kBigRead);
             std::atomic<bool> bad{false};
             c->pool->parallel_for(parts, [&](int t) {
