@@ -135,7 +135,7 @@ def main() -> None:
     from oxen_amd import _capi
     from oxen_amd import build as hb
     from oxen_amd.device import DeviceArena, to_numpy_u64
-    from oxen_amd.shard import gather_digest_table
+    from oxen_amd.shard import PipelinedGather, gather_digest_table
 
     if rank == 0:
         hb.build()
@@ -154,32 +154,23 @@ def main() -> None:
     torch.cuda.synchronize()
 
     # N > 1 over RCCL: each step's digest gather runs on the collective's stream while the next step
-    # hashes into the other of two digest tables (the gather of step k overlaps the hash of k+1; a
-    # table is rewritten only after the gather that read it has finished)
-    outs = [out, torch.empty_like(out)] if world > 1 and args.backend == "nccl" else [out]
-    fulls = [torch.empty((n_items * world, 2), dtype=torch.int64, device=dev) for _ in outs]
-    pending = [None] * len(outs)
-    nstep = [0]
+    # hashes into the other of two digest tables (shard.PipelinedGather: the gather of step k overlaps
+    # the hash of k+1; a table is rewritten only after the gather that read it has finished)
+    pipe = PipelinedGather(n_items, world, dev) if world > 1 and args.backend == "nccl" else None
 
     def step():
-        b = nstep[0] % len(outs)
-        nstep[0] += 1
-        if pending[b] is not None:
-            pending[b].wait()
-            pending[b] = None
-        da.hash(outs[b])
+        if pipe is not None:
+            b, local = pipe.next_local()
+            da.hash(local)
+            return pipe.gather(b), local
+        da.hash(out)
         if world > 1:
-            if args.backend == "nccl":
-                pending[b] = dist.all_gather_into_tensor(fulls[b], outs[b], async_op=True)
-                return fulls[b], outs[b]
-            return gather_digest_table(outs[b].cpu(), counts), outs[b]  # gloo rehearsal: host tables
-        return outs[b], outs[b]
+            return gather_digest_table(out.cpu(), counts), out  # gloo rehearsal: host tables
+        return out, out
 
     def drain():  # the current stream waits for every outstanding gather
-        for i, w in enumerate(pending):
-            if w is not None:
-                w.wait()
-                pending[i] = None
+        if pipe is not None:
+            pipe.drain()
 
     for _ in range(args.warmup):
         step()

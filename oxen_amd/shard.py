@@ -39,3 +39,37 @@ def gather_digest_table(local: torch.Tensor, counts: Sequence[int], group=None) 
     dist.all_gather_into_tensor(full, local.contiguous(), group=group)
     parts = [full[r * m:r * m + counts[r]] for r in range(world)]
     return torch.cat(parts, 0) if parts else full[:0]
+
+
+class PipelinedGather:
+    """Double-buffered digest tables whose all-gather overlaps the next batch's hashing (bench.py's
+    N > 1 step): fill(b) hands out local table b; gather(b) starts its all-gather asynchronously; a
+    table is handed out again only after the gather that read it has completed (work.wait(), which on
+    RCCL makes the current stream wait, on gloo blocks). Every rank must hold the same count n."""
+
+    def __init__(self, n: int, world: int, device, group=None, buffers: int = 2):
+        self.local = [torch.empty((n, 2), dtype=torch.int64, device=device) for _ in range(buffers)]
+        self.full = [torch.empty((n * world, 2), dtype=torch.int64, device=device) for _ in range(buffers)]
+        self.pending = [None] * buffers
+        self.group = group
+        self.k = 0
+
+    def next_local(self) -> tuple[int, torch.Tensor]:
+        """The next local table to fill, once no gather still reads it."""
+        b = self.k % len(self.local)
+        self.k += 1
+        if self.pending[b] is not None:
+            self.pending[b].wait()
+            self.pending[b] = None
+        return b, self.local[b]
+
+    def gather(self, b: int) -> torch.Tensor:
+        """Start the all-gather of local table b; returns the full table it will fill."""
+        self.pending[b] = dist.all_gather_into_tensor(self.full[b], self.local[b], group=self.group, async_op=True)
+        return self.full[b]
+
+    def drain(self) -> None:
+        for i, w in enumerate(self.pending):
+            if w is not None:
+                w.wait()
+                self.pending[i] = None

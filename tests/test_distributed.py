@@ -69,3 +69,48 @@ def test_gather_digest_table_gloo(world, oracle_lib):
         p.join(120)
         assert p.exitcode == 0
     assert q.get(timeout=10) is True
+
+
+def _pipe_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oxen_amd.shard import PipelinedGather
+
+        n, steps = 37, 7
+
+        def table(r, k):  # what rank r hashes at step k
+            return torch.arange(2 * n, dtype=torch.int64).reshape(n, 2) * 1000 + r * 100 + k
+
+        want = [torch.cat([table(r, k) for r in range(world)]) for k in range(steps)]
+        pipe = PipelinedGather(n, world, "cpu")
+        ok, fulls = True, {}
+        for k in range(steps):
+            b, local = pipe.next_local()  # waits for the gather that last read this table
+            if k >= 2:
+                ok &= bool(torch.equal(pipe.full[b], want[k - 2]))  # step k-2's result, intact
+            local.copy_(table(rank, k))
+            fulls[k] = pipe.gather(b)
+        pipe.drain()
+        ok &= bool(torch.equal(fulls[steps - 1], want[steps - 1]) and torch.equal(fulls[steps - 2], want[steps - 2]))
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pipelined_gather_gloo():
+    """bench.py's N > 1 step (shard.PipelinedGather): double-buffered tables, each step's all-gather
+    in flight while the next table is filled, every step's gathered table correct (world size 2)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    res = dict(q.get(timeout=10) for _ in range(world))
+    assert res == {0: True, 1: True}
