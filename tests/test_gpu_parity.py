@@ -754,3 +754,27 @@ def test_hash_files_given_metadata(oracle_lib, tmp_path, cuda):
     assert sz[:-2] == [len(b) for b in blobs]
     assert d[:-2] == [(int(hi) << 64) | int(lo) for lo, hi in want_out[:-2]]
     assert d[-2] is None and d[-1] is None
+
+
+@pytest.mark.parametrize("mode", ["short", "auto"])
+def test_k1_many_ragged_items(cuda, oracle_lib, mode):
+    """Many ragged, byte-packed items (FastCDC-chunk-like, with short-path items mixed in): the
+    short-item and the default K1 dispatch against the oracle."""
+    import torch
+
+    from oxen_amd import _capi
+    from oxen_amd.device import fill_splitmix, xxh3_128_batch_device
+
+    rng = np.random.default_rng(17)
+    lens = rng.integers(0, 20_000, 40_000).astype(np.uint64)
+    lens[::97] = rng.integers(0, 241, len(lens[::97]))  # short-path items mixed in
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64) + 3
+    total = int(offs[-1] + lens[-1]) + 64
+    arena = torch.empty(total, dtype=torch.uint8, device=cuda)
+    fill_splitmix(arena, 1234)
+    o = torch.from_numpy(offs.view(np.int64)).to(cuda)
+    ln = torch.from_numpy(lens.view(np.int64)).to(cuda)
+    m = _capi.OXH_MODE_WAVE_SHORT if mode == "short" else _capi.OXH_MODE_AUTO
+    got = _u64(xxh3_128_batch_device(arena, o, ln, mode=m))
+    want = oracle_lib.batch(arena.cpu().numpy(), offs, lens, threads=8)
+    assert np.array_equal(got, want)
