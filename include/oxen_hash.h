@@ -65,7 +65,8 @@ void* oxh_ctx_stream(oxh_ctx* ctx);
  * Replaces N calls of `hash_buffer_128bit(&[u8]) -> u128` (hasher.rs:28-30) over buffers that are
  * already resident in HBM: item i is d_arena[d_offsets[i] .. d_offsets[i] + d_lens[i]).
  * d_offsets / d_lens / d_out are device pointers; d_out receives 2*n u64. Asynchronous on `stream`.
- * Buffers starting on a 16-byte boundary take the coalesced dwordx4 path; others stay correct. */
+ * Any start offset and length; starts off a dword boundary are loaded dword-aligned and re-aligned
+ * in registers. */
 int oxh_xxh3_128_batch_device(const void* d_arena, const uint64_t* d_offsets, const uint64_t* d_lens,
                               uint64_t n, uint64_t* d_out, int mode, void* stream);
 
@@ -83,9 +84,11 @@ int oxh_xxh3_128_large_device(oxh_ctx* ctx, const void* d_buf, uint64_t len, uin
 
 /* K1L over n large device-resident buffers (e.g. the 16 x 8 GiB files of the dedup experiment):
  * d_bufs and lens are HOST arrays of n device pointers / lengths; d_out (device) gets 2n u64.
- * Block sums run chip-wide per buffer, then up to 32 serial chains run concurrently in one launch.
- * The block sums live in the device's cached scratch buffer, so both K1L calls return only after
- * `stream` has finished them (calls on one device take the scratch in turn). */
+ * Buffers are processed in rounds of 1 GiB pieces: a round's block sums run chip-wide on `stream`
+ * while the previous round's serial chains (up to 32 per launch, resumed from piece to piece) run
+ * on a second stream. The block sums live in one of the device's two cached scratch buffers, so
+ * both K1L calls return only after `stream` has finished them (a third concurrent caller on the
+ * device waits for a buffer). */
 int oxh_xxh3_128_large_batch_device(const void* const* d_bufs, const uint64_t* lens, uint64_t n,
                                     uint64_t* d_out, void* stream);
 
