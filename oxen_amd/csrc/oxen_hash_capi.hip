@@ -237,6 +237,7 @@ struct oxh_ctx {
     hipEvent_t ev_bounce[2] = {};
     bool bounce_used[2] = {};
     hipEvent_t ev_piece_free[2] = {};
+    void* live = nullptr;  // the engine's current run (a FileStream, for diagnostics), under qmu
     std::vector<struct FileRequest*> rq[NSLOT];  // per staged item: its request and index in it
     std::vector<uint64_t> loc[NSLOT];
     hipEvent_t ev_copied[NSLOT] = {}, ev_done[NSLOT] = {};
@@ -921,7 +922,12 @@ int reserve(FileStream& fs, FileRequest* r, uint64_t i, uint64_t L, uint64_t roo
         SlotFill& sl = fs.slot[s];
         uint64_t w = sl.word.load(std::memory_order_acquire);
         if (w & kSealedBit) {  // full: wait for the sealer to open the next slot
-            while (fs.cur.load(std::memory_order_acquire) == s && !fs.abort.load(std::memory_order_relaxed)) pause_us(2);
+            // ... or for this slot's word to change: while this reader sleeps, the ring can go all
+            // the way round (small slots flushed early) and reopen slot s with cur == s again, and
+            // waiting on `cur` alone would then never end
+            while (fs.cur.load(std::memory_order_acquire) == s && sl.word.load(std::memory_order_acquire) == w &&
+                   !fs.abort.load(std::memory_order_relaxed))
+                pause_us(2);
             continue;
         }
         const uint64_t o = w_bytes(w), j = w_items(w);
@@ -1298,6 +1304,17 @@ int refresh_file(FileStream& fs, FileRequest* r, uint64_t i) {
 void run_stream(oxh_ctx* c) {
     FileStream fs;
     fs.c = c;
+    {
+        std::lock_guard<std::mutex> g(c->qmu);
+        c->live = &fs;
+    }
+    struct Unlive {
+        oxh_ctx* c;
+        ~Unlive() {
+            std::lock_guard<std::mutex> g(c->qmu);
+            c->live = nullptr;
+        }
+    } unlive{c};
     fs.slot[0].state.store(1);
     fs.slot[0].word.store(1ull << kGenShift);
     fs.nreaders = c->rpool->size();
@@ -1461,6 +1478,26 @@ void engine_main(oxh_ctx* c) {
 
 }  // namespace
 
+// A caller that has waited OXH_WAIT_LIMIT_S (default 60 s) for its request prints the engine's state
+// (once per period) and keeps waiting: the engine may still write into the request.
+static void dump_engine(oxh_ctx* c, const FileRequest& r) {
+    std::lock_guard<std::mutex> g(c->qmu);
+    fprintf(stderr, "[oxh] request stalled: n=%llu claimed=%llu remaining=%llu queue=%zu live=%d\n",
+            (unsigned long long)r.n, (unsigned long long)r.next, (unsigned long long)r.remaining.load(), c->queue.size(),
+            c->live != nullptr);
+    if (FileStream* fs = static_cast<FileStream*>(c->live)) {
+        fprintf(stderr, "[oxh]   run: readers=%d left=%d idle=%d closing=%d abort=%d cur=%d reqs=%zu cur_req=%zu oversize=%llu changed=%llu\n",
+                fs->nreaders, fs->readers_left.load(), fs->idle.load(), (int)fs->closing, (int)fs->abort.load(), fs->cur.load(),
+                fs->reqs.size(), fs->cur_req, (unsigned long long)fs->n_oversize.load(), (unsigned long long)fs->n_changed.load());
+        for (int k = 0; k < NSLOT; ++k) {
+            const uint64_t w = fs->slot[k].word.load();
+            fprintf(stderr, "[oxh]   slot %d: state=%d bytes=%llu items=%llu sealed=%d gen=%llu done=%llu\n", k,
+                    fs->slot[k].state.load(), (unsigned long long)w_bytes(w), (unsigned long long)w_items(w),
+                    (int)((w & kSealedBit) != 0), (unsigned long long)(w >> kGenShift), (unsigned long long)fs->slot[k].done.load());
+        }
+    }
+}
+
 static int hash_files_impl(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* sizes, int32_t* status,
                            uint64_t* counts, const ItemSink* sink = nullptr, int32_t* utf8 = nullptr,
                            const uint64_t* meta = nullptr) {
@@ -1484,8 +1521,13 @@ static int hash_files_impl(oxh_ctx* c, const char* const* paths, uint64_t n, uin
         c->queue.push_back(&r);
         c->qcv.notify_all();  // the engine (idle) or the live run's idle readers
     }
+    static const double limit = getenv("OXH_WAIT_LIMIT_S") ? atof(getenv("OXH_WAIT_LIMIT_S")) : 60.0;
     std::unique_lock<std::mutex> lk(r.mu);
-    r.cv.wait(lk, [&] { return r.done; });
+    while (!r.cv.wait_for(lk, std::chrono::duration<double>(limit), [&] { return r.done; })) {
+        lk.unlock();
+        dump_engine(c, r);
+        lk.lock();
+    }
     return r.rc ? fail(r.rc, r.msg) : OXH_OK;
 }
 

@@ -778,3 +778,55 @@ def test_k1_many_ragged_items(cuda, oracle_lib, mode):
     got = _u64(xxh3_128_batch_device(arena, o, ln, mode=m))
     want = oracle_lib.batch(arena.cpu().numpy(), offs, lens, threads=8)
     assert np.array_equal(got, want)
+
+
+def test_hash_files_path_edge_cases(oracle_lib, tmp_path, cuda):
+    """The same path many times in one call, non-ASCII and space-containing names, a symlink to a
+    file, a symlink to a directory, a FIFO-free special case (a directory) and empty files, through
+    the engine with tiny staging (many slots): digests/status as the reference loop sees them."""
+    from oxen_amd import _capi, hasher
+    from oxen_amd.workloads import splitmix_bytes
+
+    d = tmp_path / "dir with space"
+    d.mkdir()
+    files = []
+    for k, name in enumerate(["a.bin", "ünïcödé ✓.txt", "x y z", "empty"]):
+        p = d / name
+        p.write_bytes(b"" if name == "empty" else splitmix_bytes(60 + k, 0, 70_000 + k).tobytes())
+        files.append(str(p))
+    link = d / "link"
+    link.symlink_to(files[0])
+    dlink = d / "dlink"
+    dlink.symlink_to(d)
+    paths = files * 50 + [str(link), str(dlink), str(d)]
+    want_out, want_sizes, want_st = oracle_lib.hash_files(paths, threads=8)
+    with _capi.Context(0, staging_bytes=1 << 20) as c:
+        dg, sz, st = hasher.hash_files_128bit(paths, c)
+    assert [s != 0 for s in st] == [int(s) != 0 for s in want_st]
+    assert st[-2] != 0 and st[-1] != 0 and st[-3] == 0  # dirs fail, the file symlink is followed
+    for i, (lo, hi) in enumerate(want_out):
+        if st[i] == 0:
+            assert dg[i] == (int(hi) << 64) | int(lo), i
+            assert sz[i] == int(want_sizes[i]), i
+
+
+def test_engine_back_to_back_small_requests(oracle_lib, tmp_path, cuda):
+    """Regression: back-to-back calls on one context with tiny staging make the engine flush small
+    slots early, so the 3-slot ring can go all the way round while a reader sleeps; a reader waiting
+    for a sealed slot must notice the slot was reopened (it used to wait on the slot index alone and
+    hang). 300 calls x 203 paths, every result checked."""
+    from oxen_amd import _capi, hasher
+    from oxen_amd.workloads import splitmix_bytes
+
+    files = []
+    for k in range(4):
+        p = tmp_path / f"f{k}"
+        p.write_bytes(b"" if k == 3 else splitmix_bytes(60 + k, 0, 70_000 + k).tobytes())
+        files.append(str(p))
+    paths = files * 50 + [str(tmp_path), files[0], str(tmp_path / "missing")]
+    want_out, _, want_st = oracle_lib.hash_files(paths, threads=8)
+    want = [((int(hi) << 64) | int(lo)) if s == 0 else None for (lo, hi), s in zip(want_out, want_st)]
+    with _capi.Context(0, staging_bytes=1 << 20) as c:
+        for _ in range(300):
+            d, _, st = hasher.hash_files_128bit(paths, c)
+            assert d == want
