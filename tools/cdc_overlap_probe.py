@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--chunks", default="8192,65536")
     ap.add_argument("--groups", default="2,4,8")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--cu-split", default="0", help="comma list of k: stream A gets CUs with i %% 8 < k, "
+                    "stream B the rest (hipExtStreamCreateWithCUMask); 0 = unmasked torch streams")
     args = ap.parse_args()
 
     import torch
@@ -46,13 +48,28 @@ def main():
     offs = np.arange(args.files, dtype=np.uint64) * np.uint64(pitch)
     lens = np.full(args.files, size, dtype=np.uint64)
     total = size * args.files
-    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+
+    def masked_stream(bits):
+        words = (ctypes.c_uint32 * 8)()
+        for i in bits:
+            words[i // 32] |= 1 << (i % 32)
+        h = ctypes.c_void_p()
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), 8, words)
+        if rc != 0:
+            raise RuntimeError(f"hipExtStreamCreateWithCUMask: {rc}")
+        return h.value
+
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
     res = {"workload": f"{args.files} x {args.gib:g} GiB splitmix blobs, FastCDC v2020 + XXH3-128 per chunk",
            "bytes": total}
 
     def fp(dig, n):
         return (n, int(dig[:n].view(torch.int64).sum()) % 2**64)
 
+    splits = [int(k) for k in args.cu_split.split(",")]
     for chunk in [int(c) for c in args.chunks.split(",")]:
         mn, av, mx = 4096, chunk, 2 * chunk
         mode = _capi.OXH_MODE_WAVE_SHORT if av <= 16384 else _capi.OXH_MODE_WAVE
@@ -61,14 +78,19 @@ def main():
         for r in range(args.reps + 1):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            _, _, dig, first = fastcdc_device(arena, offs, lens, mn, av, mx, out=out, stream=sa)
+            _, _, dig, first = fastcdc_device(arena, offs, lens, mn, av, mx, out=out, stream=torch.cuda.current_stream())
             torch.cuda.synchronize()
             if r:
                 times.append(time.perf_counter() - t0)
         want = fp(dig, int(first[-1]))
         res[f"c{chunk}_serial_s"] = round(float(np.median(times)), 4)
         del out, dig
-        for G in [int(g) for g in args.groups.split(",")]:
+        for split, G in [(k, int(g)) for k in splits for g in args.groups.split(",")]:
+            if split:
+                sa = masked_stream([i for i in range(n_cu) if i % 8 < split])
+                sb = masked_stream([i for i in range(n_cu) if i % 8 >= split])
+            else:
+                sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
             groups = np.array_split(np.arange(args.files), G)
             outs = [fastcdc_outputs(arena, lens[g], mn) for g in groups]
             times, ok = [], True
@@ -88,8 +110,9 @@ def main():
                 n_all = sum(t[2] for t in tabs)
                 s_all = sum(int(outs[gi][2][: tabs[gi][2]].view(torch.int64).sum()) for gi in range(G))
                 ok = ok and (n_all, s_all % 2**64) == want
-            res[f"c{chunk}_overlap_g{G}_s"] = round(float(np.median(times)), 4)
-            res[f"c{chunk}_overlap_g{G}_same"] = ok
+            tag = f"c{chunk}_overlap_g{G}" + (f"_cu{split}of8" if split else "")
+            res[tag + "_s"] = round(float(np.median(times)), 4)
+            res[tag + "_same"] = ok
             del outs
         print(json.dumps(res), flush=True)
     res["GB"] = round(total / 1e9, 1)
