@@ -148,6 +148,55 @@ __global__ __launch_bounds__(64 * kWaves) void lanemajor_ilp(const uint8_t* __re
     atomicAdd(count, (unsigned long long)cnt);
 }
 
+// No LDS transpose: lane l loads its own region 128 B per round (8 x 16 B, one whole line per lane;
+// each wave load instruction touches 64 lines, the next 7 reuse them). Frees the LDS for COPIES
+// bank-private gear tables (32 copies: the 32 lanes of a ds_read_b64 group never share a bank).
+template <int kWaves, int COPIES>
+__global__ __launch_bounds__(64 * kWaves) void lanemajor_direct(const uint8_t* __restrict__ data, uint64_t n_sec,
+                                                              uint32_t ch, unsigned long long* __restrict__ count) {
+    __shared__ uint64_t gear_tab[256 * COPIES];
+    for (int i = threadIdx.x; i < 256 * COPIES; i += blockDim.x) gear_tab[i] = oxh::kGear[i / COPIES] << 16;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t* gear = gear_tab + (lane & (COPIES - 1));
+    const uint64_t sec = (uint64_t)blockIdx.x * kWaves + w;
+    if (sec >= n_sec) return;
+    const uint8_t* base = data + sec * kSec;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)kSec, 0x00020000);
+    auto load_round = [&](uint32_t r, uint4 (&dst)[8]) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t off = (uint32_t)lane * kRegion + r * 128 + 16 * k;
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, r < kRounds ? off : 0xFFFFF000u, 0, 2);
+            dst[k] = make_uint4(v.x, v.y, v.z, v.w);
+        }
+    };
+    uint64_t h = 0;
+    uint32_t cnt = 0;
+    uint4 ring[2][8];
+    load_round(0, ring[0]);
+    load_round(1, ring[1]);
+    for (uint32_t r = 0; r < kRounds; r += 2) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                uint32_t anyz = 0xFFFFFFFFu;
+#pragma unroll
+                for (int b = 0; b < 16; ++b) {
+                    h = (h << 1) + gear[byte_of(ring[q][g], b) * COPIES];
+                    const uint32_t t = (uint32_t)(h >> 32) & ch;
+                    anyz = anyz < t ? anyz : t;
+                }
+                cnt += anyz == 0;
+            }
+            load_round(r + q + 2, ring[q]);
+        }
+    }
+    atomicAdd(count, (unsigned long long)cnt);
+}
+
 int main(int argc, char** argv) {
     const double gib = argc > 1 ? atof(argv[1]) : 16.0;
     const uint64_t bytes = (uint64_t)(gib * 1073741824.0) / kSec * kSec, n_sec = bytes / kSec;
@@ -185,10 +234,9 @@ int main(int argc, char** argv) {
         fflush(stdout);
     };
     run(lanemajor<4, 1>, 4, "waves4_copies1");
-    run(lanemajor<8, 1>, 8, "waves8_copies1");
-    run(lanemajor_ilp<4, 2>, 4, "waves4_chains2");
-    run(lanemajor_ilp<2, 2>, 2, "waves2_chains2");
-    run(lanemajor_ilp<4, 4>, 4, "waves4_chains4");
-    run(lanemajor_ilp<2, 4>, 2, "waves2_chains4");
+    run(lanemajor_direct<4, 1>, 4, "direct_waves4_copies1");
+    run(lanemajor_direct<16, 32>, 16, "direct_waves16_copies32");
+    run(lanemajor_direct<8, 32>, 8, "direct_waves8_copies32");
+    run(lanemajor_direct<16, 16>, 16, "direct_waves16_copies16");
     return 0;
 }
