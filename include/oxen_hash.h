@@ -55,7 +55,11 @@ const char* oxh_last_error(void);
 /* Number of visible HIP devices (0 on a host without a GPU). */
 int oxh_device_count(int* count);
 /* Create a hashing context on `device`: owns a compute stream, a copy stream, pinned host staging
- * (`staging_bytes` per slot, 0 = default 256 MiB, 3 slots) and matching device slots. */
+ * (`staging_bytes` per slot, 0 = default 256 MiB, 3 slots) and matching device slots.
+ * staging_bytes above OXH_MAX_STAGING_BYTES fails with OXH_ERR_INVALID (a slot's fill state is one
+ * 64-bit word: 31 bits of byte offset, 19 bits of item count at one item per 4 KiB). Files of a
+ * slot's size or larger are streamed through the large-file path whatever the setting. */
+#define OXH_MAX_STAGING_BYTES 2147483392ull /* 2 GiB - 256 */
 int oxh_ctx_create(int device, uint64_t staging_bytes, oxh_ctx** out);
 int oxh_ctx_destroy(oxh_ctx* ctx);
 /* The context's compute stream (hipStream_t), for callers that want to order against it. */
@@ -101,7 +105,11 @@ int oxh_hash_buffers(oxh_ctx* ctx, const uint8_t* const* bufs, const uint64_t* l
 
 /* get_hash_given_metadata / u128_hash_file_contents x n (hasher.rs:56-65,102-112): reads each file
  * whole (parallel readers straight into pinned staging), overlaps H2D with hashing, and returns
- * digests, file sizes and a per-file status (OXH_OK or OXH_ERR_IO; digest 0 on error).
+ * digests, file sizes and a per-file status (OXH_OK; OXH_ERR_IO for a file that cannot be opened or
+ * read; OXH_ERR_NOMEM for a file larger than a staging slot whose device / pinned buffers cannot be
+ * allocated -- the other files of the call are unaffected; digest 0 on error). Files are read to
+ * EOF: one whose size differs from its stat (or, below, from the caller's size) is re-read, so the
+ * digest covers what the read returned, like read_to_end (hasher.rs:126-148).
  * `sizes` and `status` may be NULL. */
 int oxh_hash_files(oxh_ctx* ctx, const char* const* paths, uint64_t n, uint64_t* out,
                    uint64_t* sizes, int32_t* status);
@@ -116,11 +124,17 @@ int oxh_hash_files_meta(oxh_ctx* ctx, const char* const* paths, const uint64_t* 
 /* The add loop's hash and version-store copy, fused (add.rs:507-516, 718, 743;
  * storage/local.rs:104-121; util/fs/atomic_file.rs:363-463): each file is read ONCE into pinned
  * staging and hashed by K1; when its blob is not already in the store it is written from the same
- * pinned bytes to {versions_root}/{hex[..2]}/{hex[2..]}/data (hex = unpadded {:x}) via a temp file
- * + rename. The reference reads a new file three times and hashes it twice (verify-before-publish);
- * here the published bytes are the hashed bytes, so the check holds by construction.
- * stored[i] = 1 if a blob was written, 0 if it already existed or the file failed (see status:
- * OXH_ERR_IO for unreadable files or a failed publish). */
+ * pinned bytes to {versions_root}/{hex[..2]}/{hex[2..]}/data (hex = unpadded {:x}) through
+ * AtomicTempFile's protocol (util/fs/atomic_file.rs:54-159): a `data.oxentmp.<random>` sibling,
+ * data made durable, rename, rename made durable -- with one syncfs() per drained staging slot in
+ * place of an fsync per file and per parent. Files larger than a staging slot are streamed: each
+ * piece goes to the device and to a temp file in {versions_root} as it is read, and the temp is
+ * renamed into place once the digest is known (host memory stays bounded by the bounce buffers).
+ * The reference reads a new file three times and hashes it twice (verify-before-publish); here the
+ * published bytes are the hashed bytes, so the check holds by construction.
+ * Identical content in several items is published once. stored[i] = 1 for the item that wrote the
+ * blob, 0 otherwise. status[i] = OXH_ERR_IO (digest 0) for an unreadable file AND for every item
+ * whose content could not be published, OXH_ERR_NOMEM as for oxh_hash_files. */
 int oxh_add_files(oxh_ctx* ctx, const char* const* paths, uint64_t n, const char* versions_root,
                   uint64_t* out, uint64_t* sizes, int32_t* status, int32_t* stored);
 

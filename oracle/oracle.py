@@ -49,6 +49,8 @@ def lib():
         L.oxo_add_files.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_uint64, ctypes.c_char_p, _u64p, _u64p,
                                     _i32p, _i32p, ctypes.c_int]
         L.oxo_add_files.restype = None
+        L.oxo_set_add_sync.argtypes = [ctypes.c_int]
+        L.oxo_set_add_sync.restype = None
         L.oxo_chunk_digests.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, _u64p, ctypes.c_int]
         L.oxo_chunk_digests.restype = None
         L.oxo_format_hex.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_char_p]
@@ -103,9 +105,11 @@ def hash_files(paths: list[str], threads: int = 1):
     return out, sizes, status
 
 
-def add_files(paths: list[str], versions_root: str, threads: int = 1):
-    """Reference add loop restated (hash, then store_version_from_reader with verify-before-publish)."""
+def add_files(paths: list[str], versions_root: str, threads: int = 1, sync: bool = True):
+    """Reference add loop restated (hash, then store_version_from_reader with verify-before-publish,
+    AtomicTempFile's fsync of each blob and its parent; sync=False skips the fsyncs for timing A/Bs)."""
     n = len(paths)
+    lib().oxo_set_add_sync(1 if sync else 0)
     arr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
     out = np.zeros((n, 2), dtype=np.uint64)
     sizes = np.zeros(n, dtype=np.uint64)

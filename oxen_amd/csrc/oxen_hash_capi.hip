@@ -27,7 +27,9 @@
 #include <atomic>
 #include <condition_variable>
 #include <functional>
+#include <map>
 #include <mutex>
+#include <random>
 #include <set>
 #include <string>
 #include <thread>
@@ -391,9 +393,22 @@ struct Trace {
     }
 };
 
-// Called for every item of a drained slot whose digest is known, with the staged (pinned) bytes
-// still in place: lets a caller consume the exact bytes that were hashed (fused version-store copy).
-using ItemSink = std::function<void(uint64_t id, const uint8_t* bytes, uint64_t len, uint64_t lo, uint64_t hi)>;
+// Consumer of the exact bytes that were hashed (the fused version-store copy of oxh_add_files).
+//  * put(): an item whose digest is known, with its staged (pinned) bytes still in place; called
+//    from several threads at once for the items of a drained slot;
+//  * open_stream() / close_stream(): a file larger than a staging slot, whose bytes pass through
+//    bounce buffers piece by piece: the engine writes each piece to the returned fd while the
+//    digest is still being computed, then hands over the digest (or ok = false);
+//  * commit(): everything put / closed so far is made durable and visible; the engine calls it
+//    before the items' callers are released.
+// Publish failures are the sink's own business (oxh_add_files turns them into per-item statuses).
+struct ItemSink {
+    virtual ~ItemSink() = default;
+    virtual void put(uint64_t id, const uint8_t* bytes, uint64_t len, uint64_t lo, uint64_t hi) = 0;
+    virtual int open_stream(uint64_t id, std::string& tmp) = 0;
+    virtual void close_stream(uint64_t id, int fd, const std::string& tmp, bool ok, uint64_t lo, uint64_t hi) = 0;
+    virtual void commit() = 0;
+};
 
 struct Pending {
     bool busy = false;
@@ -486,7 +501,10 @@ int device_item(oxh_ctx* c, uint8_t* d, uint64_t len, uint64_t* out2, uint64_t* 
 int oversize_item(oxh_ctx* c, const uint8_t* src, uint64_t len, uint64_t* out2, uint64_t* cnt2 = nullptr,
                   int32_t* utf8_1 = nullptr) {
     uint8_t* d = nullptr;
-    if (hipMalloc(&d, align_up(len) + 256) != hipSuccess) return fail(OXH_ERR_NOMEM, "oversize hipMalloc failed");
+    if (hipMalloc(&d, align_up(len) + 256) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(OXH_ERR_NOMEM, "oversize hipMalloc failed");
+    }
     int rc = OXH_OK;
     if (hipMemcpyAsync(d, src, len, hipMemcpyHostToDevice, c->stream) != hipSuccess) rc = fail(OXH_ERR_HIP, "oversize H2D failed");
     if (rc == OXH_OK) rc = device_item(c, d, len, out2, cnt2, utf8_1);
@@ -514,6 +532,10 @@ int oxh_set_kernel_variant(int variant) { return g_variant.exchange(variant); }
 int oxh_ctx_create(int device, uint64_t staging_bytes, oxh_ctx** out) {
     if (!out) return fail(OXH_ERR_INVALID, "out is NULL");
     *out = nullptr;
+    // a slot's reservation word packs the byte offset into 31 bits and the item count into 19
+    // (stream_files below): both must hold a full slot
+    if (staging_bytes > OXH_MAX_STAGING_BYTES)
+        return fail(OXH_ERR_INVALID, "staging_bytes exceeds OXH_MAX_STAGING_BYTES (2 GiB - 256)");
     int rc = check_device(device);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(device));
@@ -762,6 +784,8 @@ constexpr int kWBytes = 31, kWItems = 19;
 constexpr uint64_t kBytesMask = (1ull << kWBytes) - 1, kItemsMask = (1ull << kWItems) - 1;
 constexpr uint64_t kSealedBit = 1ull << (kWBytes + kWItems);
 constexpr int kGenShift = kWBytes + kWItems + 1;
+static_assert(OXH_MAX_STAGING_BYTES <= kBytesMask, "a full slot's byte offset must fit the word");
+static_assert(OXH_MAX_STAGING_BYTES / 4096 <= kItemsMask, "a full slot's item count must fit the word");
 inline uint64_t w_bytes(uint64_t w) { return w & kBytesMask; }
 inline uint64_t w_items(uint64_t w) { return (w >> kWBytes) & kItemsMask; }
 
@@ -789,7 +813,7 @@ struct FileRequest {
     int32_t* status = nullptr;
     uint64_t* counts = nullptr;
     int32_t* utf8 = nullptr;
-    const ItemSink* sink = nullptr;
+    ItemSink* sink = nullptr;
     std::vector<uint64_t> lens;
     std::vector<int32_t> st;
     uint64_t next = 0;                   // claim cursor (under ctx->qmu)
@@ -963,8 +987,10 @@ void reader_loop(FileStream& fs) {
                 ++failed;
                 continue;
             }
-            // with the caller's metadata size no fstat is needed: read one byte more than expected
-            // and re-read the file (fstat + whole read) if the size turns out different
+            // with the caller's metadata size no fstat is needed. Either way the reader asks for one
+            // byte more than the expected size L and re-reads the file (fstat + whole read) if it
+            // gets a different count: a file that grew or shrank since its size was taken is hashed
+            // as it is at read time, like the reference's read_to_end (hasher.rs:126-148)
             const bool meta = r->meta != nullptr && r->meta[i] < c->stage_bytes;
             if (!meta && (fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode))) {
                 close(fd);
@@ -974,7 +1000,7 @@ void reader_loop(FileStream& fs) {
             }
             const uint64_t L = meta ? r->meta[i] : (uint64_t)sb.st_size;
             r->lens[i] = L;
-            if (L > c->stage_bytes) {  // the engine reads it through the oversize path
+            if (L >= c->stage_bytes) {  // the engine reads it through the oversize path (L + 1 > a slot)
                 close(fd);
                 {
                     std::lock_guard<std::mutex> g(fs.omu);
@@ -985,26 +1011,29 @@ void reader_loop(FileStream& fs) {
                 continue;
             }
             uint64_t off = 0, j = 0;
-            const int s = reserve(fs, r, i, L, meta ? L + 1 : L, off, j);
+            const int s = reserve(fs, r, i, L, L + 1, off, j);
             if (s < 0) {
                 close(fd);
                 stop = true;  // aborted: the engine fails every open request
                 break;
             }
             uint8_t* dst = c->h_stage[s] + off;
-            const uint64_t want = meta ? L + 1 : L;
+            const uint64_t want = L + 1;
             uint64_t got = 0;
             while (got < want) {
                 const ssize_t k = pread(fd, dst + got, want - got, (off_t)got);
-                if (k < 0 || (k == 0 && !meta)) {
+                if (k < 0) {
                     r->st[i] = OXH_ERR_IO;
                     break;
                 }
                 if (k == 0) break;  // EOF
                 got += (uint64_t)k;
+                // a short read of a regular file ends at its EOF: once the expected L bytes are in,
+                // that settles the size without the extra pread that would return 0
+                if (got >= L && (uint64_t)k < want - (got - (uint64_t)k)) break;
             }
             close(fd);
-            if (meta && r->st[i] == OXH_OK && got != L) {  // the file is not the size the caller saw
+            if (r->st[i] == OXH_OK && got != L) {  // the file is not the size the stat / the caller saw
                 c->rq[s][j] = nullptr;                     // drain skips this slot entry
                 {
                     std::lock_guard<std::mutex> g(fs.omu);
@@ -1030,7 +1059,7 @@ void drain_files(FileStream& fs, int s, const SlotRun& p) {
     const uint64_t M = c->max_items, cnt = p.cnt;
     FileRequest* const* rq = c->rq[s].data();
     const uint64_t* loc = c->loc[s].data();
-    bool any_sink = false;
+    std::vector<ItemSink*> sinks;  // the distinct sinks of this slot's requests
     for (uint64_t j = 0; j < cnt; ++j) {
         FileRequest* r = rq[j];
         if (!r) continue;  // re-read later (its size changed)
@@ -1042,9 +1071,9 @@ void drain_files(FileStream& fs, int s, const SlotRun& p) {
             r->counts[2 * i + 1] = c->h_cnt[s][2 * j + 1];
         }
         if (r->utf8 && p.utf8) r->utf8[i] = c->h_utf8[s][j];
-        any_sink |= r->sink != nullptr;
+        if (r->sink && std::find(sinks.begin(), sinks.end(), r->sink) == sinks.end()) sinks.push_back(r->sink);
     }
-    if (any_sink) {
+    if (!sinks.empty()) {
         if (!c->wpool) c->wpool = new oxh::Pool(c->pool->size());
         const int ntasks = (int)std::min<uint64_t>(cnt, (uint64_t)c->wpool->size() * 4);
         c->wpool->parallel_for(ntasks, [&](int t) {
@@ -1053,9 +1082,10 @@ void drain_files(FileStream& fs, int s, const SlotRun& p) {
                 if (!r) continue;
                 const uint64_t i = loc[j];
                 if (!r->sink || r->st[i] != OXH_OK) continue;
-                (*r->sink)(i, c->h_stage[s] + c->h_desc[s][j], c->h_desc[s][M + j], c->h_out[s][2 * j], c->h_out[s][2 * j + 1]);
+                r->sink->put(i, c->h_stage[s] + c->h_desc[s][j], c->h_desc[s][M + j], c->h_out[s][2 * j], c->h_out[s][2 * j + 1]);
             }
         });
+        for (ItemSink* k : sinks) k->commit();  // one durability barrier per slot, not per file
     }
     for (uint64_t j = 0; j < cnt;) {  // one atomic per run of items of the same request
         uint64_t k = j + 1;
@@ -1087,6 +1117,14 @@ int big_file(FileStream& fs, FileRequest* r, uint64_t i) {
     const uint64_t k = L > P + 1024 ? (L - 1025) / P : 0;
     const uint64_t cap = P + 1024;  // bytes per piece buffer
     const uint64_t slot = align_up(cap) + 256;
+    // an allocation that fails is this file's failure (status OXH_ERR_NOMEM), not the engine run's:
+    // the other requests in the live pipeline carry on
+    auto item_nomem = [&]() {
+        r->st[i] = OXH_ERR_NOMEM;
+        if (r->sink) r->sink->close_stream(i, -1, std::string(), false, 0, 0);
+        account(fs, r, 1);
+        return OXH_OK;
+    };
     if (c->d_big_size < 2 * slot + 4096) {
         if (c->d_big) {
             HIP_TRY(hipDeviceSynchronize());
@@ -1094,7 +1132,11 @@ int big_file(FileStream& fs, FileRequest* r, uint64_t i) {
             c->d_big = nullptr;
             c->d_big_size = 0;
         }
-        if (hipMalloc(&c->d_big, 2 * slot + 4096) != hipSuccess) return fail(OXH_ERR_NOMEM, "large-file device buffers");
+        if (hipMalloc(&c->d_big, 2 * slot + 4096) != hipSuccess) {
+            c->d_big = nullptr;
+            (void)hipGetLastError();
+            return item_nomem();
+        }
         c->d_big_size = 2 * slot + 4096;
     }
     uint8_t* dbuf[2] = {c->d_big, c->d_big + slot};
@@ -1106,23 +1148,39 @@ int big_file(FileStream& fs, FileRequest* r, uint64_t i) {
     } h{};
     h.len = L;
     for (int b = 0; b < 2; ++b) {
-        if (!c->h_bounce[b] && hipHostMalloc(&c->h_bounce[b], kBounce, hipHostMallocDefault) != hipSuccess)
-            return fail(OXH_ERR_NOMEM, "large-file bounce buffer");
+        if (!c->h_bounce[b] && hipHostMalloc(&c->h_bounce[b], kBounce, hipHostMallocDefault) != hipSuccess) {
+            c->h_bounce[b] = nullptr;
+            (void)hipGetLastError();
+            return item_nomem();
+        }
         if (!c->ev_bounce[b]) HIP_TRY(hipEventCreateWithFlags(&c->ev_bounce[b], hipEventDisableTiming));
         if (!c->ev_piece_free[b]) HIP_TRY(hipEventCreateWithFlags(&c->ev_piece_free[b], hipEventDisableTiming));
     }
     uint64_t* sums = nullptr;
     oxh::ScratchLease lease(c->stream);  // block sums of the two pieces in flight
     const uint64_t sums_per = (cap >> 10) * 8;
-    HIP_TRY(lease.get(2 * sums_per * 8, (void**)&sums));
+    if (lease.get(2 * sums_per * 8, (void**)&sums) != hipSuccess) {
+        (void)hipGetLastError();
+        return item_nomem();
+    }
     HIP_TRY(hipMemcpyAsync(d_res, &h, sizeof h, hipMemcpyHostToDevice, c->stream));
 
     int rc = OXH_OK;
     bool io_ok = true, piece_used[2] = {false, false};
     const int fd = open(r->paths[i], O_RDONLY | O_CLOEXEC | O_NONBLOCK);
     if (fd < 0) io_ok = false;
+    // fused add: the sink gets every bounce piece as it is read (a temp blob written while the chain
+    // runs), so the file never needs to fit in host memory; it publishes once the digest is known
+    ItemSink* sink = r->sink;
+    std::string sink_tmp;
+    int sfd = -1;
+    std::atomic<bool> sink_ok{true};
+    if (sink && io_ok) {
+        sfd = sink->open_stream(i, sink_tmp);
+        if (sfd < 0) sink_ok.store(false);
+    }
     uint8_t* map = nullptr;
-    if (io_ok) {
+    if (io_ok && !sink) {  // copy-free pieces would not pass through host memory the sink can read
         void* m = mmap(nullptr, L, PROT_READ, MAP_SHARED, fd, 0);
         if (m != MAP_FAILED) {
             map = (uint8_t*)m;
@@ -1167,6 +1225,15 @@ int big_file(FileStream& fs, FileRequest* r, uint64_t i) {
                     }
                     got += (uint64_t)x;
                 }
+                if (sfd >= 0 && sink_ok.load(std::memory_order_relaxed))  // the same bytes to the temp blob
+                    for (uint64_t put = lo; put < hi;) {
+                        const ssize_t x = pwrite(sfd, c->h_bounce[bb] + put, hi - put, (off_t)(off + o + put));
+                        if (x <= 0) {
+                            sink_ok.store(false);
+                            break;
+                        }
+                        put += (uint64_t)x;
+                    }
             });
             if (bad.load()) return false;
             if (hipMemcpyAsync(dbuf[b] + o, c->h_bounce[bb], n, hipMemcpyHostToDevice, c->copy_stream) != hipSuccess ||
@@ -1213,6 +1280,10 @@ int big_file(FileStream& fs, FileRequest* r, uint64_t i) {
     if (rc == OXH_OK && hipMemcpyAsync(&h, d_res, sizeof h, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
         rc = fail(OXH_ERR_HIP, "large-file results D2H");
     if (hipStreamSynchronize(c->stream) != hipSuccess && rc == OXH_OK) rc = fail(OXH_ERR_HIP, "large-file sync");
+    if (sink) {  // publish (or drop) the temp blob now that the digest is known
+        sink->close_stream(i, sfd, sink_tmp, rc == OXH_OK && io_ok && sink_ok.load(), h.out[0], h.out[1]);
+        sink->commit();
+    }
     if (rc) return rc;
     if (!io_ok) {
         r->st[i] = OXH_ERR_IO;
@@ -1229,38 +1300,12 @@ int big_file(FileStream& fs, FileRequest* r, uint64_t i) {
     return OXH_OK;
 }
 
-// Oversize file of a request with a sink (fused add): the sink needs the whole file in host memory.
-int oversize_file(FileStream& fs, FileRequest* r, uint64_t i) {
-    oxh_ctx* c = fs.c;
-    if (!r->sink) return big_file(fs, r, i);
-    const uint64_t L = r->lens[i];
-    std::vector<uint8_t> tmp(L);
-    const int fd = open(r->paths[i], O_RDONLY | O_CLOEXEC | O_NONBLOCK);
-    uint64_t got = 0;
-    if (fd >= 0) {
-        while (got < L) {
-            const ssize_t k = pread(fd, tmp.data() + got, L - got, (off_t)got);
-            if (k <= 0) break;
-            got += (uint64_t)k;
-        }
-        close(fd);
-    }
-    if (got != L) {
-        r->st[i] = OXH_ERR_IO;
-    } else {
-        int32_t u8 = 0;
-        const int rc = oversize_item(c, tmp.data(), L, r->out + 2 * i, r->counts ? r->counts + 2 * i : nullptr,
-                                     r->utf8 ? &u8 : nullptr);
-        if (rc) return rc;
-        if (r->utf8) r->utf8[i] = u8;
-        if (r->sink) (*r->sink)(i, tmp.data(), L, r->out[2 * i], r->out[2 * i + 1]);
-    }
-    account(fs, r, 1);
-    return OXH_OK;
-}
+// A file larger than a staging slot, with or without a sink: streamed in pieces (big_file).
+int oversize_file(FileStream& fs, FileRequest* r, uint64_t i) { return big_file(fs, r, i); }
 
-// A file whose size differed from the caller's metadata: stat and read it afresh (the reference
-// reads whatever the file holds, hasher.rs:126-148).
+// A file whose size changed between the stat (or the caller's metadata) and the read: stat and read
+// it afresh (the reference reads whatever the file holds, hasher.rs:126-148). It fits a staging
+// slot, so the host copy is bounded by the slot size.
 int refresh_file(FileStream& fs, FileRequest* r, uint64_t i) {
     oxh_ctx* c = fs.c;
     struct stat sb;
@@ -1273,27 +1318,51 @@ int refresh_file(FileStream& fs, FileRequest* r, uint64_t i) {
     }
     const uint64_t L = (uint64_t)sb.st_size;
     r->lens[i] = L;
-    if (L > c->stage_bytes) {
+    if (L >= c->stage_bytes) {
         close(fd);
         return oversize_file(fs, r, i);
     }
-    std::vector<uint8_t> tmp(std::max<uint64_t>(L, 1));
+    // read to EOF (read_to_end), whatever the stat said: st_size is a hint (a file still being
+    // written, or one whose size the stat does not report, like /proc files with st_size 0)
+    std::vector<uint8_t> tmp(std::max<uint64_t>(L + 1, 4096));
     uint64_t got = 0;
-    while (got < L) {
-        const ssize_t k = pread(fd, tmp.data() + got, L - got, (off_t)got);
+    bool bad = false;
+    for (;;) {
+        if (got == tmp.size()) {
+            if (tmp.size() >= c->stage_bytes) break;  // grew past a staging slot meanwhile
+            tmp.resize(std::min<uint64_t>(2 * tmp.size(), c->stage_bytes));
+        }
+        const ssize_t k = pread(fd, tmp.data() + got, tmp.size() - got, (off_t)got);
+        if (k < 0) bad = true;
         if (k <= 0) break;
         got += (uint64_t)k;
     }
+    if (!bad && got == tmp.size()) {  // larger than a slot now: the streamed large-file path
+        close(fd);
+        struct stat sb2;
+        r->lens[i] = stat(r->paths[i], &sb2) == 0 ? std::max<uint64_t>((uint64_t)sb2.st_size, got) : got;
+        return oversize_file(fs, r, i);
+    }
     close(fd);
-    if (got != L) {
+    r->lens[i] = got;
+    if (bad) {
         r->st[i] = OXH_ERR_IO;
     } else {
+        const uint64_t L = got;
         int32_t u8 = 0;
-        if (int rc = oversize_item(c, tmp.data(), L, r->out + 2 * i, r->counts ? r->counts + 2 * i : nullptr,
-                                   r->utf8 ? &u8 : nullptr))
+        const int rc = oversize_item(c, tmp.data(), L, r->out + 2 * i, r->counts ? r->counts + 2 * i : nullptr,
+                                     r->utf8 ? &u8 : nullptr);
+        if (rc == OXH_ERR_NOMEM) {
+            r->st[i] = OXH_ERR_NOMEM;  // this file's failure, not the run's
+        } else if (rc) {
             return rc;
-        if (r->utf8) r->utf8[i] = u8;
-        if (r->sink) (*r->sink)(i, tmp.data(), L, r->out[2 * i], r->out[2 * i + 1]);
+        } else {
+            if (r->utf8) r->utf8[i] = u8;
+            if (r->sink) {
+                r->sink->put(i, tmp.data(), L, r->out[2 * i], r->out[2 * i + 1]);
+                r->sink->commit();
+            }
+        }
     }
     account(fs, r, 1);
     return OXH_OK;
@@ -1499,7 +1568,7 @@ static void dump_engine(oxh_ctx* c, const FileRequest& r) {
 }
 
 static int hash_files_impl(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* sizes, int32_t* status,
-                           uint64_t* counts, const ItemSink* sink = nullptr, int32_t* utf8 = nullptr,
+                           uint64_t* counts, ItemSink* sink = nullptr, int32_t* utf8 = nullptr,
                            const uint64_t* meta = nullptr) {
     if (!c || (n && (!paths || !out))) return fail(OXH_ERR_INVALID, "bad arguments");
     if (n == 0) return OXH_OK;
@@ -1554,70 +1623,225 @@ int oxh_hash_files_text_utf8(oxh_ctx* c, const char* const* paths, uint64_t n, u
     return hash_files_impl(c, paths, n, out, sizes, status, counts, nullptr, is_utf8);
 }
 
-// Publish `data` as the version blob of digest (lo, hi): {root}/{hex[..2]}/{hex[2..]}/data
-// (storage/local.rs:66-75), skipped when present (local.rs:112), written as tmp + rename so a reader
-// never sees a partial blob (util/fs/atomic_file.rs). Returns 1 if written, 0 if it existed, <0 on error.
-static int store_version_blob(const std::string& root, uint64_t lo, uint64_t hi, const uint8_t* data, uint64_t len) {
-    char hex[40];
-    const int hl = oxh_format_hex(lo, hi, hex);
-    const std::string top = root + "/" + std::string(hex, std::min(hl, 2));
-    const std::string dir = top + "/" + std::string(hex + std::min(hl, 2));
-    const std::string path = dir + "/data";
-    struct stat sb;
-    if (stat(path.c_str(), &sb) == 0) return 0;
-    if (mkdir(top.c_str(), 0755) != 0 && errno != EEXIST) {
-        // first blob under a new root: create the root's missing parents too (mkdir -p)
-        for (size_t i = 1; i <= root.size(); ++i)
-            if (i == root.size() || root[i] == '/') {
-                const std::string part = root.substr(0, i);
-                if (mkdir(part.c_str(), 0755) != 0 && errno != EEXIST) return -1;
-            }
-        if (mkdir(top.c_str(), 0755) != 0 && errno != EEXIST) return -1;
-    }
-    if (mkdir(dir.c_str(), 0755) != 0 && errno != EEXIST) return -1;
-    static std::atomic<uint64_t> seq{0};
-    const std::string tmp = dir + "/.data.tmp." + std::to_string((long)getpid()) + "." + std::to_string(seq.fetch_add(1));
-    const int fd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_EXCL | O_CLOEXEC, 0644);
-    if (fd < 0) return -1;
-    uint64_t put = 0;
-    while (put < len) {
-        const ssize_t w = write(fd, data + put, len - put);
-        if (w <= 0) {
-            close(fd);
-            unlink(tmp.c_str());
-            return -1;
+namespace {
+
+// mkdir -p (std::fs::create_dir_all)
+bool mkdir_p(const std::string& dir) {
+    if (mkdir(dir.c_str(), 0755) == 0 || errno == EEXIST) return true;
+    if (errno != ENOENT) return false;
+    for (size_t i = 1; i <= dir.size(); ++i)
+        if (i == dir.size() || dir[i] == '/') {
+            const std::string part = dir.substr(0, i);
+            if (mkdir(part.c_str(), 0755) != 0 && errno != EEXIST) return false;
         }
-        put += (uint64_t)w;
-    }
-    if (close(fd) != 0 || rename(tmp.c_str(), path.c_str()) != 0) {
-        unlink(tmp.c_str());
-        return -1;
-    }
-    return 1;
+    return true;
 }
+
+// A new temp file `{dir}/data.oxentmp.<random>` (AtomicTempFile's `<target_basename>.oxentmp.<random>`,
+// util/fs/atomic_file.rs:21-25,58-96, so liboxen's leftover handling recognises it); -1 on failure.
+int make_temp(const std::string& dir, std::string& tmp) {
+    static const char an[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789";
+    thread_local uint64_t x = [] {
+        std::random_device rd;
+        return ((uint64_t)rd() << 32) ^ rd() ^ (uint64_t)std::hash<std::thread::id>()(std::this_thread::get_id());
+    }();
+    for (int attempt = 0; attempt < 32; ++attempt) {
+        tmp = dir + "/data.oxentmp.";
+        for (int k = 0; k < 8; ++k) {  // splitmix64 steps
+            uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+            z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+            z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+            tmp += an[(z ^ (z >> 31)) % 62];
+        }
+        const int fd = open(tmp.c_str(), O_RDWR | O_CREAT | O_EXCL | O_CLOEXEC, 0644);
+        if (fd >= 0 || errno != EEXIST) return fd;
+    }
+    return -1;
+}
+
+// The version-store half of the fused add: LocalVersionStore::store_version_from_reader
+// (storage/local.rs:104-121) publishing through AtomicTempFile (util/fs/atomic_file.rs:54-159) --
+// write a `data.oxentmp.<random>` sibling, make the data durable, rename it to
+// {root}/{hex[..2]}/{hex[2..]}/data (local.rs:66-75), make the rename durable; a blob already in the
+// store is not rewritten (local.rs:112). AtomicTempFile::commit fsyncs each file and its parent; here
+// one syncfs() per drained slot covers every temp of the slot before any of them is renamed, and a
+// second one covers the renames -- the same ordering, two barriers per slot instead of two per file.
+// Identical content twice in one call is published once; every duplicate shares that publish's
+// outcome (finish()).
+class VersionPublisher final : public ItemSink {
+   public:
+    VersionPublisher(oxh_ctx* c, std::string root, uint64_t n) : c_(c), root_(std::move(root)), owner_(n, kNone), result_(n, 0) {}
+    ~VersionPublisher() override {
+        if (root_fd_ >= 0) close(root_fd_);
+    }
+
+    void put(uint64_t id, const uint8_t* bytes, uint64_t len, uint64_t lo, uint64_t hi) override {
+        if (!claim(id, lo, hi)) return;
+        std::string dir, path;
+        target(lo, hi, dir, path);
+        struct stat sb;
+        if (stat(path.c_str(), &sb) == 0) {
+            result_[id] = kExisted;
+            return;
+        }
+        std::string tmp;
+        const int fd = mkdir_p(dir) ? make_temp(dir, tmp) : -1;
+        if (fd < 0) {
+            result_[id] = kFailed;
+            return;
+        }
+        bool ok = true;
+        for (uint64_t done = 0; ok && done < len;) {
+            const ssize_t w = write(fd, bytes + done, len - done);
+            if (w <= 0) ok = false;
+            else done += (uint64_t)w;
+        }
+        if (close(fd) != 0) ok = false;
+        if (!ok) {
+            unlink(tmp.c_str());
+            result_[id] = kFailed;
+            return;
+        }
+        stage(id, tmp, path);
+    }
+
+    // a streamed file's temp lives in the root until its digest names the target directory
+    int open_stream(uint64_t, std::string& tmp) override { return mkdir_p(root_) ? make_temp(root_, tmp) : -1; }
+
+    void close_stream(uint64_t id, int fd, const std::string& tmp, bool ok, uint64_t lo, uint64_t hi) override {
+        if (fd >= 0 && close(fd) != 0) ok = false;
+        if (!ok || fd < 0) {
+            if (!tmp.empty()) unlink(tmp.c_str());
+            owner_[id] = id;
+            result_[id] = kFailed;
+            return;
+        }
+        if (!claim(id, lo, hi)) {
+            unlink(tmp.c_str());
+            return;
+        }
+        std::string dir, path;
+        target(lo, hi, dir, path);
+        struct stat sb;
+        if (stat(path.c_str(), &sb) == 0) {
+            unlink(tmp.c_str());
+            result_[id] = kExisted;
+        } else if (!mkdir_p(dir)) {
+            unlink(tmp.c_str());
+            result_[id] = kFailed;
+        } else {
+            stage(id, tmp, path);
+        }
+    }
+
+    void commit() override {
+        std::vector<Staged> batch;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            batch.swap(staged_);
+        }
+        if (batch.empty()) return;
+        // 1. the data of every temp is durable before any rename (AtomicTempFile::commit's sync_all,
+        //    atomic_file.rs:122); should syncfs fail, each temp is fsynced on its own
+        const bool synced = sync_fs();
+        auto each = [&](const std::function<void(Staged&)>& fn) {
+            if (batch.size() < 64) {
+                for (Staged& s : batch) fn(s);
+                return;
+            }
+            if (!c_->wpool) c_->wpool = new oxh::Pool(c_->pool->size());
+            const int ntasks = (int)std::min<size_t>(batch.size(), (size_t)c_->wpool->size() * 4);
+            c_->wpool->parallel_for(ntasks, [&](int t) {
+                for (size_t k = (size_t)t; k < batch.size(); k += (size_t)ntasks) fn(batch[k]);
+            });
+        };
+        each([&](Staged& s) {
+            bool ok = true;
+            if (!synced) {
+                const int fd = open(s.tmp.c_str(), O_RDONLY | O_CLOEXEC);
+                ok = fd >= 0 && fsync(fd) == 0;
+                if (fd >= 0) close(fd);
+            }
+            // 2. publish (atomic_file.rs:132-139): a failed rename removes the temp
+            if (ok && rename(s.tmp.c_str(), s.path.c_str()) == 0) {
+                result_[s.id] = kWritten;
+            } else {
+                unlink(s.tmp.c_str());
+                result_[s.id] = kFailed;
+            }
+        });
+        // 3. the renames themselves, best effort like the reference's parent fsync (:141-156)
+        (void)sync_fs();
+    }
+
+    // Per-item outcome into the caller's arrays: a file whose content failed to publish (its own
+    // publish or the one its duplicate claimed) fails with OXH_ERR_IO and digest 0, like the
+    // reference's add of that file (add.rs:533-544).
+    void finish(uint64_t n, uint64_t* out, int32_t* status, int32_t* stored) const {
+        for (uint64_t i = 0; i < n; ++i) {
+            stored[i] = 0;
+            if (status[i] != OXH_OK) continue;
+            const uint64_t o = owner_[i];
+            if (o == kNone || result_[o] == kFailed) {
+                status[i] = OXH_ERR_IO;
+                out[2 * i] = out[2 * i + 1] = 0;
+                continue;
+            }
+            stored[i] = (o == i && result_[o] == kWritten) ? 1 : 0;
+        }
+    }
+
+   private:
+    static constexpr uint64_t kNone = ~0ull;
+    static constexpr int8_t kExisted = 0, kWritten = 1, kFailed = -1;
+    struct Staged {
+        uint64_t id;
+        std::string tmp, path;
+    };
+
+    // the first item with this digest publishes it; the others share its outcome
+    bool claim(uint64_t id, uint64_t lo, uint64_t hi) {
+        std::lock_guard<std::mutex> g(mu_);
+        const auto it = owner_of_.emplace(std::make_pair(lo, hi), id).first;
+        owner_[id] = it->second;
+        return it->second == id;
+    }
+    void target(uint64_t lo, uint64_t hi, std::string& dir, std::string& path) const {
+        char hex[40];
+        const int hl = oxh_format_hex(lo, hi, hex);
+        const int p = std::min(hl, 2);
+        dir = root_ + "/" + std::string(hex, p) + "/" + std::string(hex + p);
+        path = dir + "/data";
+    }
+    void stage(uint64_t id, const std::string& tmp, const std::string& path) {
+        std::lock_guard<std::mutex> g(mu_);
+        staged_.push_back({id, tmp, path});
+    }
+    bool sync_fs() {
+        if (root_fd_ < 0) root_fd_ = open(root_.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+        return root_fd_ >= 0 && syncfs(root_fd_) == 0;
+    }
+
+    oxh_ctx* c_;
+    std::string root_;
+    std::mutex mu_;
+    std::map<std::pair<uint64_t, uint64_t>, uint64_t> owner_of_;
+    std::vector<uint64_t> owner_;  // per item: the item that publishes its content (itself if first)
+    std::vector<int8_t> result_;   // per publishing item: kWritten / kExisted / kFailed
+    std::vector<Staged> staged_;   // temps written, waiting for commit()
+    int root_fd_ = -1;
+};
+
+}  // namespace
 
 int oxh_add_files(oxh_ctx* c, const char* const* paths, uint64_t n, const char* versions_root, uint64_t* out,
                   uint64_t* sizes, int32_t* status, int32_t* stored) {
     if (n && (!versions_root || !stored || !status)) return fail(OXH_ERR_INVALID, "versions_root/status/stored is NULL");
-    const std::string root(versions_root ? versions_root : "");
     for (uint64_t i = 0; i < n; ++i) stored[i] = 0;
-    std::vector<uint8_t> pub_err(n, 0);
-    // identical content twice in one call: exactly one item publishes (the others find it claimed)
-    std::mutex claim_mu;
-    std::set<std::pair<uint64_t, uint64_t>> claimed;
-    ItemSink sink = [&](uint64_t id, const uint8_t* bytes, uint64_t len, uint64_t lo, uint64_t hi) {
-        {
-            std::lock_guard<std::mutex> g(claim_mu);
-            if (!claimed.insert({lo, hi}).second) return;
-        }
-        const int r = store_version_blob(root, lo, hi, bytes, len);
-        stored[id] = r > 0 ? 1 : 0;
-        if (r < 0) pub_err[id] = 1;
-    };
-    const int rc = hash_files_impl(c, paths, n, out, sizes, status, nullptr, &sink);
+    VersionPublisher pub(c, versions_root ? versions_root : "", n);
+    const int rc = hash_files_impl(c, paths, n, out, sizes, status, nullptr, &pub);
     if (rc) return rc;
-    for (uint64_t i = 0; i < n; ++i)
-        if (pub_err[i]) status[i] = OXH_ERR_IO;  // could not publish the blob: the add of this file fails
+    pub.finish(n, out, status, stored);
     return OXH_OK;
 }
 

@@ -58,3 +58,14 @@ def test_no_cpu_fallback_without_device(built_lib):
 
     with pytest.raises(_capi.OxenError):
         hasher.hash_buffer(b"hello")
+
+
+def test_staging_limit_is_rejected_before_any_device_work(built_lib):
+    """staging_bytes above OXH_MAX_STAGING_BYTES would overflow a slot's packed fill word (31-bit byte
+    offset, 19-bit item count): ctx_create refuses it with OXH_ERR_INVALID, GPU or not."""
+    assert _capi.OXH_MAX_STAGING_BYTES == (1 << 31) - 256
+    assert _capi.OXH_MAX_STAGING_BYTES // 4096 < (1 << 19)
+    for bad in [_capi.OXH_MAX_STAGING_BYTES + 1, 1 << 31, 1 << 40]:
+        with pytest.raises(_capi.OxenError) as e:
+            _capi.Context(0, staging_bytes=bad)
+        assert e.value.code == _capi.OXH_ERR_INVALID, e.value

@@ -1,0 +1,136 @@
+"""The fused add's version-store publish and the file engine's failure isolation, through the C ABI.
+
+Covers the round-1 advisor findings: oversize files streamed into a `data.oxentmp.<random>` temp
+(never whole in host memory), per-file allocation failures as per-item statuses (the live run keeps
+going), a failed publish shared by every duplicate of that content, read-to-EOF semantics for files
+whose stat size is wrong, and a context at the staging-size limit.
+"""
+import os
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+BIG_SIZES = [(9 << 20) + 17, (6 << 20) + 3]  # > the 4 MiB staging slots below
+
+
+def _small(k):
+    from oxen_amd.workloads import splitmix_bytes
+
+    return splitmix_bytes(500 + k, 0, 70_000 + k).tobytes()
+
+
+def _big(k):
+    from oxen_amd.workloads import splitmix_bytes
+
+    return splitmix_bytes(700 + k, 0, BIG_SIZES[k]).tobytes()
+
+
+def _write(tmp_path, name, data):
+    p = tmp_path / name
+    p.write_bytes(data)
+    return str(p)
+
+
+def _tree(root):
+    return sorted(os.path.relpath(os.path.join(dp, f), root) for dp, _, fs in os.walk(root) for f in fs)
+
+
+def test_add_files_streams_oversize_blobs_and_shares_publish_failures(cuda, oracle_lib, tmp_path):
+    from oracle import oracle
+    from oxen_amd import _capi, hasher
+
+    smalls = {k: _small(k) for k in (0, 2, 3, 4, 6, 7)}
+    bigs = [_big(0), _big(1)]
+    paths, blobs = [], []
+    for k, b in smalls.items():
+        paths.append(_write(tmp_path, f"s{k}", b)), blobs.append(b)
+    for k, b in enumerate(bigs):
+        paths.append(_write(tmp_path, f"b{k}", b)), blobs.append(b)
+    paths.append(_write(tmp_path, "b0-copy", bigs[0])), blobs.append(bigs[0])      # duplicate big content
+    paths.append(_write(tmp_path, "s7-copy", smalls[7])), blobs.append(smalls[7])  # duplicate small content
+    paths.append(str(tmp_path / "missing"))
+    want = [oracle.xxh3_128_int(b) for b in blobs]
+    hexes = [format(w, "x") for w in want]
+    blocked = hexes[paths.index(str(tmp_path / "s7"))][:2]
+    assert sum(h[:2] == blocked for h in hexes) == 2  # only s7 and its copy live under that prefix
+    root = tmp_path / "store" / "versions" / "files"
+    root.mkdir(parents=True)
+    (root / blocked).write_bytes(b"not a directory")  # s7's publish cannot create its blob dir
+
+    with _capi.Context(0, staging_bytes=4 << 20) as c:
+        d, sz, st, stored = hasher.add_files(paths, str(root), c)
+        for i, p in enumerate(paths[:-1]):
+            if hexes[i][:2] == blocked:  # the publish failed: both items fail, digest None
+                assert st[i] == _capi.OXH_ERR_IO and d[i] is None and not stored[i], p
+                continue
+            assert st[i] == 0 and d[i] == want[i] and sz[i] == len(blobs[i]), p
+            with open(hasher.version_path(str(root), want[i]), "rb") as f:
+                assert f.read() == blobs[i], p
+        assert st[-1] != 0 and d[-1] is None
+        # every distinct published content stored exactly once (the big duplicate included)
+        ok_hex = {hexes[i] for i in range(len(paths) - 1) if hexes[i][:2] != blocked}
+        assert sum(stored) == len(ok_hex)
+        assert stored[paths.index(str(tmp_path / "b0"))] != stored[paths.index(str(tmp_path / "b0-copy"))]
+        assert not any(".oxentmp." in f for f in _tree(root)), _tree(root)
+        # a second add publishes nothing new; the blocked content still fails
+        d2, _, st2, stored2 = hasher.add_files(paths[:-1], str(root), c)
+        assert not any(stored2) and [s != 0 for s in st2] == [h[:2] == blocked for h in hexes]
+        assert not any(".oxentmp." in f for f in _tree(root))
+
+
+def test_big_file_allocation_failure_is_per_file(cuda, oracle_lib, tmp_path, monkeypatch):
+    """A device allocation the large-file path cannot get (here: 512 GiB pieces) fails that file with
+    OXH_ERR_NOMEM; the other files of the same call, and later calls, are unaffected."""
+    from oracle import oracle
+    from oxen_amd import _capi, hasher
+
+    small, big = _small(0), _big(1)
+    paths = [_write(tmp_path, "s", small), _write(tmp_path, "b", big)]
+    root = str(tmp_path / "store")
+    with _capi.Context(0, staging_bytes=4 << 20) as c:
+        monkeypatch.setenv("OXH_BIG_PIECE_MIB", str(1 << 19))
+        d, sz, st = hasher.hash_files_128bit(paths, c)
+        assert st == [0, _capi.OXH_ERR_NOMEM] and d == [oracle.xxh3_128_int(small), None]
+        d, sz, st, stored = hasher.add_files(paths, root, c)
+        assert st == [0, _capi.OXH_ERR_NOMEM] and stored == [True, False]
+        assert not any(".oxentmp." in f for f in _tree(root))
+        monkeypatch.delenv("OXH_BIG_PIECE_MIB")
+        d, sz, st, stored = hasher.add_files(paths, root, c)
+        assert st == [0, 0] and stored == [False, True]
+        assert d == [oracle.xxh3_128_int(small), oracle.xxh3_128_int(big)]
+        with open(hasher.version_path(root, d[1]), "rb") as f:
+            assert f.read() == big
+
+
+def test_files_are_read_to_eof_whatever_the_stat_size(cuda, oracle_lib, tmp_path):
+    """read_to_end semantics (hasher.rs:126-148): /proc/version stats as 0 bytes but reads as text;
+    the fstat path and the caller-metadata path both hash what the read returns."""
+    from oracle import oracle
+    from oxen_amd import _capi, hasher
+
+    if not os.path.exists("/proc/version") or os.stat("/proc/version").st_size != 0:
+        pytest.skip("needs a procfs file whose stat size is 0")
+    data = open("/proc/version", "rb").read()
+    assert data
+    other = _write(tmp_path, "f", _small(2))
+    paths = ["/proc/version", other]
+    want = [oracle.xxh3_128_int(data), oracle.xxh3_128_int(_small(2))]
+    with _capi.Context(0, staging_bytes=1 << 20) as c:
+        d, sz, st = hasher.hash_files_128bit(paths, c)
+        assert st == [0, 0] and d == want and sz[0] == len(data)
+        d, sz, st = hasher.hash_files_given_metadata_128bit(paths, [0, os.path.getsize(other)], c)
+        assert st == [0, 0] and d == want
+
+
+def test_context_at_the_staging_limit(cuda, oracle_lib, tmp_path):
+    """The largest accepted staging size (3 x (2 GiB - 256) pinned + device) hashes files correctly."""
+    from oracle import oracle
+    from oxen_amd import _capi, hasher
+
+    blobs = [_small(k) for k in range(4)] + [b"", _big(0)]
+    paths = [_write(tmp_path, f"f{k}", b) for k, b in enumerate(blobs)]
+    with _capi.Context(0, staging_bytes=_capi.OXH_MAX_STAGING_BYTES) as c:
+        d, sz, st = hasher.hash_files_128bit(paths * 3, c)
+    assert st == [0] * len(paths) * 3
+    assert d == [oracle.xxh3_128_int(b) for b in blobs] * 3
