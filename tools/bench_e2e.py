@@ -114,8 +114,9 @@ def main():
                          st.ctypes.data_as(oracle._i32p), a.threads)
         return time.perf_counter() - t0, out, st
 
-    # fused add (hash + version-store publish from the same pinned bytes) vs the reference loop
-    # restated (hash, then re-read + re-hash + write + rename per new file), warm cache, fresh stores
+    # fused add (hash + version-store publish from the same pinned bytes, one syncfs per slot before
+    # the renames and one after) vs the reference loop restated (hash, then re-read + re-hash + write +
+    # fsync + rename + parent fsync per new file), warm cache, fresh stores
     vroot = os.path.join(a.dir, ".oxen_gpu", "versions", "files")
     rroot = os.path.join(a.dir, ".oxen_ref", "versions", "files")
     oracle.hash_files(paths[: min(len(paths), 1000)], a.threads)
@@ -123,8 +124,14 @@ def main():
     gd, _, gst, gstored = hasher.add_files(paths, vroot, ctx)
     res["gpu_add_fused_s"] = round(time.perf_counter() - t0, 3)
     t0 = time.perf_counter()
-    rout, _, rst, rstored = oracle.add_files(paths, rroot, a.threads)
+    rout, _, rst, rstored = oracle.add_files(paths, rroot, a.threads)  # AtomicTempFile fsyncs per blob
     res["cpu_ref_add_s"] = round(time.perf_counter() - t0, 3)
+    # the same loop without the per-blob fsyncs (the r01 restatement), for the A/B
+    nroot = os.path.join(a.dir, ".oxen_nosync", "versions", "files")
+    t0 = time.perf_counter()
+    oracle.add_files(paths, nroot, a.threads, sync=False)
+    res["cpu_ref_add_nosync_s"] = round(time.perf_counter() - t0, 3)
+    shutil.rmtree(os.path.join(a.dir, ".oxen_nosync"), ignore_errors=True)
     res["gpu_add_fused_GiBs"] = round(nbytes / res["gpu_add_fused_s"] / 2**30, 2)
     res["cpu_ref_add_GiBs"] = round(nbytes / res["cpu_ref_add_s"] / 2**30, 2)
     res["add_blobs_written"] = [int(sum(gstored)), int(rstored.sum())]
