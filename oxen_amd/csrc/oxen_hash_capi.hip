@@ -512,6 +512,246 @@ int oversize_item(oxh_ctx* c, const uint8_t* src, uint64_t len, uint64_t* out2, 
     return rc;
 }
 
+// Items larger than a staging slot (K1L). A file larger than a slot takes the reference's streaming
+// branch (hasher.rs:150-174); a host buffer that large (oxh_hash_buffers / _streams) the same path.
+// The item is hashed in device pieces of OXH_BIG_PIECE_MIB (default 1 GiB) through two piece
+// buffers, so device memory stays bounded whatever the item size and piece j+1's transfer overlaps
+// piece j's K1L chain: each piece's block sums are computed chip-wide and the serial chain continues
+// from the previous piece's accumulators (ChainJob kChainResume / kChainPartial); the last piece
+// (> 1 KiB) takes the tail and the merge. A file piece reaches the device copy-free when its pages
+// are in the page cache (mincore) and can be pinned (mmap + hipHostRegister read-only, ~2 ms per GiB;
+// the DMA engine then reads them at 46-57 GB/s, tools/mmap_register_probe.hip); otherwise pieces pass
+// through two pinned 64 MiB bounce buffers filled by the worker pool (parallel 4 MiB reads). Text
+// counts accumulate over the pieces; is_utf8 reads the first 4 KiB of piece 0. With a sink (fused
+// add) every bounce part is also written to the sink's temp as it is read, and the temp is published
+// once the digest is known: the item never has to fit in host memory.
+constexpr uint64_t kBounce = 64ull << 20, kBigRead = 4ull << 20;
+
+// Where a large item's bytes come from.
+struct LargeSource {
+    virtual ~LargeSource() = default;
+    // Copy [off, off + n) straight to device memory `d` (no bounce buffer) if this source can; true
+    // once the copy has completed.
+    virtual bool direct(oxh_ctx*, uint64_t, uint64_t, uint8_t*) { return false; }
+    // [off, off + n) will be read soon.
+    virtual void will_need(uint64_t, uint64_t) {}
+    // Read [off, off + n) into dst; called from several threads for disjoint ranges. false = I/O error.
+    virtual bool read(uint64_t off, uint64_t n, uint8_t* dst) = 0;
+};
+
+// A regular file: preads, or mmap pages pinned in place for the copy-free path.
+struct FileSource final : LargeSource {
+    int fd = -1;
+    uint8_t* map = nullptr;
+    uint64_t len = 0;
+    std::vector<unsigned char> resident;
+    FileSource(const char* path, uint64_t L, bool allow_direct) : len(L) {
+        fd = path ? open(path, O_RDONLY | O_CLOEXEC | O_NONBLOCK) : -1;
+        if (fd >= 0 && allow_direct) {
+            void* m = mmap(nullptr, L, PROT_READ, MAP_SHARED, fd, 0);
+            if (m != MAP_FAILED) {
+                map = (uint8_t*)m;
+                (void)madvise(m, L, MADV_SEQUENTIAL);
+            }
+        }
+    }
+    ~FileSource() override {
+        if (map) munmap(map, len);
+        if (fd >= 0) close(fd);
+    }
+    // pinning faults missing pages in one thread, so a piece that is mostly on disk is read by the
+    // parallel preads instead
+    bool mostly_resident(uint64_t off, uint64_t n) {
+        const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE), npg = (n + pg - 1) / pg;
+        resident.resize(npg);
+        if (mincore(map + off, n, resident.data()) != 0) return false;
+        uint64_t in = 0;
+        for (unsigned char v : resident) in += v & 1;
+        return in * 10 >= npg * 9;
+    }
+    bool direct(oxh_ctx* c, uint64_t off, uint64_t n, uint8_t* d) override {
+        if (!map || !mostly_resident(off, n) || hipHostRegister(map + off, n, hipHostRegisterReadOnly) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        const bool ok = hipMemcpyAsync(d, map + off, n, hipMemcpyHostToDevice, c->copy_stream) == hipSuccess &&
+                        hipStreamSynchronize(c->copy_stream) == hipSuccess;
+        (void)hipHostUnregister(map + off);
+        (void)hipGetLastError();
+        return ok;
+    }
+    void will_need(uint64_t off, uint64_t n) override { (void)posix_fadvise(fd, (off_t)off, (off_t)n, POSIX_FADV_WILLNEED); }
+    bool read(uint64_t off, uint64_t n, uint8_t* dst) override {
+        for (uint64_t got = 0; got < n;) {
+            const ssize_t x = pread(fd, dst + got, n - got, (off_t)(off + got));
+            if (x <= 0) return false;
+            got += (uint64_t)x;
+        }
+        return true;
+    }
+};
+
+// A caller's host buffer (pageable): copied into the pinned bounce buffers by the pool.
+struct MemSource final : LargeSource {
+    const uint8_t* p;
+    explicit MemSource(const uint8_t* q) : p(q) {}
+    bool read(uint64_t off, uint64_t n, uint8_t* dst) override {
+        memcpy(dst, p + off, n);
+        return true;
+    }
+};
+
+struct LargeResult {
+    uint64_t out[2] = {0, 0}, cnt[2] = {0, 0};  // digest; text counts (num_lines, num_chars)
+    int32_t utf8 = 0;
+    int status = OXH_OK;  // this item's status: OXH_OK, OXH_ERR_IO or OXH_ERR_NOMEM
+};
+
+// Hash one large item of L bytes from `src` (see above). Returns a run-level error code only for
+// HIP failures; the item's own outcome (I/O error, allocation failure) is res.status.
+int large_item(oxh_ctx* c, uint64_t L, LargeSource& src, bool want_counts, bool want_utf8, ItemSink* sink, uint64_t id,
+               LargeResult& res) {
+    const uint64_t P = std::max<uint64_t>(
+        1, getenv("OXH_BIG_PIECE_MIB") ? strtoull(getenv("OXH_BIG_PIECE_MIB"), nullptr, 10) : 1024) << 20;
+    // pieces 0 .. k-1 hold P bytes each; the last one L - k*P bytes, in [1025, P + 1024]
+    const uint64_t k = L > P + 1024 ? (L - 1025) / P : 0;
+    const uint64_t cap = P + 1024;  // bytes per piece buffer
+    const uint64_t slot = align_up(cap) + 256;
+    // an allocation that fails is this item's failure (OXH_ERR_NOMEM), not the engine run's: the
+    // other requests in the live pipeline carry on
+    auto nomem = [&]() {
+        (void)hipGetLastError();
+        res.status = OXH_ERR_NOMEM;
+        return OXH_OK;
+    };
+    if (c->d_big_size < 2 * slot + 4096) {
+        if (c->d_big) {
+            HIP_TRY(hipDeviceSynchronize());
+            (void)hipFree(c->d_big);
+            c->d_big = nullptr;
+            c->d_big_size = 0;
+        }
+        if (hipMalloc(&c->d_big, 2 * slot + 4096) != hipSuccess) {
+            c->d_big = nullptr;
+            return nomem();
+        }
+        c->d_big_size = 2 * slot + 4096;
+    }
+    uint8_t* dbuf[2] = {c->d_big, c->d_big + slot};
+    // results area: [digest 2 | counts 2 | desc off, len | utf8 | state 8]
+    uint64_t* d_res = reinterpret_cast<uint64_t*>(c->d_big + 2 * slot);
+    struct Res {
+        uint64_t out[2], cnt[2], off, len;
+        int32_t utf8, pad;
+    } h{};
+    h.len = L;
+    for (int b = 0; b < 2; ++b) {
+        if (!c->h_bounce[b] && hipHostMalloc(&c->h_bounce[b], kBounce, hipHostMallocDefault) != hipSuccess) {
+            c->h_bounce[b] = nullptr;
+            return nomem();
+        }
+        if (!c->ev_bounce[b]) HIP_TRY(hipEventCreateWithFlags(&c->ev_bounce[b], hipEventDisableTiming));
+        if (!c->ev_piece_free[b]) HIP_TRY(hipEventCreateWithFlags(&c->ev_piece_free[b], hipEventDisableTiming));
+    }
+    uint64_t* sums = nullptr;
+    oxh::ScratchLease lease(c->stream);  // block sums of the two pieces in flight
+    const uint64_t sums_per = (cap >> 10) * 8;
+    if (lease.get(2 * sums_per * 8, (void**)&sums) != hipSuccess) return nomem();
+    HIP_TRY(hipMemcpyAsync(d_res, &h, sizeof h, hipMemcpyHostToDevice, c->stream));
+
+    std::string sink_tmp;
+    int sfd = -1;
+    std::atomic<bool> sink_ok{true};
+    if (sink) {
+        sfd = sink->open_stream(id, sink_tmp);
+        if (sfd < 0) sink_ok.store(false);
+    }
+    int rc = OXH_OK;
+    bool io_ok = true, piece_used[2] = {false, false};
+    // piece [off, off + plen) -> device buffer d on the copy stream; false on an I/O error
+    auto copy_piece = [&](uint64_t off, uint64_t plen, uint8_t* d) -> bool {
+        if (!sink && src.direct(c, off, plen, d)) return true;  // a sink must see the bytes on the host
+        for (uint64_t o = 0, q = 0; o < plen; o += kBounce, ++q) {  // bounce-buffer path
+            const int bb = (int)(q & 1);
+            if (c->bounce_used[bb] && hipEventSynchronize(c->ev_bounce[bb]) != hipSuccess) return false;
+            const uint64_t n = std::min(kBounce, plen - o);
+            src.will_need(off + o + n, 2 * kBounce);  // two bounce pieces ahead while the pool reads this one
+            const int parts = (int)((n + kBigRead - 1) / kBigRead);
+            std::atomic<bool> bad{false};
+            c->pool->parallel_for(parts, [&](int t) {
+                const uint64_t lo = (uint64_t)t * kBigRead, hi = std::min(n, lo + kBigRead);
+                if (!src.read(off + o + lo, hi - lo, c->h_bounce[bb] + lo)) {
+                    bad.store(true);
+                    return;
+                }
+                if (sfd >= 0 && sink_ok.load(std::memory_order_relaxed))  // the same bytes to the temp blob
+                    for (uint64_t put = lo; put < hi;) {
+                        const ssize_t x = pwrite(sfd, c->h_bounce[bb] + put, hi - put, (off_t)(off + o + put));
+                        if (x <= 0) {
+                            sink_ok.store(false);
+                            break;
+                        }
+                        put += (uint64_t)x;
+                    }
+            });
+            if (bad.load()) return false;
+            if (hipMemcpyAsync(d + o, c->h_bounce[bb], n, hipMemcpyHostToDevice, c->copy_stream) != hipSuccess ||
+                hipEventRecord(c->ev_bounce[bb], c->copy_stream) != hipSuccess)
+                return false;
+            c->bounce_used[bb] = true;
+        }
+        return hipStreamSynchronize(c->copy_stream) == hipSuccess;
+    };
+    for (uint64_t j = 0; j <= k && io_ok && rc == OXH_OK; ++j) {
+        const int b = (int)(j & 1);
+        const uint64_t off = j * P, plen = j < k ? P : L - off;
+        // the chain of piece j-2 (which read dbuf[b] and its block sums) is done
+        if (piece_used[b] && hipEventSynchronize(c->ev_piece_free[b]) != hipSuccess) {
+            rc = fail(OXH_ERR_HIP, "large-item piece wait");
+            break;
+        }
+        if (!copy_piece(off, plen, dbuf[b])) {
+            io_ok = false;
+            break;
+        }
+        piece_used[b] = true;
+        uint64_t* s_b = sums + (uint64_t)b * sums_per;
+        const bool last = j == k;
+        const uint64_t nb = last ? (plen - 1) >> 10 : plen >> 10;
+        const uint64_t nwaves = (nb + 3) / 4, blocks = (nwaves + 3) / 4;
+        hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, c->stream, dbuf[b], nb, s_b);
+        if (want_counts)
+            hipLaunchKernelGGL(oxh::text_count_kernel, dim3(2048), dim3(256), 0, c->stream, dbuf[b], plen,
+                               (unsigned long long*)(d_res + 2));
+        if (j == 0 && want_utf8)
+            hipLaunchKernelGGL(oxh::utf8_prefix_kernel, dim3(1), dim3(64), 0, c->stream, dbuf[b], d_res + 4, d_res + 5,
+                               (uint64_t)1, (int32_t*)(d_res + 6));
+        oxh::ChainBatch batch;
+        batch.job[0] = {dbuf[b], plen, s_b, d_res, L, d_res + 7, (j > 0 ? oxh::kChainResume : 0u) | (last ? 0u : oxh::kChainPartial)};
+        hipLaunchKernelGGL(oxh::xxh3_chain_kernel, dim3(1), dim3(64), kChainLdsPad, c->stream, batch);
+        if (hipGetLastError() != hipSuccess || hipEventRecord(c->ev_piece_free[b], c->stream) != hipSuccess)
+            rc = fail(OXH_ERR_HIP, "large-item piece launch");
+    }
+    if (rc == OXH_OK && hipMemcpyAsync(&h, d_res, sizeof h, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+        rc = fail(OXH_ERR_HIP, "large-item results D2H");
+    if (hipStreamSynchronize(c->stream) != hipSuccess && rc == OXH_OK) rc = fail(OXH_ERR_HIP, "large-item sync");
+    if (sink) {  // publish (or drop) the temp blob now that the digest is known
+        sink->close_stream(id, sfd, sink_tmp, rc == OXH_OK && io_ok && sink_ok.load(), h.out[0], h.out[1]);
+        sink->commit();
+    }
+    if (rc) return rc;
+    if (!io_ok) {
+        res.status = OXH_ERR_IO;
+        return OXH_OK;
+    }
+    res.out[0] = h.out[0];
+    res.out[1] = h.out[1];
+    res.cnt[0] = 1 + h.cnt[0];
+    res.cnt[1] = L - h.cnt[1];
+    res.utf8 = h.utf8;
+    return OXH_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -666,7 +906,7 @@ int oxh_combined_hash_device(const uint64_t* d_content, const uint64_t* d_metada
 // copy(i, dst) straight into a pinned slot; slots are packed greedily in order, hashed on the GPU
 // while the next one fills, and items larger than a slot go through the oversize path.
 static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
-                           const std::function<void(uint64_t, uint8_t*)>& copy, uint64_t* out, bool short_only_lane) {
+                           const std::function<const uint8_t*(uint64_t)>& src, uint64_t* out, bool short_only_lane) {
     Trace tr;
     Pending pend[NSLOT];
     int slot = 0;
@@ -677,11 +917,14 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
         uint64_t bytes = 0;
         while (i < n && batch.size() < c->max_items) {
             const uint64_t L = lens[i];
-            if (L > c->stage_bytes) {
+            if (L > c->stage_bytes) {  // straight from the caller's buffer, in pieces (large_item)
                 if (!batch.empty()) break;
-                std::vector<uint8_t> tmp(L);
-                copy(i, tmp.data());
-                if (int rc = oversize_item(c, tmp.data(), L, out + 2 * i)) return rc;
+                MemSource ms(src(i));
+                LargeResult res;
+                if (int rc = large_item(c, L, ms, false, false, nullptr, i, res)) return rc;
+                if (res.status != OXH_OK) return fail(res.status, "large host buffer: device or pinned memory unavailable");
+                out[2 * i] = res.out[0];
+                out[2 * i + 1] = res.out[1];
                 ++i;
                 continue;
             }
@@ -712,7 +955,8 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
         STEP("fill s=%d items=%zu", s, batch.size());
         const int ntasks = (int)std::min<size_t>(batch.size(), (size_t)c->pool->size() * 4);
         c->pool->parallel_for(ntasks, [&](int t) {
-            for (size_t j = (size_t)t; j < batch.size(); j += (size_t)ntasks) copy(batch[j], c->h_stage[s] + hoff[j]);
+            for (size_t j = (size_t)t; j < batch.size(); j += (size_t)ntasks)
+                if (hlen[j]) memcpy(c->h_stage[s] + hoff[j], src(batch[j]), hlen[j]);
         });
         const double t2 = Trace::now();
         tr.fill += t2 - t1;
@@ -739,9 +983,7 @@ int oxh_hash_buffers(oxh_ctx* c, const uint8_t* const* bufs, const uint64_t* len
     if (!c || (n && (!bufs || !lens || !out))) return fail(OXH_ERR_INVALID, "bad arguments");
     std::lock_guard<std::mutex> g(c->mu);
     HIP_TRY(hipSetDevice(c->device));
-    return hash_host_items(c, n, lens, [&](uint64_t i, uint8_t* dst) {
-        if (lens[i]) memcpy(dst, bufs[i], lens[i]);
-    }, out, false);
+    return hash_host_items(c, n, lens, [&](uint64_t i) { return bufs[i]; }, out, false);
 }
 
 int oxh_hash_streams(oxh_ctx* c, const uint8_t* streams, const uint64_t* offsets, const uint64_t* lens, uint64_t n,
@@ -751,9 +993,7 @@ int oxh_hash_streams(oxh_ctx* c, const uint8_t* streams, const uint64_t* offsets
     std::lock_guard<std::mutex> g(c->mu);
     HIP_TRY(hipSetDevice(c->device));
     STEP("hash_streams locked");
-    return hash_host_items(c, n, lens, [&](uint64_t i, uint8_t* dst) {
-        if (lens[i]) memcpy(dst, streams + offsets[i], lens[i]);
-    }, out, true);
+    return hash_host_items(c, n, lens, [&](uint64_t i) { return streams + offsets[i]; }, out, true);
 }
 
 // ---------------------------------------------------------------- streaming file engine
@@ -1095,206 +1335,28 @@ void drain_files(FileStream& fs, int s, const SlotRun& p) {
     }
 }
 
-// One file read through the oversize path (files larger than a staging slot, K1L).
-// A file larger than a staging slot (the reference's streaming branch, hasher.rs:150-174) is hashed
-// in device pieces of OXH_BIG_PIECE_MIB (default 1 GiB) through two piece buffers, so device memory
-// stays bounded whatever the file size and piece j+1's transfer overlaps piece j's K1L chain: each
-// piece's block sums are computed chip-wide and the serial chain continues from the previous piece's
-// accumulators (ChainJob kChainResume / kChainPartial); the last piece (> 1 KiB) takes the tail and
-// the merge. A piece reaches the device copy-free when its pages are in the page cache (mincore)
-// and can be pinned (mmap + hipHostRegister read-only, ~2 ms per GiB; the DMA engine then reads
-// them at 46-57 GB/s, tools/mmap_register_probe.hip), else through two pinned bounce buffers
-// filled by the worker pool (parallel 4 MiB preads, 64 MiB at a time). Text counts accumulate over the pieces; is_utf8 reads
-// the first 4 KiB of piece 0.
-constexpr uint64_t kBounce = 64ull << 20, kBigRead = 4ull << 20;
-
+// A file of the engine larger than a staging slot.
 int big_file(FileStream& fs, FileRequest* r, uint64_t i) {
-    oxh_ctx* c = fs.c;
     const uint64_t L = r->lens[i];
-    const uint64_t P = std::max<uint64_t>(
-        1, getenv("OXH_BIG_PIECE_MIB") ? strtoull(getenv("OXH_BIG_PIECE_MIB"), nullptr, 10) : 1024) << 20;
-    // pieces 0 .. k-1 hold P bytes each; the last one L - k*P bytes, in [1025, P + 1024]
-    const uint64_t k = L > P + 1024 ? (L - 1025) / P : 0;
-    const uint64_t cap = P + 1024;  // bytes per piece buffer
-    const uint64_t slot = align_up(cap) + 256;
-    // an allocation that fails is this file's failure (status OXH_ERR_NOMEM), not the engine run's:
-    // the other requests in the live pipeline carry on
-    auto item_nomem = [&]() {
-        r->st[i] = OXH_ERR_NOMEM;
-        if (r->sink) r->sink->close_stream(i, -1, std::string(), false, 0, 0);
-        account(fs, r, 1);
-        return OXH_OK;
-    };
-    if (c->d_big_size < 2 * slot + 4096) {
-        if (c->d_big) {
-            HIP_TRY(hipDeviceSynchronize());
-            (void)hipFree(c->d_big);
-            c->d_big = nullptr;
-            c->d_big_size = 0;
-        }
-        if (hipMalloc(&c->d_big, 2 * slot + 4096) != hipSuccess) {
-            c->d_big = nullptr;
-            (void)hipGetLastError();
-            return item_nomem();
-        }
-        c->d_big_size = 2 * slot + 4096;
-    }
-    uint8_t* dbuf[2] = {c->d_big, c->d_big + slot};
-    // results area: [digest 2 | counts 2 | desc off, len | utf8 | state 8]
-    uint64_t* d_res = reinterpret_cast<uint64_t*>(c->d_big + 2 * slot);
-    struct Res {
-        uint64_t out[2], cnt[2], off, len;
-        int32_t utf8, pad;
-    } h{};
-    h.len = L;
-    for (int b = 0; b < 2; ++b) {
-        if (!c->h_bounce[b] && hipHostMalloc(&c->h_bounce[b], kBounce, hipHostMallocDefault) != hipSuccess) {
-            c->h_bounce[b] = nullptr;
-            (void)hipGetLastError();
-            return item_nomem();
-        }
-        if (!c->ev_bounce[b]) HIP_TRY(hipEventCreateWithFlags(&c->ev_bounce[b], hipEventDisableTiming));
-        if (!c->ev_piece_free[b]) HIP_TRY(hipEventCreateWithFlags(&c->ev_piece_free[b], hipEventDisableTiming));
-    }
-    uint64_t* sums = nullptr;
-    oxh::ScratchLease lease(c->stream);  // block sums of the two pieces in flight
-    const uint64_t sums_per = (cap >> 10) * 8;
-    if (lease.get(2 * sums_per * 8, (void**)&sums) != hipSuccess) {
-        (void)hipGetLastError();
-        return item_nomem();
-    }
-    HIP_TRY(hipMemcpyAsync(d_res, &h, sizeof h, hipMemcpyHostToDevice, c->stream));
-
-    int rc = OXH_OK;
-    bool io_ok = true, piece_used[2] = {false, false};
-    const int fd = open(r->paths[i], O_RDONLY | O_CLOEXEC | O_NONBLOCK);
-    if (fd < 0) io_ok = false;
-    // fused add: the sink gets every bounce piece as it is read (a temp blob written while the chain
-    // runs), so the file never needs to fit in host memory; it publishes once the digest is known
-    ItemSink* sink = r->sink;
-    std::string sink_tmp;
-    int sfd = -1;
-    std::atomic<bool> sink_ok{true};
-    if (sink && io_ok) {
-        sfd = sink->open_stream(i, sink_tmp);
-        if (sfd < 0) sink_ok.store(false);
-    }
-    uint8_t* map = nullptr;
-    if (io_ok && !sink) {  // copy-free pieces would not pass through host memory the sink can read
-        void* m = mmap(nullptr, L, PROT_READ, MAP_SHARED, fd, 0);
-        if (m != MAP_FAILED) {
-            map = (uint8_t*)m;
-            (void)madvise(m, L, MADV_SEQUENTIAL);
+    LargeResult res;
+    {
+        FileSource src(r->paths[i], L, r->sink == nullptr);
+        if (src.fd < 0) {
+            res.status = OXH_ERR_IO;
+        } else if (int rc = large_item(fs.c, L, src, r->counts != nullptr, r->utf8 != nullptr, r->sink, i, res)) {
+            return rc;
         }
     }
-    // piece j of the file -> dbuf[b] on the copy stream; false on an I/O error
-    // pages of [off, off + plen) in the page cache: pinning faults missing pages in one thread,
-    // so a piece that is mostly on disk is read by the parallel preads instead
-    std::vector<unsigned char> resident;
-    auto mostly_resident = [&](uint64_t off, uint64_t plen) {
-        const uint64_t pg = (uint64_t)sysconf(_SC_PAGESIZE), npg = (plen + pg - 1) / pg;
-        resident.resize(npg);
-        if (mincore(map + off, plen, resident.data()) != 0) return false;
-        uint64_t in = 0;
-        for (unsigned char v : resident) in += v & 1;
-        return in * 10 >= npg * 9;
-    };
-    auto copy_piece = [&](uint64_t off, uint64_t plen, int b) -> bool {
-        if (map && mostly_resident(off, plen) && hipHostRegister(map + off, plen, hipHostRegisterReadOnly) == hipSuccess) {
-            const bool ok = hipMemcpyAsync(dbuf[b], map + off, plen, hipMemcpyHostToDevice, c->copy_stream) == hipSuccess &&
-                            hipStreamSynchronize(c->copy_stream) == hipSuccess;
-            (void)hipHostUnregister(map + off);
-            if (ok) return true;
-        }
-        (void)hipGetLastError();
-        for (uint64_t o = 0, q = 0; o < plen; o += kBounce, ++q) {  // bounce-buffer path
-            const int bb = (int)(q & 1);
-            if (c->bounce_used[bb] && hipEventSynchronize(c->ev_bounce[bb]) != hipSuccess) return false;
-            const uint64_t n = std::min(kBounce, plen - o);
-            // the kernel reads the next two bounce pieces ahead while the pool reads this one
-            (void)posix_fadvise(fd, (off_t)(off + o + n), (off_t)(2 * kBounce), POSIX_FADV_WILLNEED);
-            const int parts = (int)((n + kBigRead - 1) / kBigRead);
-            std::atomic<bool> bad{false};
-            c->pool->parallel_for(parts, [&](int t) {
-                const uint64_t lo = (uint64_t)t * kBigRead, hi = std::min(n, lo + kBigRead);
-                for (uint64_t got = lo; got < hi;) {
-                    const ssize_t x = pread(fd, c->h_bounce[bb] + got, hi - got, (off_t)(off + o + got));
-                    if (x <= 0) {
-                        bad.store(true);
-                        return;
-                    }
-                    got += (uint64_t)x;
-                }
-                if (sfd >= 0 && sink_ok.load(std::memory_order_relaxed))  // the same bytes to the temp blob
-                    for (uint64_t put = lo; put < hi;) {
-                        const ssize_t x = pwrite(sfd, c->h_bounce[bb] + put, hi - put, (off_t)(off + o + put));
-                        if (x <= 0) {
-                            sink_ok.store(false);
-                            break;
-                        }
-                        put += (uint64_t)x;
-                    }
-            });
-            if (bad.load()) return false;
-            if (hipMemcpyAsync(dbuf[b] + o, c->h_bounce[bb], n, hipMemcpyHostToDevice, c->copy_stream) != hipSuccess ||
-                hipEventRecord(c->ev_bounce[bb], c->copy_stream) != hipSuccess)
-                return false;
-            c->bounce_used[bb] = true;
-        }
-        return hipStreamSynchronize(c->copy_stream) == hipSuccess;
-    };
-    for (uint64_t j = 0; j <= k && io_ok && rc == OXH_OK; ++j) {
-        const int b = (int)(j & 1);
-        const uint64_t off = j * P, plen = j < k ? P : L - off;
-        // the chain of piece j-2 (which read dbuf[b] and its block sums) is done
-        if (piece_used[b] && hipEventSynchronize(c->ev_piece_free[b]) != hipSuccess) {
-            rc = fail(OXH_ERR_HIP, "large-file piece wait");
-            break;
-        }
-        if (!copy_piece(off, plen, b)) {
-            io_ok = false;
-            break;
-        }
-        piece_used[b] = true;
-        uint64_t* s_b = sums + (uint64_t)b * sums_per;
-        const bool last = j == k;
-        const uint64_t nb = last ? (plen - 1) >> 10 : plen >> 10;
-        const uint64_t nwaves = (nb + 3) / 4, blocks = (nwaves + 3) / 4;
-        hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, c->stream, dbuf[b], nb, s_b);
-        if (r->counts) {
-            hipLaunchKernelGGL(oxh::text_count_kernel, dim3(2048), dim3(256), 0, c->stream, dbuf[b], plen,
-                               (unsigned long long*)(d_res + 2));
-        }
-        if (j == 0 && r->utf8) {
-            hipLaunchKernelGGL(oxh::utf8_prefix_kernel, dim3(1), dim3(64), 0, c->stream, dbuf[b], d_res + 4, d_res + 5,
-                               (uint64_t)1, (int32_t*)(d_res + 6));
-        }
-        oxh::ChainBatch batch;
-        batch.job[0] = {dbuf[b], plen, s_b, d_res, L, d_res + 7, (j > 0 ? oxh::kChainResume : 0u) | (last ? 0u : oxh::kChainPartial)};
-        hipLaunchKernelGGL(oxh::xxh3_chain_kernel, dim3(1), dim3(64), kChainLdsPad, c->stream, batch);
-        if (hipGetLastError() != hipSuccess || hipEventRecord(c->ev_piece_free[b], c->stream) != hipSuccess)
-            rc = fail(OXH_ERR_HIP, "large-file piece launch");
-    }
-    if (map) munmap(map, L);
-    if (fd >= 0) close(fd);
-    if (rc == OXH_OK && hipMemcpyAsync(&h, d_res, sizeof h, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
-        rc = fail(OXH_ERR_HIP, "large-file results D2H");
-    if (hipStreamSynchronize(c->stream) != hipSuccess && rc == OXH_OK) rc = fail(OXH_ERR_HIP, "large-file sync");
-    if (sink) {  // publish (or drop) the temp blob now that the digest is known
-        sink->close_stream(i, sfd, sink_tmp, rc == OXH_OK && io_ok && sink_ok.load(), h.out[0], h.out[1]);
-        sink->commit();
-    }
-    if (rc) return rc;
-    if (!io_ok) {
-        r->st[i] = OXH_ERR_IO;
+    if (res.status != OXH_OK) {
+        r->st[i] = res.status;
     } else {
-        r->out[2 * i] = h.out[0];
-        r->out[2 * i + 1] = h.out[1];
+        r->out[2 * i] = res.out[0];
+        r->out[2 * i + 1] = res.out[1];
         if (r->counts) {
-            r->counts[2 * i] = 1 + h.cnt[0];
-            r->counts[2 * i + 1] = L - h.cnt[1];
+            r->counts[2 * i] = res.cnt[0];
+            r->counts[2 * i + 1] = res.cnt[1];
         }
-        if (r->utf8) r->utf8[i] = h.utf8;
+        if (r->utf8) r->utf8[i] = res.utf8;
     }
     account(fs, r, 1);
     return OXH_OK;

@@ -134,3 +134,22 @@ def test_context_at_the_staging_limit(cuda, oracle_lib, tmp_path):
         d, sz, st = hasher.hash_files_128bit(paths * 3, c)
     assert st == [0] * len(paths) * 3
     assert d == [oracle.xxh3_128_int(b) for b in blobs] * 3
+
+
+@pytest.mark.parametrize("piece_mib", [None, "2"], ids=["one-piece", "2MiB-pieces"])
+def test_host_buffers_larger_than_staging(cuda, oracle_lib, monkeypatch, piece_mib):
+    """oxh_hash_buffers / oxh_hash_streams with items above the 1 MiB staging slot: they go straight
+    from the caller's memory through the bounce buffers and the device pieces (no whole-item copy on
+    the host or the device), between ordinary staged items."""
+    from oracle import oracle
+    from oxen_amd import _capi, hasher
+    from oxen_amd.workloads import splitmix_bytes
+
+    if piece_mib:
+        monkeypatch.setenv("OXH_BIG_PIECE_MIB", piece_mib)
+    sizes = [100, (5 << 20) + 3, 70_000, 1 << 20, (1 << 20) + 1, 0, (2 << 20) + 1025, 241]
+    bufs = [splitmix_bytes(900 + k, 0, s).tobytes() for k, s in enumerate(sizes)]
+    want = [oracle.xxh3_128_int(b) for b in bufs]
+    with _capi.Context(0, staging_bytes=1 << 20) as c:
+        assert hasher.hash_buffers_128bit(bufs, c) == want
+        assert hasher.hash_streams_128bit(bufs, c) == want
