@@ -96,6 +96,20 @@ int oxh_xxh3_128_large_device(oxh_ctx* ctx, const void* d_buf, uint64_t len, uin
 int oxh_xxh3_128_large_batch_device(const void* const* d_bufs, const uint64_t* lens, uint64_t n,
                                     uint64_t* d_out, void* stream);
 
+/* ---------------------------------------------------------------- streaming XXH3
+ * xxhash-rust's `Xxh3` (new / update / digest128) as used by hasher.rs:73-76, 157-173 (large files),
+ * HashingReader / HashingWriter (hasher.rs:183-244) and AtomicFile's verify (atomic_file.rs:396-431).
+ * Bytes collect in a pinned buffer; every 16 MiB (OXH_STREAM_PIECE_MIB) of whole 1 KiB blocks go to
+ * the device as one K1L piece whose chain resumes from the stream's accumulators, so memory stays
+ * bounded whatever the length. digest (2 u64, lo then hi) = xxh3_128 of everything updated so far
+ * and leaves the state unchanged. A stream is used by one thread at a time (like `&mut Xxh3`). */
+typedef struct oxh_xxh3_stream oxh_xxh3_stream;
+int oxh_xxh3_stream_create(oxh_ctx* ctx, oxh_xxh3_stream** out);
+int oxh_xxh3_stream_update(oxh_xxh3_stream* s, const void* data, uint64_t len);
+int oxh_xxh3_stream_digest(oxh_xxh3_stream* s, uint64_t* out2);
+int oxh_xxh3_stream_reset(oxh_xxh3_stream* s);
+int oxh_xxh3_stream_destroy(oxh_xxh3_stream* s);
+
 /* ---------------------------------------------------------------- host-resident entry points
  * These block until the digests are in host memory. */
 

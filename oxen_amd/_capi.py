@@ -59,6 +59,11 @@ SIGNATURES = {
     "oxh_format_dec": (_int, [_u64, _u64, ctypes.c_char_p]),
     "oxh_fill_splitmix": (_int, [_vp, _u64, _u64, _vp]),
     "oxh_set_kernel_variant": (_int, [_int]),
+    "oxh_xxh3_stream_create": (_int, [_vp, ctypes.POINTER(_vp)]),
+    "oxh_xxh3_stream_update": (_int, [_vp, _vp, _u64]),
+    "oxh_xxh3_stream_digest": (_int, [_vp, _u64p]),
+    "oxh_xxh3_stream_reset": (_int, [_vp]),
+    "oxh_xxh3_stream_destroy": (_int, [_vp]),
     "oxh_fastcdc_device": (_int, [_vp, _u64p, _u64p, _u64, _u32, _u32, _u32, _u32, _vp, _vp, _vp, _u64, _u64p, _vp]),
     "oxh_fastcdc_max_chunks": (_u64, [_u64p, _u64, _u32]),
     "oxh_fastcdc_gear": (_int, [_u64p]),

@@ -892,6 +892,173 @@ int oxh_xxh3_128_large_batch_device(const void* const* d_bufs, const uint64_t* l
     return large_batch_device((const uint8_t* const*)d_bufs, lens, n, d_out, (hipStream_t)stream);
 }
 
+// ---------------------------------------------------------------- streaming XXH3 (Xxh3)
+// xxhash-rust's Xxh3::new / update / digest128 (hasher.rs:9,73-76,157-173, 183-244), with the device
+// doing the hashing: bytes collect in a pinned buffer of S + 1025 bytes (S = OXH_STREAM_PIECE_MIB,
+// default 16 MiB, whole 1 KiB blocks); each time it fills, its first S bytes go to the device as one
+// K1L piece (block sums chip-wide, then the chain resumed from the stream's 8 accumulators, which stay
+// in device memory) and the last 1025 bytes move to the front. XXH3 scrambles every block but the
+// last and reads the last stripe at len - 64, so keeping > 1 KiB back means the digest always has
+// the item's tail on hand. digest128() hashes what is pending as the final piece without changing
+// the state (updates may continue). Memory stays bounded whatever the stream's length.
+struct oxh_xxh3_stream {
+    int device = 0;
+    uint64_t piece = 0;           // S
+    uint8_t* h_pend = nullptr;    // pinned, S + 1025
+    uint64_t fill = 0, total = 0, pieces = 0;
+    uint8_t* d_mem = nullptr;     // [piece 0 | piece 1 | sums 0 | sums 1 | state 8 | out 2]
+    uint8_t* d_piece[2] = {};
+    uint64_t* d_sums[2] = {};
+    uint64_t *d_state = nullptr, *d_out = nullptr;
+    hipStream_t st = nullptr;
+    hipEvent_t ev_copied = nullptr, ev_free[2] = {};
+    bool used[2] = {};
+};
+
+namespace {
+
+int stream_device(oxh_xxh3_stream* s) {
+    if (s->d_mem) return OXH_OK;
+    const uint64_t pb = align_up(s->piece + 1025) + 256, sb = ((s->piece >> 10) + 1) * 64;
+    if (hipMalloc(&s->d_mem, 2 * pb + 2 * sb + 256) != hipSuccess) {
+        s->d_mem = nullptr;
+        (void)hipGetLastError();
+        return fail(OXH_ERR_NOMEM, "stream device buffers");
+    }
+    s->d_piece[0] = s->d_mem;
+    s->d_piece[1] = s->d_mem + pb;
+    s->d_sums[0] = reinterpret_cast<uint64_t*>(s->d_mem + 2 * pb);
+    s->d_sums[1] = reinterpret_cast<uint64_t*>(s->d_mem + 2 * pb + sb);
+    s->d_state = reinterpret_cast<uint64_t*>(s->d_mem + 2 * pb + 2 * sb);
+    s->d_out = s->d_state + 8;
+    return OXH_OK;
+}
+
+// the next device piece buffer, once the chain that last read it is done
+int stream_take_piece(oxh_xxh3_stream* s, int& b) {
+    b = (int)(s->pieces & 1);
+    if (s->used[b]) HIP_TRY(hipEventSynchronize(s->ev_free[b]));
+    return OXH_OK;
+}
+
+// block sums + chain of `len` bytes already in d_piece[b]
+int stream_chain(oxh_xxh3_stream* s, int b, uint64_t len, bool partial) {
+    const uint64_t nb = partial ? len >> 10 : (len - 1) >> 10;
+    const uint64_t nwaves = (nb + 3) / 4, blocks = (nwaves + 3) / 4;
+    if (blocks)
+        hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s->st, s->d_piece[b], nb,
+                           s->d_sums[b]);
+    oxh::ChainBatch batch;
+    batch.job[0] = {s->d_piece[b], len, s->d_sums[b], s->d_out, s->total, s->d_state,
+                    (s->pieces > 0 ? oxh::kChainResume : 0u) | (partial ? oxh::kChainPartial : 0u)};
+    hipLaunchKernelGGL(oxh::xxh3_chain_kernel, dim3(1), dim3(64), kChainLdsPad, s->st, batch);
+    HIP_TRY(hipGetLastError());
+    return OXH_OK;
+}
+
+// the first S pending bytes become a piece; the last 1025 move to the front
+int stream_flush(oxh_xxh3_stream* s) {
+    if (int rc = stream_device(s)) return rc;
+    int b = 0;
+    if (int rc = stream_take_piece(s, b)) return rc;
+    HIP_TRY(hipMemcpyAsync(s->d_piece[b], s->h_pend, s->piece, hipMemcpyHostToDevice, s->st));
+    HIP_TRY(hipEventRecord(s->ev_copied, s->st));
+    if (int rc = stream_chain(s, b, s->piece, true)) return rc;
+    HIP_TRY(hipEventRecord(s->ev_free[b], s->st));
+    s->used[b] = true;
+    s->pieces++;
+    HIP_TRY(hipEventSynchronize(s->ev_copied));  // the pinned bytes were read: reuse the buffer
+    memmove(s->h_pend, s->h_pend + s->piece, 1025);
+    s->fill = 1025;
+    return OXH_OK;
+}
+
+}  // namespace
+
+int oxh_xxh3_stream_create(oxh_ctx* ctx, oxh_xxh3_stream** out) {
+    if (!ctx || !out) return fail(OXH_ERR_INVALID, "bad stream arguments");
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(ctx->device));
+    oxh_xxh3_stream* s = new oxh_xxh3_stream();
+    s->device = ctx->device;
+    const char* e = getenv("OXH_STREAM_PIECE_MIB");
+    const uint64_t kib = e && strtoull(e, nullptr, 10) ? strtoull(e, nullptr, 10) << 10 : 16ull << 10;
+    s->piece = kib << 10;  // whole 1 KiB blocks
+    if (hipHostMalloc(&s->h_pend, s->piece + 1025, hipHostMallocDefault) != hipSuccess ||
+        hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&s->ev_copied, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&s->ev_free[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&s->ev_free[1], hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        oxh_xxh3_stream_destroy(s);
+        return fail(OXH_ERR_NOMEM, "stream buffers");
+    }
+    *out = s;
+    return OXH_OK;
+}
+
+int oxh_xxh3_stream_update(oxh_xxh3_stream* s, const void* data, uint64_t len) {
+    if (!s || (len && !data)) return fail(OXH_ERR_INVALID, "bad stream update");
+    HIP_TRY(hipSetDevice(s->device));
+    const uint8_t* p = (const uint8_t*)data;
+    const uint64_t cap = s->piece + 1025;
+    while (len) {
+        const uint64_t take = std::min(len, cap - s->fill);
+        memcpy(s->h_pend + s->fill, p, take);
+        s->fill += take;
+        s->total += take;
+        p += take;
+        len -= take;
+        if (s->fill == cap)
+            if (int rc = stream_flush(s)) return rc;
+    }
+    return OXH_OK;
+}
+
+int oxh_xxh3_stream_digest(oxh_xxh3_stream* s, uint64_t* out2) {
+    if (!s || !out2) return fail(OXH_ERR_INVALID, "bad stream digest");
+    HIP_TRY(hipSetDevice(s->device));
+    if (int rc = stream_device(s)) return rc;
+    int b = 0;
+    if (int rc = stream_take_piece(s, b)) return rc;
+    if (s->fill) HIP_TRY(hipMemcpyAsync(s->d_piece[b], s->h_pend, s->fill, hipMemcpyHostToDevice, s->st));
+    if (s->pieces == 0) {  // the whole stream is pending: a one-shot digest (K1, or K1L above 1 MiB)
+        const uint8_t* d = s->d_piece[b];
+        if (int rc = large_batch_device(&d, &s->fill, 1, s->d_out, s->st)) return rc;
+    } else if (int rc = stream_chain(s, b, s->fill, false)) {  // fill >= 1025: the final piece
+        return rc;
+    }
+    HIP_TRY(hipEventRecord(s->ev_free[b], s->st));
+    s->used[b] = true;
+    uint64_t h[2];
+    HIP_TRY(hipMemcpyAsync(h, s->d_out, 16, hipMemcpyDeviceToHost, s->st));
+    HIP_TRY(hipStreamSynchronize(s->st));
+    out2[0] = h[0];
+    out2[1] = h[1];
+    return OXH_OK;
+}
+
+int oxh_xxh3_stream_reset(oxh_xxh3_stream* s) {
+    if (!s) return fail(OXH_ERR_INVALID, "stream is NULL");
+    if (s->st) HIP_TRY(hipStreamSynchronize(s->st));
+    s->fill = s->total = s->pieces = 0;
+    return OXH_OK;
+}
+
+int oxh_xxh3_stream_destroy(oxh_xxh3_stream* s) {
+    if (!s) return OXH_OK;
+    (void)hipSetDevice(s->device);
+    if (s->st) (void)hipStreamSynchronize(s->st);
+    if (s->d_mem) (void)hipFree(s->d_mem);
+    if (s->h_pend) (void)hipHostFree(s->h_pend);
+    if (s->ev_copied) (void)hipEventDestroy(s->ev_copied);
+    for (hipEvent_t e : s->ev_free)
+        if (e) (void)hipEventDestroy(e);
+    if (s->st) (void)hipStreamDestroy(s->st);
+    delete s;
+    return OXH_OK;
+}
+
 int oxh_combined_hash_device(const uint64_t* d_content, const uint64_t* d_metadata, uint64_t n, uint64_t* d_out,
                              void* stream) {
     if (n == 0) return OXH_OK;

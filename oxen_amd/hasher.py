@@ -331,43 +331,79 @@ def get_combined_hash(oxen_metadata_hash: Optional[int], content_hash: int) -> i
     return hash_streams_128bit([stream])[0]
 
 
+class Xxh3:
+    """xxhash-rust `Xxh3` (new / update / digest128) on the GPU through oxh_xxh3_stream_*: bytes are
+    staged in pinned memory and hashed on the device in 16 MiB pieces as they arrive, so a stream of
+    any length holds bounded memory. `digest128()` does not consume the state."""
+
+    def __init__(self, ctx: Optional[_capi.Context] = None):
+        self._ctx = ctx or default_context()  # keeps the context alive as long as the stream
+        h = _capi._vp()
+        _capi.check(_capi.lib().oxh_xxh3_stream_create(self._ctx.handle, ctypes.byref(h)), "oxh_xxh3_stream_create")
+        self._h = h
+
+    def update(self, data) -> None:
+        mv = memoryview(data).cast("B")
+        if not mv.nbytes:
+            return
+        arr = np.frombuffer(mv, dtype=np.uint8)  # no copy, read-only buffers included
+        _capi.check(_capi.lib().oxh_xxh3_stream_update(self._h, arr.ctypes.data, mv.nbytes), "oxh_xxh3_stream_update")
+
+    def digest128(self) -> int:
+        out = (ctypes.c_uint64 * 2)()
+        _capi.check(_capi.lib().oxh_xxh3_stream_digest(self._h, out), "oxh_xxh3_stream_digest")
+        return _to_u128(out[0], out[1])
+
+    def reset(self) -> None:
+        _capi.check(_capi.lib().oxh_xxh3_stream_reset(self._h), "oxh_xxh3_stream_reset")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            _capi.lib().oxh_xxh3_stream_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class HashingReader:
-    """hasher.rs:183-209: wraps a reader, feeds every byte read into the hash.
+    """hasher.rs:183-209: wraps a reader, feeds every byte read into an `Xxh3` (GPU stream)."""
 
-    XXH3's streaming form equals its one-shot form, so the bytes are kept and hashed on the GPU when
-    `digest128()` is asked for."""
-
-    def __init__(self, inner):
+    def __init__(self, inner, ctx: Optional[_capi.Context] = None):
         self.inner = inner
-        self._buf = bytearray()
+        self.hasher = Xxh3(ctx)
 
     def read(self, n: int = -1) -> bytes:
         b = self.inner.read(n)
         if b:
-            self._buf += b
+            self.hasher.update(b)
         return b
 
     def digest128(self) -> int:
-        return hash_buffer_128bit(bytes(self._buf))
+        return self.hasher.digest128()
 
 
 class HashingWriter:
-    """hasher.rs:214-244: wraps a writer, feeds every byte successfully written into the hash."""
+    """hasher.rs:214-244: wraps a writer, feeds every byte successfully written into an `Xxh3`
+    (only the bytes the inner writer accepted, as in the reference's short-write test)."""
 
-    def __init__(self, inner):
+    def __init__(self, inner, ctx: Optional[_capi.Context] = None):
         self.inner = inner
-        self._buf = bytearray()
+        self.hasher = Xxh3(ctx)
 
     def write(self, b: bytes) -> int:
         n = self.inner.write(b)
         if n is None:
             n = len(b)
         if n > 0:
-            self._buf += bytes(b[:n])
+            self.hasher.update(memoryview(b)[:n])
         return n
 
     def flush(self) -> None:
         self.inner.flush()
 
     def digest128(self) -> int:
-        return hash_buffer_128bit(bytes(self._buf))
+        return self.hasher.digest128()

@@ -1,0 +1,99 @@
+"""Streaming XXH3 on the GPU (oxh_xxh3_stream_*, the `Xxh3` of hasher.rs) and the HashingReader /
+HashingWriter mirrors -- the reference's own tests (hasher.rs:246-350) restated, plus piece-boundary
+lengths, ragged updates and digests taken mid-stream, all against the oracle."""
+import io
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+PAYLOAD = b"the quick brown fox jumps over the lazy dog"
+
+
+def test_sync_reader_matches_one_shot(cuda, oracle_lib):  # hasher.rs:250-259
+    from oxen_amd import hasher
+
+    hashing = hasher.HashingReader(io.BytesIO(PAYLOAD))
+    sink = b""
+    while chunk := hashing.read(7):
+        sink += chunk
+    assert sink == PAYLOAD
+    assert hashing.digest128() == oracle_lib.xxh3_128_int(PAYLOAD)
+
+
+def test_sync_reader_empty_input(cuda, oracle_lib):  # hasher.rs:261-269
+    from oxen_amd import hasher
+
+    hashing = hasher.HashingReader(io.BytesIO(b""))
+    assert hashing.read() == b""
+    assert hashing.digest128() == oracle_lib.xxh3_128_int(b"")
+
+
+def test_sync_writer_matches_one_shot_and_accumulates(cuda, oracle_lib):  # hasher.rs:276-308
+    from oxen_amd import hasher
+
+    sink = io.BytesIO()
+    w = hasher.HashingWriter(sink)
+    w.write(PAYLOAD)
+    w.flush()
+    assert w.digest128() == oracle_lib.xxh3_128_int(PAYLOAD) and sink.getvalue() == PAYLOAD
+    sink = io.BytesIO()
+    w = hasher.HashingWriter(sink)
+    for chunk in (b"hello ", b"brave ", b"world"):
+        w.write(chunk)
+    assert w.digest128() == oracle_lib.xxh3_128_int(b"hello brave world")
+    assert hasher.HashingWriter(io.BytesIO()).digest128() == oracle_lib.xxh3_128_int(b"")
+
+
+def test_sync_writer_hashes_only_accepted_bytes(cuda, oracle_lib):  # hasher.rs:321-349
+    from oxen_amd import hasher
+
+    class ShortWriter:
+        def __init__(self):
+            self.written = b""
+
+        def write(self, b):
+            n = min(len(b), 4)
+            self.written += bytes(b[:n])
+            return n
+
+        def flush(self):
+            pass
+
+    inner = ShortWriter()
+    w = hasher.HashingWriter(inner)
+    assert w.write(b"0123456789") == 4
+    assert inner.written == b"0123" and w.digest128() == oracle_lib.xxh3_128_int(b"0123")
+
+
+@pytest.mark.parametrize("piece_mib", ["1", None], ids=["1MiB-pieces", "16MiB-pieces"])
+def test_stream_pieces_ragged_updates_and_mid_stream_digests(cuda, oracle_lib, monkeypatch, piece_mib):
+    """Lengths around every piece boundary (S + 1024, S + 1025, S + 1026, 2S + 2049 ...), updates of
+    ragged sizes (1 B to several pieces at once), a digest after every update (the state must not
+    change), and reset()."""
+    from oxen_amd import hasher
+    from oxen_amd.workloads import splitmix_bytes
+
+    if piece_mib:
+        monkeypatch.setenv("OXH_STREAM_PIECE_MIB", piece_mib)
+    S = (int(piece_mib) if piece_mib else 16) << 20
+    data = splitmix_bytes(4242, 0, 3 * S + 5000).tobytes()
+    marks = sorted({0, 1, 240, 241, 1024, 1025, 4096, S - 1, S, S + 1023, S + 1024, S + 1025, S + 1026,
+                    2 * S + 2048, 2 * S + 2049, 2 * S + 2050, 3 * S + 5000})
+    rng = np.random.default_rng(5)
+    h = hasher.Xxh3()
+    pos = 0
+    for m in marks:
+        while pos < m:  # ragged updates up to the next mark
+            step = int(min(m - pos, rng.choice([1, 7, 63, 1025, 70_000, S + 3])))
+            h.update(data[pos:pos + step])
+            pos += step
+        assert h.digest128() == oracle_lib.xxh3_128_int(data[:m]), m
+        assert h.digest128() == oracle_lib.xxh3_128_int(data[:m]), m  # digest does not consume
+    h.reset()
+    h.update(data[:S + 1025])
+    assert h.digest128() == oracle_lib.xxh3_128_int(data[:S + 1025])
+    h.update(bytearray(data[S + 1025:S + 9000]))  # writable buffers as well as bytes
+    assert h.digest128() == oracle_lib.xxh3_128_int(data[:S + 9000])
+    h.close()
