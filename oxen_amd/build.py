@@ -33,8 +33,41 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in DEPS)
 
 
+HOST_SRC = os.path.join(HERE, "host", "oxen_hasher.cpp")
+HOST_HDR = os.path.join(HERE, "host", "oxen_hasher.hpp")
+HOST_LIB = os.path.join(HERE, "liboxen_hasher.so")
+NATIVE_TEST_SRC = os.path.join(ROOT, "tests", "native", "test_hasher.cpp")
+NATIVE_TEST = os.path.join(ROOT, "tests", "native", "test_hasher")
+
+
+def _stale(target: str, deps: list[str]) -> bool:
+    return not os.path.exists(target) or any(os.path.getmtime(d) > os.path.getmtime(target) for d in deps)
+
+
+def build_host(force: bool = False, verbose: bool = False) -> str:
+    """The C++ mirror of liboxen `util::hasher` over the C ABI (oxen_amd/host, g++) and its native
+    test program (tests/native/test_hasher.cpp), both linked against liboxen_hash.so."""
+    hdr = os.path.join(ROOT, "include", "oxen_hash.h")
+    steps = [
+        (HOST_LIB, [HOST_SRC, HOST_HDR, hdr, LIB],
+         ["g++", "-std=c++17", "-O2", "-Wall", "-shared", "-fPIC", "-o", HOST_LIB + ".tmp", HOST_SRC,
+          f"-L{HERE}", "-l:liboxen_hash.so", "-Wl,-rpath,$ORIGIN"]),
+        (NATIVE_TEST, [NATIVE_TEST_SRC, HOST_HDR, HOST_LIB],
+         ["g++", "-std=c++17", "-O2", "-Wall", "-o", NATIVE_TEST + ".tmp", NATIVE_TEST_SRC,
+          f"-L{HERE}", "-l:liboxen_hasher.so", "-l:liboxen_hash.so", "-Wl,-rpath,$ORIGIN/../../oxen_amd"]),
+    ]
+    for target, deps, cmd in steps:
+        if force or _stale(target, deps):
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            subprocess.run(cmd, check=True)
+            os.replace(target + ".tmp", target)
+    return HOST_LIB
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
+        build_host(verbose=verbose)
         return LIB
     tmp = LIB + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall", "-Wl,--no-undefined",
@@ -43,6 +76,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
+    build_host(force=True, verbose=verbose)
     return LIB
 
 

@@ -1,0 +1,208 @@
+// oxen_amd/host/oxen_hasher.cpp -- liboxen `util::hasher` mirror over the C ABI (see the header).
+#include "oxen_hasher.hpp"
+
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdlib>
+#include <mutex>
+#include <thread>
+
+#include "../../include/oxen_hash.h"
+
+namespace liboxen {
+
+namespace {
+
+u128 to_u128(uint64_t lo, uint64_t hi) { return ((u128)hi << 64) | lo; }
+
+[[noreturn]] void raise(int rc, const char* what) {
+    const std::string msg = std::string(what) + ": " + oxh_last_error();
+    throw OxenError(rc == OXH_ERR_NODEVICE ? OxenError::Kind::NoDevice : OxenError::Kind::Basic, msg, rc);
+}
+
+void check(int rc, const char* what) {
+    if (rc != OXH_OK) raise(rc, what);
+}
+
+}  // namespace
+
+MerkleHash MerkleHash::from_str(std::string_view s) {
+    // u128::from_str_radix(s, 16): optional '+', at least one digit, no overflow
+    if (!s.empty() && s[0] == '+') s.remove_prefix(1);
+    if (s.empty()) throw OxenError::basic_str("cannot parse integer from empty string");
+    u128 v = 0;
+    for (char ch : s) {
+        int d;
+        if (ch >= '0' && ch <= '9') d = ch - '0';
+        else if (ch >= 'a' && ch <= 'f') d = ch - 'a' + 10;
+        else if (ch >= 'A' && ch <= 'F') d = ch - 'A' + 10;
+        else throw OxenError::basic_str("invalid digit found in string");
+        if (v >> 124) throw OxenError::basic_str("number too large to fit in target type");
+        v = (v << 4) | (u128)d;
+    }
+    return MerkleHash(v);
+}
+
+std::string MerkleHash::to_string() const { return util::hasher::format_hex(v_); }
+
+std::string MerkleHash::to_short_str() const {
+    const std::string s = to_string();
+    return s.size() > 10 ? s.substr(0, 10) : s;
+}
+
+void MerkleHash::to_le_bytes(uint8_t out[16]) const {
+    for (int i = 0; i < 16; ++i) out[i] = (uint8_t)(v_ >> (8 * i));
+}
+
+std::string MerkleHash::node_db_prefix() const {
+    const std::string s = to_string();
+    return s.substr(0, 3) + "/" + (s.size() > 3 ? s.substr(3) : std::string());
+}
+
+namespace util::hasher {
+
+oxh_ctx* default_context() {
+    static std::once_flag once;
+    static oxh_ctx* ctx = nullptr;
+    static int rc = OXH_OK;
+    static std::string err;
+    std::call_once(once, [] {
+        const char* dev = getenv("OXH_DEVICE");
+        rc = oxh_ctx_create(dev ? atoi(dev) : 0, 0, &ctx);
+        if (rc != OXH_OK) err = oxh_last_error();
+    });
+    if (rc != OXH_OK)
+        throw OxenError(rc == OXH_ERR_NODEVICE ? OxenError::Kind::NoDevice : OxenError::Kind::Basic,
+                        "oxh_ctx_create: " + err, rc);
+    return ctx;
+}
+
+std::string format_hex(u128 v) {
+    char buf[40];
+    const int n = oxh_format_hex((uint64_t)v, (uint64_t)(v >> 64), buf);
+    return std::string(buf, (size_t)n);
+}
+
+std::vector<u128> hash_buffers_128bit(const std::vector<std::string_view>& buffers, oxh_ctx* ctx) {
+    ctx = ctx ? ctx : default_context();
+    const size_t n = buffers.size();
+    std::vector<const uint8_t*> ptrs(n);
+    std::vector<uint64_t> lens(n), out(2 * n);
+    for (size_t i = 0; i < n; ++i) {
+        ptrs[i] = reinterpret_cast<const uint8_t*>(buffers[i].data());
+        lens[i] = buffers[i].size();
+    }
+    check(oxh_hash_buffers(ctx, ptrs.data(), lens.data(), n, out.data()), "oxh_hash_buffers");
+    std::vector<u128> r(n);
+    for (size_t i = 0; i < n; ++i) r[i] = to_u128(out[2 * i], out[2 * i + 1]);
+    return r;
+}
+
+u128 hash_buffer_128bit(const void* data, size_t len) {
+    return hash_buffers_128bit({std::string_view(static_cast<const char*>(data), len)})[0];
+}
+
+std::string hash_buffer(const void* data, size_t len) { return format_hex(hash_buffer_128bit(data, len)); }
+
+std::string hash_str(std::string_view s) { return hash_buffer(s.data(), s.size()); }
+
+std::vector<FileHash> hash_files(const std::vector<std::string>& paths, oxh_ctx* ctx) {
+    ctx = ctx ? ctx : default_context();
+    const size_t n = paths.size();
+    std::vector<const char*> cp(n);
+    for (size_t i = 0; i < n; ++i) cp[i] = paths[i].c_str();
+    std::vector<uint64_t> out(2 * n), sizes(n);
+    std::vector<int32_t> status(n);
+    check(oxh_hash_files(ctx, cp.data(), n, out.data(), sizes.data(), status.data()), "oxh_hash_files");
+    std::vector<FileHash> r(n);
+    for (size_t i = 0; i < n; ++i) {
+        if (status[i] == OXH_OK) {
+            r[i].ok = true;
+            r[i].hash = to_u128(out[2 * i], out[2 * i + 1]);
+            r[i].size = sizes[i];
+        } else if (access(paths[i].c_str(), F_OK) != 0) {  // File::open failed (hasher.rs:142-146)
+            r[i].error = "util::hasher::hash_file_contents Could not open file \"" + paths[i] + "\"";
+        } else {  // read_to_end failed (hasher.rs:136-139)
+            r[i].error = "Could not read file for hashing";
+        }
+    }
+    return r;
+}
+
+namespace {
+u128 hash_one_file(const std::string& path) {
+    const std::vector<FileHash> r = hash_files({path});
+    if (!r[0].ok) throw OxenError::basic_str(r[0].error, OXH_ERR_IO);
+    return r[0].hash;
+}
+}  // namespace
+
+// Both size branches (one-shot below 1e9 B, 4 KiB streaming above) give the same XXH3-128; here
+// both go through the batched file path (K1, or the K1L piece pipeline above a staging slot).
+u128 get_hash_given_metadata(const std::string& path, const struct stat& metadata) {
+    (void)metadata;
+    return hash_one_file(path);
+}
+
+u128 u128_hash_file_contents(const std::string& path) {
+    struct stat sb;
+    if (stat(path.c_str(), &sb) != 0)  // util::fs::metadata(path)? (hasher.rs:105)
+        throw OxenError::basic_str("Could not get metadata for \"" + path + "\"", OXH_ERR_IO);
+    return hash_one_file(path);
+}
+
+std::string hash_file_contents(const std::string& path) { return format_hex(u128_hash_file_contents(path)); }
+
+std::string hash_file_contents_with_retry(const std::string& path, int total_retries,
+                                          const std::function<void(int)>& sleep) {
+    int timeout = 1, retries = 0;
+    for (;;) {
+        try {
+            return hash_file_contents(path);
+        } catch (const OxenError&) {
+            retries += 1;
+            timeout *= 2;
+            if (sleep) sleep(timeout);
+            else std::this_thread::sleep_for(std::chrono::seconds(timeout));
+            if (retries > total_retries) throw;
+        }
+    }
+}
+
+u128 get_combined_hash(std::optional<u128> oxen_metadata_hash, u128 content_hash) {
+    if (!oxen_metadata_hash) return content_hash;
+    uint8_t buf[32];
+    MerkleHash(content_hash).to_le_bytes(buf);
+    MerkleHash(*oxen_metadata_hash).to_le_bytes(buf + 16);
+    return hash_buffer_128bit(buf, sizeof buf);
+}
+
+u128 get_metadata_hash(const std::optional<std::string>& metadata_json) {
+    const std::string s = metadata_json ? *metadata_json : std::string("null");
+    return hash_buffer_128bit(s.data(), s.size());
+}
+
+std::optional<u128> maybe_get_metadata_hash(const std::optional<std::string>& metadata_json) {
+    if (!metadata_json) return std::nullopt;
+    return get_metadata_hash(metadata_json);
+}
+
+Xxh3::Xxh3(oxh_ctx* ctx) {
+    check(oxh_xxh3_stream_create(ctx ? ctx : default_context(), &s_), "oxh_xxh3_stream_create");
+}
+
+Xxh3::~Xxh3() { oxh_xxh3_stream_destroy(s_); }
+
+void Xxh3::update(const void* data, size_t len) { check(oxh_xxh3_stream_update(s_, data, len), "oxh_xxh3_stream_update"); }
+
+u128 Xxh3::digest128() const {
+    uint64_t out[2];
+    check(oxh_xxh3_stream_digest(s_, out), "oxh_xxh3_stream_digest");
+    return to_u128(out[0], out[1]);
+}
+
+void Xxh3::reset() { check(oxh_xxh3_stream_reset(s_), "oxh_xxh3_stream_reset"); }
+
+}  // namespace util::hasher
+}  // namespace liboxen

@@ -1,0 +1,157 @@
+// oxen_amd/host/oxen_hasher.hpp -- C++ host mirror of liboxen `util::hasher`
+// (crates/liboxen/src/util/hasher.rs) over the MI355X C ABI (include/oxen_hash.h).
+//
+// The reference is Rust; its toolchain is not in this image, so the host side above the C ABI is
+// C++: the same function names, argument meaning and error behaviour as the Rust module, with
+// Result<T, OxenError> mapped to "returns T or throws OxenError" and u128 to unsigned __int128
+// (MerkleHash, model/merkle_tree/merkle_hash.rs:16). Every digest is computed on the GPU; there is
+// no CPU hashing path (without a gfx950 device every call throws OxenError).
+#pragma once
+
+#include <sys/stat.h>
+
+#include <cstdint>
+#include <functional>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <string_view>
+#include <vector>
+
+struct oxh_ctx;
+struct oxh_xxh3_stream;
+
+namespace liboxen {
+
+using u128 = unsigned __int128;
+
+// error/mod.rs: the variants this path raises, with the reference's messages.
+class OxenError : public std::runtime_error {
+   public:
+    enum class Kind { Basic, HashMismatch, NoDevice };
+    OxenError(Kind k, const std::string& msg, int code = 0) : std::runtime_error(msg), kind_(k), code_(code) {}
+    static OxenError basic_str(const std::string& msg, int code = 0) { return OxenError(Kind::Basic, msg, code); }
+    Kind kind() const { return kind_; }
+    int code() const { return code_; }  // the C ABI status (OXH_ERR_*) behind it, 0 if none
+
+   private:
+    Kind kind_;
+    int code_;
+};
+
+// model/merkle_tree/merkle_hash.rs:16-131
+class MerkleHash {
+   public:
+    MerkleHash() = default;
+    explicit MerkleHash(u128 v) : v_(v) {}
+    static MerkleHash from_str(std::string_view hex);  // FromStr, radix 16 (:54-61)
+    u128 to_u128() const { return v_; }
+    std::string to_string() const;                      // Display "{:x}", unpadded (:73-77)
+    std::string to_short_str() const;                   // first 10 hex chars (:79-83)
+    void to_le_bytes(uint8_t out[16]) const;            // (:25-27)
+    std::string node_db_prefix() const;                 // "{hex[..3]}/{hex[3..]}" (:125-131)
+    bool operator==(const MerkleHash& o) const { return v_ == o.v_; }
+    bool operator!=(const MerkleHash& o) const { return v_ != o.v_; }
+
+   private:
+    u128 v_ = 0;
+};
+
+namespace util::hasher {
+
+// The process-wide GPU context (device $OXH_DEVICE, default 0), created on first use.
+oxh_ctx* default_context();
+
+std::string format_hex(u128 v);  // format!("{:x}", u128)
+
+std::string hash_buffer(const void* data, size_t len);        // hasher.rs:11-14
+std::string hash_str(std::string_view s);                      // hasher.rs:16-19
+u128 hash_buffer_128bit(const void* data, size_t len);        // hasher.rs:28-30
+inline u128 hash_buffer_128bit(std::string_view s) { return hash_buffer_128bit(s.data(), s.size()); }
+
+u128 get_hash_given_metadata(const std::string& path, const struct stat& metadata);  // hasher.rs:56-65
+u128 u128_hash_file_contents(const std::string& path);                               // hasher.rs:102-112
+std::string hash_file_contents(const std::string& path);                             // hasher.rs:114-124
+// hasher.rs:32-54: exponential backoff 2, 4, 8 ... s; `sleep` is injectable for tests
+std::string hash_file_contents_with_retry(const std::string& path, int total_retries = 5,
+                                          const std::function<void(int)>& sleep = nullptr);
+
+// hasher.rs:67-80
+u128 get_combined_hash(std::optional<u128> oxen_metadata_hash, u128 content_hash);
+// hasher.rs:82-100: XXH3-128 of serde_json::to_string(&Option<GenericMetadata>); the caller passes
+// the JSON text (nullopt = None, serialised as "null")
+u128 get_metadata_hash(const std::optional<std::string>& metadata_json);
+std::optional<u128> maybe_get_metadata_hash(const std::optional<std::string>& metadata_json);
+
+// The batched form the add loop calls once per batch (add.rs:422-444): one entry per path, the
+// digest and size, or the error hash_small_file_contents would have raised (hasher.rs:126-148).
+struct FileHash {
+    bool ok = false;
+    u128 hash = 0;
+    uint64_t size = 0;
+    std::string error;
+};
+std::vector<FileHash> hash_files(const std::vector<std::string>& paths, oxh_ctx* ctx = nullptr);
+std::vector<u128> hash_buffers_128bit(const std::vector<std::string_view>& buffers, oxh_ctx* ctx = nullptr);
+
+// xxhash-rust Xxh3 (new / update / digest128 / reset) on the GPU (oxh_xxh3_stream_*).
+class Xxh3 {
+   public:
+    explicit Xxh3(oxh_ctx* ctx = nullptr);
+    ~Xxh3();
+    Xxh3(const Xxh3&) = delete;
+    Xxh3& operator=(const Xxh3&) = delete;
+    void update(const void* data, size_t len);
+    void update(std::string_view s) { update(s.data(), s.size()); }
+    u128 digest128() const;
+    void reset();
+
+   private:
+    oxh_xxh3_stream* s_ = nullptr;
+};
+
+// hasher.rs:183-209. R: size_t read(uint8_t* buf, size_t n) (0 = EOF; throws on error).
+template <class R>
+class HashingReader {
+   public:
+    explicit HashingReader(R& inner, oxh_ctx* ctx = nullptr) : inner_(inner), hasher_(ctx) {}
+    size_t read(uint8_t* buf, size_t n) {
+        const size_t got = inner_.read(buf, n);
+        if (got > 0) hasher_.update(buf, got);
+        return got;
+    }
+    u128 digest128() const { return hasher_.digest128(); }
+
+   private:
+    R& inner_;
+    Xxh3 hasher_;
+};
+
+// hasher.rs:214-244. W: size_t write(const uint8_t* buf, size_t n) (bytes accepted), void flush().
+template <class W>
+class HashingWriter {
+   public:
+    explicit HashingWriter(W& inner, oxh_ctx* ctx = nullptr) : inner_(inner), hasher_(ctx) {}
+    size_t write(const uint8_t* buf, size_t n) {
+        const size_t put = inner_.write(buf, n);
+        if (put > 0) hasher_.update(buf, put);  // only what the inner writer accepted
+        return put;
+    }
+    void write_all(const uint8_t* buf, size_t n) {
+        while (n) {
+            const size_t put = write(buf, n);
+            if (put == 0) throw OxenError::basic_str("failed to write whole buffer");
+            buf += put;
+            n -= put;
+        }
+    }
+    void flush() { inner_.flush(); }
+    u128 digest128() const { return hasher_.digest128(); }
+
+   private:
+    W& inner_;
+    Xxh3 hasher_;
+};
+
+}  // namespace util::hasher
+}  // namespace liboxen

@@ -1,0 +1,231 @@
+// tests/native/test_hasher.cpp -- the C++ host mirror of liboxen `util::hasher` on the GPU, tested
+// the way the reference tests hasher.rs (hashing_reader_tests / hashing_writer_tests, :246-350), plus
+// known-answer digests (the reference's schemas.rs:131 KAT, data/test/text/hello.txt),
+// the error behaviour of the file functions, MerkleHash formatting and a long GPU stream.
+//
+// Built by oxen_amd/build.py (g++ against liboxen_hasher.so + liboxen_hash.so); run by
+// tests/test_native_mirror.py on the GPU box. argv[1] = tests/golden. Exit status 0 = all passed.
+#include <sys/stat.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../oxen_amd/host/oxen_hasher.hpp"
+
+using liboxen::MerkleHash;
+using liboxen::OxenError;
+using liboxen::u128;
+namespace hasher = liboxen::util::hasher;
+
+static int g_fail = 0, g_pass = 0;
+#define CHECK(cond)                                                               \
+    do {                                                                          \
+        if (cond) {                                                               \
+            ++g_pass;                                                             \
+        } else {                                                                  \
+            ++g_fail;                                                             \
+            fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #cond);       \
+        }                                                                         \
+    } while (0)
+
+template <class F>
+static bool throws_oxen(F f, const char* needle = nullptr) {
+    try {
+        f();
+    } catch (const OxenError& e) {
+        return !needle || strstr(e.what(), needle) != nullptr;
+    }
+    return false;
+}
+
+static u128 hex(const char* s) { return MerkleHash::from_str(s).to_u128(); }
+
+// a `Read` over a byte string, `chunk` bytes per call
+struct SliceReader {
+    const std::string& data;
+    size_t pos = 0, chunk;
+    size_t read(uint8_t* buf, size_t n) {
+        const size_t k = std::min({n, chunk, data.size() - pos});
+        memcpy(buf, data.data() + pos, k);
+        pos += k;
+        return k;
+    }
+};
+
+struct VecWriter {
+    std::string written;
+    size_t write(const uint8_t* b, size_t n) {
+        written.append(reinterpret_cast<const char*>(b), n);
+        return n;
+    }
+    void flush() {}
+};
+
+struct ShortWriter {  // hasher.rs:323-335: accepts at most 4 bytes per call
+    std::string written;
+    size_t write(const uint8_t* b, size_t n) {
+        const size_t k = std::min<size_t>(n, 4);
+        written.append(reinterpret_cast<const char*>(b), k);
+        return k;
+    }
+    void flush() {}
+};
+
+static const std::string kPayload = "the quick brown fox jumps over the lazy dog";
+
+static void hashing_reader_tests() {
+    {  // sync_reader_matches_one_shot (hasher.rs:250-259)
+        SliceReader src{kPayload, 0, 5};
+        hasher::HashingReader<SliceReader> hashing(src);
+        std::string sink;
+        uint8_t buf[64];
+        while (size_t n = hashing.read(buf, sizeof buf)) sink.append(reinterpret_cast<char*>(buf), n);
+        CHECK(sink == kPayload);
+        CHECK(hashing.digest128() == hasher::hash_buffer_128bit(kPayload));
+        CHECK(hashing.digest128() == hex("e9a1932627d7f46d15c21eead63fa21f"));
+    }
+    {  // sync_reader_empty_input (:261-269)
+        const std::string empty;
+        SliceReader src{empty, 0, 5};
+        hasher::HashingReader<SliceReader> hashing(src);
+        uint8_t buf[8];
+        CHECK(hashing.read(buf, sizeof buf) == 0);
+        CHECK(hashing.digest128() == hex("99aa06d3014798d86001c324468d497f"));
+    }
+}
+
+static void hashing_writer_tests() {
+    {  // sync_writer_matches_one_shot (:276-289)
+        VecWriter sink;
+        u128 digest;
+        {
+            hasher::HashingWriter<VecWriter> hashing(sink);
+            hashing.write_all(reinterpret_cast<const uint8_t*>(kPayload.data()), kPayload.size());
+            hashing.flush();
+            digest = hashing.digest128();
+        }
+        CHECK(digest == hasher::hash_buffer_128bit(kPayload));
+        CHECK(sink.written == kPayload);
+    }
+    {  // sync_writer_accumulates_across_writes (:293-308)
+        VecWriter sink;
+        hasher::HashingWriter<VecWriter> hashing(sink);
+        for (const char* chunk : {"hello ", "brave ", "world"})
+            hashing.write_all(reinterpret_cast<const uint8_t*>(chunk), strlen(chunk));
+        CHECK(hashing.digest128() == hex("6a11bc56dc3c4cce2f81a90bed1a8d2c"));
+        CHECK(sink.written == "hello brave world");
+    }
+    {  // sync_writer_empty_input (:310-317)
+        VecWriter sink;
+        CHECK(hasher::HashingWriter<VecWriter>(sink).digest128() == hex("99aa06d3014798d86001c324468d497f"));
+        CHECK(sink.written.empty());
+    }
+    {  // sync_writer_hashes_only_accepted_bytes (:321-349)
+        ShortWriter inner;
+        u128 digest;
+        {
+            hasher::HashingWriter<ShortWriter> hashing(inner);
+            const size_t accepted = hashing.write(reinterpret_cast<const uint8_t*>("0123456789"), 10);
+            CHECK(accepted == 4);
+            digest = hashing.digest128();
+        }
+        CHECK(inner.written == "0123");
+        CHECK(digest == hex("e7f00c8d576b45ee824b77d5917b737b"));
+    }
+}
+
+static void known_answers(const std::string& golden) {
+    CHECK(hasher::hash_str("") == "99aa06d3014798d86001c324468d497f");
+    CHECK(hasher::hash_str("hello") == "b5e9c1ad071b3e7fc779cfaa5e523818");
+    CHECK(hasher::hash_str(std::string(65536, 'x')) == "2da4b9c5a75caad3688558138047f8a");  // unpadded
+    // repositories/data_frames/schemas.rs:131
+    CHECK(hasher::hash_str("filestrlabelstrmin_xf64min_yf64widthi64heighti64") == "b821946753334c083124fd563377d795");
+    // add.rs:833-842 on a C1 text file: content, metadata and combined hashes
+    const u128 c = hasher::hash_buffer_128bit(std::string_view("File content 0"));
+    CHECK(hasher::format_hex(c) == "393ba5849f5590fc5985c4bbcec0003f");
+    const auto m = hasher::maybe_get_metadata_hash(std::string("{\"text\":{\"num_lines\":1,\"num_chars\":14}}"));
+    CHECK(m && hasher::format_hex(*m) == "5b1951f1adb8e39ebda9b20e8c20a11");
+    CHECK(hasher::format_hex(hasher::get_combined_hash(m, c)) == "957a1ebb6676cdb2a326863b0858a474");
+    CHECK(hasher::get_combined_hash(std::nullopt, c) == c);
+    CHECK(!hasher::maybe_get_metadata_hash(std::nullopt));
+    CHECK(hasher::get_metadata_hash(std::nullopt) == hasher::hash_buffer_128bit(std::string_view("null")));
+    // the reference's data/test fixture (tests/golden/data_test/text/hello.txt)
+    const std::string hello = golden + "/data_test/text/hello.txt";
+    CHECK(hasher::hash_file_contents(hello) == "1bfd09d1a433fb78117b4c7b1583d16d");
+    struct stat sb;
+    CHECK(stat(hello.c_str(), &sb) == 0 && hasher::format_hex(hasher::get_hash_given_metadata(hello, sb)) ==
+                                               "1bfd09d1a433fb78117b4c7b1583d16d");
+}
+
+static void file_errors(const std::string& golden) {
+    const std::string missing = golden + "/no-such-file";
+    CHECK(throws_oxen([&] { hasher::hash_file_contents(missing); }, "Could not get metadata"));
+    struct stat sb {};
+    CHECK(throws_oxen([&] { hasher::get_hash_given_metadata(missing, sb); }, "Could not open file"));
+    CHECK(throws_oxen([&] { hasher::get_hash_given_metadata(golden, sb); }, "Could not read file for hashing"));
+    std::vector<int> sleeps;
+    CHECK(throws_oxen([&] { hasher::hash_file_contents_with_retry(missing, 5, [&](int s) { sleeps.push_back(s); }); }));
+    CHECK((sleeps == std::vector<int>{2, 4, 8, 16, 32, 64}));  // hasher.rs:32-54
+    const auto r = hasher::hash_files({golden + "/data_test/text/hello.txt", missing, golden});
+    CHECK(r.size() == 3 && r[0].ok && r[0].size == 5 && !r[1].ok && !r[2].ok);
+    CHECK(r[1].error.find("Could not open file") != std::string::npos);
+    CHECK(r[2].error == "Could not read file for hashing");
+}
+
+static void merkle_hash() {
+    const MerkleHash h = MerkleHash::from_str("2da4b9c5a75caad3688558138047f8a");
+    CHECK(h.to_string() == "2da4b9c5a75caad3688558138047f8a");
+    CHECK(h.to_short_str() == "2da4b9c5a7");
+    CHECK(h.node_db_prefix() == "2da/4b9c5a75caad3688558138047f8a");
+    uint8_t le[16];
+    h.to_le_bytes(le);
+    CHECK(le[0] == 0x8a && le[15] == 0x02);
+    CHECK(MerkleHash::from_str("FF").to_u128() == 255 && MerkleHash::from_str("+1").to_u128() == 1);
+    CHECK(MerkleHash(0).to_string() == "0");
+    CHECK(throws_oxen([] { MerkleHash::from_str(""); }));
+    CHECK(throws_oxen([] { MerkleHash::from_str("xyz"); }));
+    CHECK(throws_oxen([] { MerkleHash::from_str("1ffffffffffffffffffffffffffffffff"); }));  // 33 digits
+}
+
+static void long_stream() {
+    // 40 MiB + 1234 B in ragged updates: three 16 MiB device pieces with resumed chains + the tail
+    std::string data(40u * 1024 * 1024 + 1234, '\0');
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    for (size_t i = 0; i < data.size(); i += 8) {
+        x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+        memcpy(&data[i], &x, std::min<size_t>(8, data.size() - i));
+    }
+    hasher::Xxh3 h;
+    size_t pos = 0, step = 1;
+    while (pos < data.size()) {
+        const size_t k = std::min(step, data.size() - pos);
+        h.update(data.data() + pos, k);
+        pos += k;
+        step = step * 7 % 5000011 + 1;
+    }
+    const u128 one_shot = hasher::hash_buffer_128bit(data.data(), data.size());
+    CHECK(h.digest128() == one_shot);
+    CHECK(h.digest128() == one_shot);  // digest128 does not consume the state
+    h.reset();
+    h.update(std::string_view("hello"));
+    CHECK(h.digest128() == hex("b5e9c1ad071b3e7fc779cfaa5e523818"));
+}
+
+int main(int argc, char** argv) {
+    const std::string golden = argc > 1 ? argv[1] : "tests/golden";
+    try {
+        hashing_reader_tests();
+        hashing_writer_tests();
+        known_answers(golden);
+        file_errors(golden);
+        merkle_hash();
+        long_stream();
+    } catch (const std::exception& e) {
+        fprintf(stderr, "FAIL: unexpected exception: %s\n", e.what());
+        ++g_fail;
+    }
+    printf("%d passed, %d failed\n", g_pass, g_fail);
+    return g_fail ? 1 : 0;
+}
