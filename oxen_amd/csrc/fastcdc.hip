@@ -67,9 +67,10 @@ constexpr int kHashSpan = 47;          // positions after a chunk's start index 
 struct CdcParams {
     uint64_t min, avg, max;
     uint64_t mask_s, mask_l;
-    uint64_t sec;      // section bytes: a multiple of 1 KiB
+    uint64_t sec;      // section bytes: a multiple of 8 KiB (F1 wave / F2 lane unit)
+    uint64_t unit;     // sec / 64: the candidate list unit (F1 lane)
     uint64_t warmup;   // bytes a speculative walk runs before its section (unrecorded)
-    uint32_t cap;      // candidate entries stored per section
+    uint32_t cap;      // candidate entries stored per unit
     uint32_t speccap;  // speculative chunk starts stored per section
 };
 
@@ -79,10 +80,10 @@ struct CdcFiles {
     const uint64_t* flen;      // [n]
     const uint64_t* sec_base;  // [n+1] first global section of each file
     const uint32_t* sec_file;  // [n_sec] file of each section
-    uint32_t* cand;            // [n_sec * cap] candidate groups: offset in the section (16-aligned), in order
-    uint64_t* cand_h;          // [n_sec * cap] full-window hash before each group's first byte (mod 2^48)
-    uint4* cand_b;             // [n_sec * cap] the group's 16 bytes (the walk resolves flags from these)
-    uint32_t* cand_cnt;        // [n_sec] true count (> cap: list truncated, dense fallback)
+    uint32_t* cand;            // [n_sec * 64 * cap] candidate groups per unit: offset in the unit (16-aligned), in order
+    uint64_t* cand_h;          // [n_sec * 64 * cap] full-window hash before each group's first byte (mod 2^48)
+    uint4* cand_b;             // [n_sec * 64 * cap] the group's 16 bytes (the walk resolves flags from these)
+    uint32_t* cand_cnt;        // [n_sec * 64] true count per unit (> cap: list truncated, dense fallback)
     uint32_t* spec;            // [n_sec * speccap] speculative starts, relative to section start
     uint32_t* spec_cnt;        // [n_sec]
 };
@@ -100,6 +101,11 @@ __device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t b, uint32_t c) {
     return r;
 }
 __device__ __forceinline__ uint32_t min_u32(uint32_t a, uint32_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint32_t min3_u32(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 
 // 16 bytes at p[pos .. pos+16) of a file of length flen as four little-endian words (zeros past the
 // end): one raw buffer load (gfx950 buffer loads take any alignment) instead of 16 dependent byte
@@ -124,166 +130,180 @@ __device__ __forceinline__ uint32_t byte_of(const uint4& v, int j) {
 }
 
 // ---------------------------------------------------------------- F1: candidates
-// Lane l of the wave owns bytes [16l, 16l+16) of a 1 KiB sub-block. Its first byte's hash needs the
-// state at the byte before it: H = hl(l-1) + hl(l-2) << 16 + hl(l-3) << 32 (mod the 48 live bits),
-// with hl(m) the hash lane m's 16 bytes alone produce from 0. Lanes 0..2 take lanes 61..63 of the
-// previous sub-block. Candidates are rare (~2^-bits), so the fast path only tests the bits the two
-// masks share and a rare path recomputes both flags for the sub-block.
+// Lane-major scan. A section of S bytes is split into 64 list units of U = S/64 bytes; lane l owns
+// unit l and rolls ONE hash through it, starting from the 48 bytes before the unit (warm-up; only
+// the last 48 bytes reach the masked bits, so the rolled hash is the full-window hash from the unit's
+// first byte on). Per byte: one v_perm_b32 (the LDS address: byte << 8 | copy offset), one
+// ds_read_b64, one v_lshl_add_u64, one AND and a share of a v_min3 -- against ~6.4 VALU per byte for
+// the wave-cooperative form this replaces, which rolled every byte twice (the lane-local hash, then
+// again from the carry of the three lanes before it).
 //
-// The gear lookups are random 8-byte LDS gathers: with one shared table, the 32 lanes of a
-// ds_read_b64 group collide on bank pairs (~3.2 cycles per group instead of 1). With COPIES = 32 the
-// table is stored 32 times, copy c entirely in bank pair c (entry k of copy c at u64 index 32k + c,
-// 64 KiB), and lane l reads copy l % 32: no two lanes of a group ever share a bank, so every gather
-// costs the conflict-free 2 cycles. WAVES waves per workgroup share one table.
+// The bytes reach the lanes through LDS without a VGPR round trip: a round is 128 B of every unit;
+// 8 `buffer_load_dwordx4 ... lds` per round (lanes 8m..8m+7 of DMA k fetch the whole 128-B line of
+// unit 8k+m, so every line is fetched once, coalesced) land unit r's bytes at slot + 128 r, and lane
+// r reads them back with 8 ds_read_b128. The DMA lanes fetch their pieces rotated (piece q of unit r
+// at position (q + (r >> 1)) & 7 of its line) so that the 16 lanes of every ds_read_b128 group cover
+// the 64 banks exactly once. The gear table is stored 32 times (entry k of copy c at byte 256 k + 8 c,
+// lane l reads copy l % 32): the 32 lanes of a ds_read_b64 group never share a bank.
+// LDS: 64 KiB table + one 8 KiB slot per wave (the round being rolled sits in VGPRs while the next
+// round's DMA is in flight). tools/cdc_segment_probe.hip has the variants this was chosen from.
 //
-// SH: run the whole hash 16 bits to the left (table entries GEAR << 16, masks << 16). Only bits
-// below 48 matter, so nothing is lost, and when the bits both masks share are all >= 16 they land
-// in the high 32-bit word: the per-byte fast test is then one AND on one register.
-template <int D, int COPIES, int WAVES, bool SH>
-__global__ __launch_bounds__(64 * WAVES) void cdc_scan_kernel(CdcFiles f, CdcParams prm, uint64_t n_sec) {
-    __shared__ uint64_t lds_tab[256 * COPIES];
-    for (int i = threadIdx.x; i < 256 * COPIES; i += blockDim.x) lds_tab[i] = kGear[i / COPIES] << (SH ? 16 : 0);
+// Candidates: a lane records a 16-byte group of its unit when one of its positions has none of the
+// bits both masks share (offset in the unit, the hash before the group, its 16 bytes); the walk
+// resolves exact mask_s / mask_l flags from those. Lists are per unit, in position order.
+//
+// SH: the whole hash runs 16 bits to the left (table entries GEAR << 16, masks << 16; only bits below
+// 48 matter). When the bits both masks share are all >= 16 they then sit in the high 32-bit word and
+// the per-byte test is one AND; otherwise (avg < ~2 KiB) the low word is tested too (v_and_or).
+constexpr int kScanWaves = 8;
+
+template <bool SH>
+__global__ __launch_bounds__(64 * kScanWaves) void cdc_scan_kernel(CdcFiles f, CdcParams prm, uint64_t n_sec) {
+    // one LDS block: the table at address 0 (a gather address is then a single v_perm), slots after it
+    __shared__ __attribute__((aligned(16))) uint64_t lds[256 * 32 + kScanWaves * 1024];
+    for (int i = threadIdx.x; i < 256 * 32; i += blockDim.x) lds[i] = kGear[i >> 5] << (SH ? 16 : 0);
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const uint64_t* lds_gear = lds_tab + (COPIES == 1 ? 0 : (lane & (COPIES - 1)));  // index b * COPIES
-    const uint64_t sec = (uint64_t)blockIdx.x * WAVES + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint4* const slot = (uint4*)(lds + 256 * 32) + w * 512;
+    const uint64_t sec = (uint64_t)blockIdx.x * kScanWaves + (uint64_t)w;
     if (sec >= n_sec) return;
     const uint32_t file = f.sec_file[sec];
     const uint64_t flen = f.flen[file];
     const uint64_t sec_start = (sec - f.sec_base[file]) * prm.sec;
-    const uint64_t sec_len = flen - sec_start < prm.sec ? flen - sec_start : prm.sec;
+    const uint32_t sec_len = (uint32_t)(flen - sec_start < prm.sec ? flen - sec_start : prm.sec);
     const uint8_t* __restrict__ base = f.arena + f.foff[file] + sec_start;
+    const uint32_t unit = (uint32_t)prm.unit, rounds = unit / 128;
+    const uint32_t us = (uint32_t)lane * unit;  // this lane's unit, section-relative
+    // the resource covers the 48 bytes before the section (none at a file start) and every whole
+    // 16-byte piece of the section: loads past it return zeros without touching memory
+    const uint32_t pre = sec_start > 0 ? 48u : 0u, full16 = sec_len & ~15u;
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(base - pre), (short)0, (int)(pre + full16), 0x00020000);
     const uint64_t mask_s = prm.mask_s << (SH ? 16 : 0), mask_l = prm.mask_l << (SH ? 16 : 0);
     const uint64_t common = mask_s & mask_l;
     const uint32_t ch = (uint32_t)(common >> 32), cl = (uint32_t)common;  // SH: cl == 0 (host checks)
-    uint32_t* __restrict__ out = f.cand + sec * prm.cap;
-    uint64_t* __restrict__ out_h = f.cand_h + sec * prm.cap;
-    uint4* __restrict__ out_b = f.cand_b + sec * prm.cap;
-    uint32_t count = 0;  // wave-uniform
-
-    // carries: hl of the 3 lanes before lane 0 (bytes [-48, 0) of the section); zero at file start
-    // (positions < 47 of a file are never tested: every tested position is >= min + 47 >= 111)
-    uint64_t c1 = 0, c2 = 0, c3 = 0;  // hl of lanes 63, 62, 61 of the previous sub-block
-    if (sec_start > 0) {
-        // lanes 0..2 load the 48 bytes before the section: lane j holds bytes [-48 + 16j, -32 + 16j)
-        uint64_t hl = 0;
-        if (lane < 3) {
-            uint4 d;
-            __builtin_memcpy(&d, base - 48 + 16 * lane, 16);
-            const uint32_t w[4] = {d.x, d.y, d.z, d.w};
-#pragma unroll
-            for (int j = 0; j < 16; ++j) hl = (hl << 1) + lds_gear[((w[j >> 2] >> (8 * (j & 3))) & 0xFF) * COPIES];
-        }
-        const uint64_t h0 = ((uint64_t)__builtin_amdgcn_readlane((int)(hl >> 32), 0) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)hl, 0);
-        const uint64_t h1 = ((uint64_t)__builtin_amdgcn_readlane((int)(hl >> 32), 1) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)hl, 1);
-        const uint64_t h2 = ((uint64_t)__builtin_amdgcn_readlane((int)(hl >> 32), 2) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)hl, 2);
-        c1 = h2;
-        c2 = h1;
-        c3 = h0;
-    }
-
-    const uint64_t nsub = (sec_len + 1023) >> 10;
-    // raw buffer over the section: loads past its end return zeros without touching memory, so the
-    // prefetch ring below never branches around a load (the same idiom as K1)
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)sec_len, 0x00020000);
-    auto load_sub = [&](uint64_t sb) -> uint4 {
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        const uint64_t off = sb * 1024 + 16 * (uint64_t)lane;
-        const uint32_t vo = off + 16 <= sec_len ? (uint32_t)off : 0xFFFFF000u;
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo, 0, 2 /* nt */);
-        return make_uint4(v.x, v.y, v.z, v.w);
+    const uint32_t copy_off = (uint32_t)(lane & 31) * 8;
+    const char* const tab = (const char*)lds;
+    auto gear = [&](uint32_t word, int j) -> uint64_t {
+        const uint32_t a = __builtin_amdgcn_perm(word, copy_off, 0x0c0c0000u | ((4u + (uint32_t)j) << 8));
+        return *(const uint64_t*)(tab + a);
     };
-    // FULL: all 1024 bytes of the sub-block lie in the section (every sub-block but the last)
-    auto process = [&](const uint4 d, uint64_t sb, auto full_tag) {
-        constexpr bool FULL = decltype(full_tag)::value;
-        const uint64_t off = sb * 1024 + 16 * (uint64_t)lane;
-        uint64_t live = 16;
-        uint32_t w[4] = {d.x, d.y, d.z, d.w};
-        if constexpr (!FULL) {
-            live = off < sec_len ? (sec_len - off < 16 ? sec_len - off : 16) : 0;
-            if (live > 0 && live < 16) {  // the section's last partial 16 B: byte loads, constant indices
-                w[0] = w[1] = w[2] = w[3] = 0;
+    const uint64_t ubase = sec * 64 + (uint64_t)lane;  // global unit index
+    uint32_t* __restrict__ out = f.cand + ubase * prm.cap;
+    uint64_t* __restrict__ out_h = f.cand_h + ubase * prm.cap;
+    uint4* __restrict__ out_b = f.cand_b + ubase * prm.cap;
+    uint32_t count = 0;  // per lane
+
+    // warm-up over the 48 bytes before the unit (lane 0 at a file start: none, the hash starts at 0)
+    uint64_t h = 0;
+    {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        uint32_t wv[12];
 #pragma unroll
-                for (int j = 0; j < 16; ++j)
-                    if ((uint64_t)j < live) w[j >> 2] |= (uint32_t)base[off + j] << (8 * (j & 3));
-            }
+        for (int k = 0; k < 3; ++k) {
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, pre + us - 48 + 16 * k, 0, 0);
+            wv[4 * k] = v.x, wv[4 * k + 1] = v.y, wv[4 * k + 2] = v.z, wv[4 * k + 3] = v.w;
         }
-        uint64_t g[16];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) g[j] = lds_gear[((w[j >> 2] >> (8 * (j & 3))) & 0xFF) * COPIES];
-        uint64_t hl = 0;
+        for (int i = 0; i < 12; ++i)
 #pragma unroll
-        for (int j = 0; j < 16; ++j) hl = (hl << 1) + g[j];
-        // previous three lanes' hl: DPP wave shifts by one lane; lanes shifted in from "before lane
-        // 0" take the carries (lanes 63, 62, 61 of the previous sub-block) as the DPP `old` value
-        const uint32_t hi = (uint32_t)(hl >> 32), lo = (uint32_t)hl;
-        const uint32_t p1h = wave_shr1(hi, (uint32_t)(c1 >> 32)), p1l = wave_shr1(lo, (uint32_t)c1);
-        const uint32_t p2h = wave_shr1(p1h, (uint32_t)(c2 >> 32)), p2l = wave_shr1(p1l, (uint32_t)c2);
-        const uint32_t p3h = wave_shr1(p2h, (uint32_t)(c3 >> 32)), p3l = wave_shr1(p2l, (uint32_t)c3);
-        const uint64_t p1 = ((uint64_t)p1h << 32) | p1l, p2 = ((uint64_t)p2h << 32) | p2l;
-        const uint64_t p3 = ((uint64_t)p3h << 32) | p3l;
-        const uint64_t H = p1 + (p2 << 16) + (p3 << 32);
-        uint64_t h = H;
+            for (int b = 0; b < 4; ++b) h = (h << 1) + gear(wv[i], b);
+        if (pre + us < 48) h = 0;
+    }
+    // round t of every unit into this wave's slot (DMA k, lane 8m + j: unit 8k + m, rotated piece)
+    const int dm = lane >> 3, dj = lane & 7;
+    auto dma_round = [&](uint32_t t) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t r = 8 * k + dm;
+            const uint32_t piece = (uint32_t)(dj - (int)((r >> 1) & 7)) & 7;
+            // the whole offset in the VGPR operand, so the range check sees it
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(slot + 64 * k), 16,
+                                                     pre + r * unit + t * 128 + 16 * piece, 0, 0, 0);
+        }
+    };
+    dma_round(0);
+    const int rot = (lane >> 1) & 7;
+#pragma unroll 1
+    for (uint32_t t = 0; t < rounds; ++t) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this round's DMA has landed
+        uint32_t wv[32];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint4 v = slot[lane * 8 + ((q + rot) & 7)];
+            wv[4 * q] = v.x, wv[4 * q + 1] = v.y, wv[4 * q + 2] = v.z, wv[4 * q + 3] = v.w;
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot is free for the next DMA
+        if (t + 1 < rounds) dma_round(t + 1);
+        const uint32_t rb = us + t * 128;  // section-relative start of this lane's 128 B
+        // the section's partial last 16 B (outside the resource): byte loads, in the one lane that has it
+        if (sec_len != full16 && rb <= full16 && full16 < rb + 128) {
+            const int pi = (int)((full16 - rb) >> 4);
+            uint32_t pw[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (uint32_t q = 0; q < 16; ++q)
+                if (full16 + q < sec_len) pw[q >> 2] |= (uint32_t)base[full16 + q] << (8 * (q & 3));
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (q == pi) wv[4 * q] = pw[0], wv[4 * q + 1] = pw[1], wv[4 * q + 2] = pw[2], wv[4 * q + 3] = pw[3];
+        }
+        // roll the 128 bytes; the gathers of word i + P are issued before word i is rolled
+        constexpr int P = 3;
+        uint64_t G[P + 1][4];
+#pragma unroll
+        for (int i = 0; i < P; ++i)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) G[i][b] = gear(wv[i], b);
+        uint64_t hb = h;  // the hash before the current group
         uint32_t anyz = 0xFFFFFFFFu;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            h = (h << 1) + g[j];
-            if constexpr (SH) anyz = min_u32(anyz, (uint32_t)(h >> 32) & ch);
-            else anyz = min_u32(anyz, and_or((uint32_t)h, cl, (uint32_t)(h >> 32) & ch));
-        }
-        // bytes past the section end are not positions of this section
-        const bool maybe = (anyz == 0) && (FULL || live > 0);
-        // a lane whose 16 bytes may hold a candidate records its group (offset + the hash before it);
-        // the walk resolves the exact mask_s / mask_l flags of the group when it needs them
-        const uint64_t bal = __builtin_amdgcn_ballot_w64(maybe);
-        if (bal != 0) {
-            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-            const uint32_t idx = count + below;
-            if (maybe && idx < prm.cap) {
-                out[idx] = (uint32_t)off;
-                out_h[idx] = SH ? (H >> 16) : H;
-                out_b[idx] = make_uint4(w[0], w[1], w[2], w[3]);
+        for (int i = 0; i < 32; ++i) {
+            if (i + P < 32) {
+#pragma unroll
+                for (int b = 0; b < 4; ++b) G[(i + P) % (P + 1)][b] = gear(wv[i + P], b);
             }
-            count += (uint32_t)__builtin_popcountll(bal);
-        }
-        // carries for the next sub-block: hl of lanes 63, 62, 61
-        c1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 63) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
-        c2 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 62) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)lo, 62);
-        c3 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 61) << 32) | (uint32_t)__builtin_amdgcn_readlane((int)lo, 61);
-    };
-    // software pipeline: D sub-blocks (D KiB per wave) in flight while one is folded
-    uint4 ring[D];
+            __builtin_amdgcn_sched_barrier(0);
+            uint32_t tt[4];
 #pragma unroll
-    for (int d = 0; d < D; ++d) ring[d] = load_sub((uint64_t)d);
-    const uint64_t nfull = sec_len >> 10;
-    uint64_t sb = 0;
-    for (; sb + D <= nfull; sb += D) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            process(ring[d], sb + d, std::true_type{});
-            ring[d] = load_sub(sb + d + D);
+            for (int b = 0; b < 4; ++b) {
+                h = (h << 1) + G[i % (P + 1)][b];
+                if constexpr (SH) tt[b] = (uint32_t)(h >> 32) & ch;
+                else tt[b] = ((uint32_t)h & cl) | ((uint32_t)(h >> 32) & ch);
+            }
+            anyz = min3_u32(min3_u32(anyz, tt[0], tt[1]), tt[2], tt[3]);  // two v_min3 per 4 bytes
+            if ((i & 3) == 3) {
+                const uint32_t g = rb + 16 * (uint32_t)(i >> 2);  // the group, section-relative
+                if (anyz == 0 && g < sec_len) {
+                    if (count < prm.cap) {
+                        out[count] = g - us;
+                        out_h[count] = SH ? (hb >> 16) : hb;
+                        out_b[count] = make_uint4(wv[i - 3], wv[i - 2], wv[i - 1], wv[i]);
+                    }
+                    ++count;
+                }
+                anyz = 0xFFFFFFFFu;
+                hb = h;
+            }
             __builtin_amdgcn_sched_barrier(0);
         }
     }
-    // the last < D sub-blocks (the final one may be partial) are already in the ring
-#pragma unroll
-    for (int d = 0; d < D; ++d)
-        if (sb + d < nsub) process(ring[d], sb + d, std::false_type{});
-    if (lane == 0) f.cand_cnt[sec] = count;
+    f.cand_cnt[ubase] = count;
 }
 
 // ---------------------------------------------------------------- the walk (F2, F3)
-// Cursor over the candidate lists of one file, monotone in position.
+// Cursor over the candidate lists of one file, monotone in position. Lists are per unit (sec / 64
+// bytes, one F1 lane); unit u of global section s has global index 64 s + u.
 struct CandCursor {
-    uint64_t sec;   // global section index of the cursor
-    uint32_t idx;   // group index within that section's list
-    uint32_t rsec_idx = 0xFFFFFFFFu;  // the last resolved group (sec low bits + idx) and its flags
+    uint64_t sec;   // global unit index of the cursor
+    uint32_t idx;   // group index within that unit's list
+    uint32_t rsec_idx = 0xFFFFFFFFu;  // the last resolved group (unit + idx) and its flags
     uint64_t rsec = ~0ull;
     uint32_t rfs = 0, rfl = 0;
 };
 
 // Full-window hash test of positions [lo, hi) (all inside one file, lo >= 47) by direct byte scan:
-// used where a section's candidate list overflowed. Returns the first position with
+// used where a unit's candidate list overflowed. Returns the first position with
 // (hash & mask) == 0, or hi.
 __device__ uint64_t scan_bytes(const uint8_t* __restrict__ fbase, uint64_t lo, uint64_t hi, uint64_t mask,
                                const uint64_t* __restrict__ gear) {
@@ -328,14 +348,16 @@ __device__ uint64_t first_cand(const CdcFiles& f, const CdcParams& prm, uint64_t
                                const uint8_t* fbase, uint64_t flen, CandCursor& cur, uint64_t lo, uint64_t hi,
                                uint32_t flag, const uint64_t* gear) {
     if (lo >= hi) return hi;
-    uint64_t s = lo / prm.sec;
-    if (cur.sec < sec0 + s) {
-        cur.sec = sec0 + s;
+    // units: the file's sections [sec0, sec0 + nsec_file) hold units [64 sec0, 64 (sec0 + nsec_file))
+    const uint64_t u0 = 64 * sec0, nu = 64 * nsec_file;
+    const uint64_t s = lo / prm.unit;
+    if (cur.sec < u0 + s) {
+        cur.sec = u0 + s;
         cur.idx = 0;
     }
-    if (cur.sec >= sec0 + nsec_file) return hi;
+    if (cur.sec >= u0 + nu) return hi;
     while (true) {
-        const uint64_t sec_start = (cur.sec - sec0) * prm.sec;
+        const uint64_t sec_start = (cur.sec - u0) * prm.unit;  // the unit's start, file-relative
         if (sec_start >= hi) return hi;
         const uint32_t* list = f.cand + cur.sec * prm.cap;
         const uint64_t* hs = f.cand_h + cur.sec * prm.cap;
@@ -361,7 +383,7 @@ __device__ uint64_t first_cand(const CdcFiles& f, const CdcParams& prm, uint64_t
             // follows an S query from eS on), so the group is never needed again
             ++cur.idx;
         }
-        const uint64_t sec_end = sec_start + prm.sec;
+        const uint64_t sec_end = sec_start + prm.unit;
         if (cnt > prm.cap) {
             // overflowed list: positions after the last stored group were not recorded
             const uint64_t after = stored ? sec_start + list[stored - 1] + 16 : sec_start;
@@ -374,7 +396,7 @@ __device__ uint64_t first_cand(const CdcFiles& f, const CdcParams& prm, uint64_t
         }
         // move to the next section only if the query reaches into it: a later query (the L range
         // after an S range) may still need this section
-        if (sec_end >= hi || cur.sec + 1 >= sec0 + nsec_file) return hi;
+        if (sec_end >= hi || cur.sec + 1 >= u0 + nu) return hi;
         ++cur.sec;
         cur.idx = 0;
     }
@@ -435,7 +457,7 @@ __global__ __launch_bounds__(256) void cdc_walk_kernel(CdcFiles f, CdcParams prm
     // warm up over the `warmup` bytes before the section (unrecorded): a walk started anywhere meets
     // the true walk within a few chunks, so the recorded starts are almost always the true ones
     uint64_t s = sec_start > prm.warmup ? sec_start - prm.warmup : 0;
-    CandCursor cur{sec0 + s / prm.sec, 0};
+    CandCursor cur{64 * sec0 + s / prm.unit, 0};
     while (s < sec_start) s += cdc_cut(f, prm, sec0, nsec_file, fbase, flen, s, cur, lds_gear);
     uint32_t n = 0;
     while (true) {
@@ -537,7 +559,7 @@ __global__ __launch_bounds__(64) void cdc_fixup_kernel(CdcFiles f, CdcParams prm
         uint64_t next = i;
         if (lane == 0) {
             uint64_t pos = s.exit[sec0 + i - 1];
-            CandCursor cur{sec0 + i, 0};
+            CandCursor cur{64 * (sec0 + i), 0};
             for (uint64_t t = i; t < nsec_file; ++t) {
                 const uint64_t sec = sec0 + t;
                 const uint64_t sec_start = t * prm.sec;
@@ -559,7 +581,7 @@ __global__ __launch_bounds__(64) void cdc_fixup_kernel(CdcFiles f, CdcParams prm
                         }
                     }
                     fix[n++] = (uint32_t)(pos - sec_start);
-                    if (cur.sec < sec) cur = CandCursor{sec, 0};
+                    if (cur.sec < 64 * sec) cur = CandCursor{64 * sec, 0};
                     pos += cdc_cut(f, prm, sec0, nsec_file, fbase, flen, pos, cur, lds_gear);
                 }
                 s.status[sec] = kFixed;
@@ -732,8 +754,9 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     int rc = oxh_fastcdc_masks(avg_size, level, &prm.mask_s, &prm.mask_l);
     if (rc) return rc;
     // F1 records a 16-byte group wherever the bits both masks share are clear at one of its bytes:
-    // ~16 * 2^-popcount(common) groups per 16 bytes. Store 8x the expected count (+64) per section,
-    // at most one per group; a denser section keeps a truncated list and the walk scans its bytes.
+    // ~16 * 2^-popcount(common) groups per 16 bytes. Store 8x the expected count (+8) per list unit
+    // (sec / 64 bytes), at most one per group; a denser unit keeps a truncated list and the walk
+    // scans its bytes (C5 at 8 KiB: 2 expected per 8 KiB unit, 24 stored: P(overflow) ~ 1e-16).
     const double dens = std::min(1.0, 16.0 * std::ldexp(1.0, -__builtin_popcountll(prm.mask_s & prm.mask_l))) / 16.0;
     prm.sec = oxh::kSecDefault;
     if (const char* e = getenv("OXH_CDC_SECTION_BYTES")) {  // tests: many small sections per file
@@ -751,8 +774,11 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     prm.warmup = std::max<uint64_t>(4 * (uint64_t)max_size, 128 * 1024);
     if (prm.sec < max_rounded) prm.sec = max_rounded;
     if (!getenv("OXH_CDC_SECTION_BYTES") && prm.sec < 8 * max_rounded) prm.sec = 8 * max_rounded;
+    prm.sec = (prm.sec + 8191) / 8192 * 8192;  // 64 F1 units of whole 128-byte rounds
+    prm.unit = prm.sec / 64;
     if (const char* e = getenv("OXH_CDC_WARMUP_BYTES")) prm.warmup = strtoull(e, nullptr, 10);  // tests
-    prm.cap = (uint32_t)std::min<double>(prm.sec / 16, 8.0 * dens * prm.sec + 64);
+    prm.cap = (uint32_t)std::min<double>(prm.unit / 16, 8.0 * dens * prm.unit + 8);
+    if (const char* e = getenv("OXH_CDC_UNIT_CAP")) prm.cap = std::max(1, atoi(e));  // tests: force overflow
     prm.speccap = (uint32_t)(prm.sec / min_size + 2 + (max_size + min_size - 1) / min_size);
 
     std::vector<uint64_t> sec_base(n + 1);
@@ -774,10 +800,10 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     sc.want(&d_sec_base, n + 1);
     sc.want(&d_first, n + 1);
     sc.want(&d_sec_file, n_sec);
-    sc.want(&d_cand, n_sec * prm.cap);
-    sc.want(&d_cand_h, n_sec * prm.cap);
-    sc.want(&d_cand_b, n_sec * prm.cap);
-    sc.want(&d_cand_cnt, n_sec);
+    sc.want(&d_cand, n_sec * 64 * prm.cap);
+    sc.want(&d_cand_h, n_sec * 64 * prm.cap);
+    sc.want(&d_cand_b, n_sec * 64 * prm.cap);
+    sc.want(&d_cand_cnt, n_sec * 64);
     sc.want(&d_spec, n_sec * prm.speccap);
     sc.want(&d_spec_cnt, n_sec);
     sc.want(&d_status, n_sec);
@@ -801,21 +827,11 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     oxh::CdcFiles f{(const uint8_t*)d_arena, d_foff, d_flen, d_sec_base, d_sec_file, d_cand, d_cand_h, d_cand_b, d_cand_cnt, d_spec, d_spec_cnt};
     oxh::CdcStitch sti{d_status, d_k0, d_count, d_exit, d_fix, d_out_base};
     if (n_sec) {
-        // F1 shape (diagnostic override OXH_CDC_SCAN): 0 = one shared table, 4 waves/WG, 8 KiB in
-        // flight per wave (default); 1 = 32 bank-private table copies, 8 waves/WG; 2 = unshifted
-        // hash domain. Measured: no LDS bank conflicts (1), ring depth 2-8, 5-8 waves
-        // per SIMD and two interleaved sub-blocks per wave all land within +-4 %: F1 is bound by
-        // VALU issue (~103 instructions per KiB, a third of them 64-bit shift-adds).
-        static const int scan_shape = getenv("OXH_CDC_SCAN") ? atoi(getenv("OXH_CDC_SCAN")) : 0;
+        // F1: one wave per section (kScanWaves per workgroup, 128 KiB of LDS); SH when the bits both
+        // masks share are all >= 16
         const bool sh = (((prm.mask_s & prm.mask_l) << 16) & 0xFFFFFFFFull) == 0;
-        auto scan = sh ? oxh::cdc_scan_kernel<8, 1, 4, true> : oxh::cdc_scan_kernel<8, 1, 4, false>;
-        int waves = 4;
-        if (scan_shape == 1) {
-            scan = sh ? oxh::cdc_scan_kernel<8, 32, 8, true> : oxh::cdc_scan_kernel<8, 32, 8, false>;
-            waves = 8;
-        } else if (scan_shape == 2) {
-            scan = oxh::cdc_scan_kernel<8, 1, 4, false>;  // unshifted, for A/B
-        }
+        auto scan = sh ? oxh::cdc_scan_kernel<true> : oxh::cdc_scan_kernel<false>;
+        constexpr int waves = oxh::kScanWaves;
         hipLaunchKernelGGL(scan, dim3((unsigned)((n_sec + waves - 1) / waves)), dim3(64 * waves), 0, st, f, prm, n_sec);
         CDC_HIP(hipGetLastError());
         hipLaunchKernelGGL(oxh::cdc_walk_kernel, dim3((unsigned)((n_sec + 255) / 256)), dim3(256), 0, st, f, prm, n_sec);

@@ -209,9 +209,9 @@ def test_fastcdchunker_pack(cuda, oracle_lib, tmp_path):
 @pytest.mark.parametrize("section", [1024, 4096, 65536])
 @pytest.mark.parametrize("cfg", [CONFIGS[0], CONFIGS[2], CONFIGS[3], CONFIGS[4]], ids=lambda c: "-".join(map(str, c)))
 def test_fastcdc_small_sections(cuda, oracle_lib, monkeypatch, section, cfg, warmup):
-    """Many sections per file (OXH_CDC_SECTION_BYTES, raised to `max` where smaller): speculative walks
-    start mid-chunk everywhere, candidate lists overflow at 1 KiB sections (the byte-scan fallback),
-    and the stitch re-walks wherever a speculative walk has not converged (constant data never does)."""
+    """Many sections per file (OXH_CDC_SECTION_BYTES, raised to `max` where smaller and rounded up to
+    8 KiB: 64 F1 units of whole 128-byte rounds): speculative walks start mid-chunk everywhere, and the
+    stitch re-walks wherever a speculative walk has not converged (constant data never does)."""
     monkeypatch.setenv("OXH_CDC_SECTION_BYTES", str(section))
     if warmup is not None:  # no warm-up: most sections fail the check and are re-walked (F3b)
         monkeypatch.setenv("OXH_CDC_WARMUP_BYTES", warmup)
@@ -232,3 +232,20 @@ def test_fastcdc_many_default_sections(cuda, oracle_lib, avg):
     files = [rng.integers(0, 256, 12_345_679, dtype=np.uint8), text[:9_000_001].copy(),
              rng.integers(0, 256, 3 * (1 << 20) + 5, dtype=np.uint8)]
     assert _check(cuda, oracle_lib, files, 4096, avg, 2 * avg) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", ["1", "3"])
+def test_fastcdc_unit_list_overflow(cuda, oracle_lib, monkeypatch, cap):
+    """OXH_CDC_UNIT_CAP shrinks F1's per-unit candidate lists so that most units overflow: the walk
+    then scans the bytes after a unit's last stored group (the dense fallback). Same chunks as the
+    oracle, at default and at small sections."""
+    monkeypatch.setenv("OXH_CDC_UNIT_CAP", cap)
+    rng = np.random.default_rng(int(cap))
+    text = np.frombuffer(b"".join(b"id %d;%d\n" % (i, i % 5) for i in range(120_000)), dtype=np.uint8)
+    files = [rng.integers(0, 256, s, dtype=np.uint8) for s in (9, 70_001, 1_300_000)]
+    files += [text.copy(), rng.integers(0, 2, 300_000, dtype=np.uint8)]
+    _check(cuda, oracle_lib, files, 4096, 8192, 16384)
+    _check(cuda, oracle_lib, files, 64, 256, 1024)
+    monkeypatch.setenv("OXH_CDC_SECTION_BYTES", "16384")
+    _check(cuda, oracle_lib, files, 4096, 8192, 16384)
