@@ -273,14 +273,17 @@ __global__ __launch_bounds__(64 * kScanWaves) void cdc_scan_kernel(CdcFiles f, C
             }
             anyz = min3_u32(min3_u32(anyz, tt[0], tt[1]), tt[2], tt[3]);  // two v_min3 per 4 bytes
             if ((i & 3) == 3) {
-                const uint32_t g = rb + 16 * (uint32_t)(i >> 2);  // the group, section-relative
-                if (anyz == 0 && g < sec_len) {
-                    if (count < prm.cap) {
-                        out[count] = g - us;
-                        out_h[count] = SH ? (hb >> 16) : hb;
-                        out_b[count] = make_uint4(wv[i - 3], wv[i - 2], wv[i - 1], wv[i]);
+                // one VALU compare and a uniform branch when no lane of the wave has a candidate here
+                if (__builtin_amdgcn_ballot_w64(anyz == 0)) {
+                    const uint32_t g = rb + 16 * (uint32_t)(i >> 2);  // the group, section-relative
+                    if (anyz == 0 && g < sec_len) {
+                        if (count < prm.cap) {
+                            out[count] = g - us;
+                            out_h[count] = SH ? (hb >> 16) : hb;
+                            out_b[count] = make_uint4(wv[i - 3], wv[i - 2], wv[i - 1], wv[i]);
+                        }
+                        ++count;
                     }
-                    ++count;
                 }
                 anyz = 0xFFFFFFFFu;
                 hb = h;
