@@ -187,6 +187,7 @@ def main() -> None:
         table, last = step()
     drain()
     ev1.record()
+    t_enq = time.perf_counter() - t0
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     if world > 1:
@@ -204,6 +205,8 @@ def main() -> None:
     kernel_s = kev[0].elapsed_time(kev[1]) / 1e3 / kreps
 
     elapsed = max(wall, gpu_s)
+    log(f"[bench] rank {rank}: wall {wall * 1e3:.3f} ms, events {gpu_s * 1e3:.3f} ms, enqueue {t_enq * 1e3:.3f} ms, "
+        f"kernel {kernel_s * 1e3:.4f} ms x {args.steps} = {kernel_s * args.steps * 1e3:.3f} ms")
     t = torch.tensor([elapsed, kernel_s], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -35,9 +35,13 @@ def needs_build() -> bool:
 
 HOST_SRC = os.path.join(HERE, "host", "oxen_hasher.cpp")
 HOST_HDR = os.path.join(HERE, "host", "oxen_hasher.hpp")
+COMMIT_SRC = os.path.join(HERE, "host", "commit_writer.cpp")
+COMMIT_HDR = os.path.join(HERE, "host", "commit_writer.hpp")
 HOST_LIB = os.path.join(HERE, "liboxen_hasher.so")
 NATIVE_TEST_SRC = os.path.join(ROOT, "tests", "native", "test_hasher.cpp")
 NATIVE_TEST = os.path.join(ROOT, "tests", "native", "test_hasher")
+COMMIT_CLI_SRC = os.path.join(ROOT, "tests", "native", "commit_tree_cli.cpp")
+COMMIT_CLI = os.path.join(ROOT, "tests", "native", "commit_tree_cli")
 
 
 def _stale(target: str, deps: list[str]) -> bool:
@@ -45,15 +49,19 @@ def _stale(target: str, deps: list[str]) -> bool:
 
 
 def build_host(force: bool = False, verbose: bool = False) -> str:
-    """The C++ mirror of liboxen `util::hasher` over the C ABI (oxen_amd/host, g++) and its native
-    test program (tests/native/test_hasher.cpp), both linked against liboxen_hash.so."""
+    """The C++ host mirror over the C ABI (oxen_amd/host, g++): liboxen `util::hasher` + MerkleHash
+    and the commit writer's K2 driver, in liboxen_hasher.so; its native test programs
+    (tests/native/test_hasher.cpp, commit_tree_cli.cpp). All link against liboxen_hash.so."""
     hdr = os.path.join(ROOT, "include", "oxen_hash.h")
     steps = [
-        (HOST_LIB, [HOST_SRC, HOST_HDR, hdr, LIB],
-         ["g++", "-std=c++17", "-O2", "-Wall", "-shared", "-fPIC", "-o", HOST_LIB + ".tmp", HOST_SRC,
+        (HOST_LIB, [HOST_SRC, HOST_HDR, COMMIT_SRC, COMMIT_HDR, hdr, LIB],
+         ["g++", "-std=c++17", "-O2", "-Wall", "-shared", "-fPIC", "-o", HOST_LIB + ".tmp", HOST_SRC, COMMIT_SRC,
           f"-L{HERE}", "-l:liboxen_hash.so", "-Wl,-rpath,$ORIGIN"]),
         (NATIVE_TEST, [NATIVE_TEST_SRC, HOST_HDR, HOST_LIB],
          ["g++", "-std=c++17", "-O2", "-Wall", "-o", NATIVE_TEST + ".tmp", NATIVE_TEST_SRC,
+          f"-L{HERE}", "-l:liboxen_hasher.so", "-l:liboxen_hash.so", "-Wl,-rpath,$ORIGIN/../../oxen_amd"]),
+        (COMMIT_CLI, [COMMIT_CLI_SRC, COMMIT_HDR, HOST_HDR, HOST_LIB],
+         ["g++", "-std=c++17", "-O2", "-Wall", "-o", COMMIT_CLI + ".tmp", COMMIT_CLI_SRC,
           f"-L{HERE}", "-l:liboxen_hasher.so", "-l:liboxen_hash.so", "-Wl,-rpath,$ORIGIN/../../oxen_amd"]),
     ]
     for target, deps, cmd in steps:

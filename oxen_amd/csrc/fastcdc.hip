@@ -84,6 +84,7 @@ struct CdcFiles {
     uint64_t* cand_h;          // [n_sec * 64 * cap] full-window hash before each group's first byte (mod 2^48)
     uint4* cand_b;             // [n_sec * 64 * cap] the group's 16 bytes (the walk resolves flags from these)
     uint32_t* cand_cnt;        // [n_sec * 64] true count per unit (> cap: list truncated, dense fallback)
+    uint64_t* cand_occ;        // [n_sec] bit u: unit u of the section has a non-empty list
     uint32_t* spec;            // [n_sec * speccap] speculative starts, relative to section start
     uint32_t* spec_cnt;        // [n_sec]
 };
@@ -292,6 +293,8 @@ __global__ __launch_bounds__(64 * kScanWaves) void cdc_scan_kernel(CdcFiles f, C
         }
     }
     f.cand_cnt[ubase] = count;
+    const uint64_t occ = __builtin_amdgcn_ballot_w64(count != 0);
+    if (lane == 0) f.cand_occ[sec] = occ;
 }
 
 // ---------------------------------------------------------------- the walk (F2, F3)
@@ -302,6 +305,7 @@ struct CandCursor {
     uint32_t idx;   // group index within that unit's list
     uint32_t rsec_idx = 0xFFFFFFFFu;  // the last resolved group (unit + idx) and its flags
     uint64_t rsec = ~0ull;
+    uint64_t occ_sec = ~0ull, occ = 0;  // the occupancy mask of section occ_sec (F1's ballot)
     uint32_t rfs = 0, rfl = 0;
 };
 
@@ -360,6 +364,24 @@ __device__ uint64_t first_cand(const CdcFiles& f, const CdcParams& prm, uint64_t
     }
     if (cur.sec >= u0 + nu) return hi;
     while (true) {
+        // skip the units F1 found no candidate in without loading their counts
+        const uint64_t gsec = cur.sec >> 6;
+        if (cur.occ_sec != gsec) {
+            cur.occ = f.cand_occ[gsec];
+            cur.occ_sec = gsec;
+        }
+        const uint64_t rest = cur.occ >> (cur.sec & 63);
+        if (rest == 0) {
+            const uint64_t next = (gsec + 1) * 64;  // the next section's first unit
+            if (next >= u0 + nu || (next - u0) * prm.unit >= hi) return hi;
+            cur.sec = next;
+            cur.idx = 0;
+            continue;
+        }
+        if (!(rest & 1)) {
+            cur.sec += (uint64_t)__builtin_ctzll(rest);
+            cur.idx = 0;
+        }
         const uint64_t sec_start = (cur.sec - u0) * prm.unit;  // the unit's start, file-relative
         if (sec_start >= hi) return hi;
         const uint32_t* list = f.cand + cur.sec * prm.cap;
@@ -796,7 +818,7 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     Scratch sc(st);
     uint64_t *d_foff, *d_flen, *d_sec_base, *d_first, *d_exit, *d_out_base;
     uint32_t *d_sec_file, *d_cand, *d_cand_cnt, *d_spec, *d_spec_cnt, *d_status, *d_k0, *d_count, *d_fix;
-    uint64_t* d_cand_h;
+    uint64_t *d_cand_h, *d_cand_occ;
     uint4* d_cand_b;
     sc.want(&d_foff, n);
     sc.want(&d_flen, n);
@@ -807,6 +829,7 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     sc.want(&d_cand_h, n_sec * 64 * prm.cap);
     sc.want(&d_cand_b, n_sec * 64 * prm.cap);
     sc.want(&d_cand_cnt, n_sec * 64);
+    sc.want(&d_cand_occ, n_sec);
     sc.want(&d_spec, n_sec * prm.speccap);
     sc.want(&d_spec_cnt, n_sec);
     sc.want(&d_status, n_sec);
@@ -827,7 +850,7 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     }
 
     const double t_alloc = since();
-    oxh::CdcFiles f{(const uint8_t*)d_arena, d_foff, d_flen, d_sec_base, d_sec_file, d_cand, d_cand_h, d_cand_b, d_cand_cnt, d_spec, d_spec_cnt};
+    oxh::CdcFiles f{(const uint8_t*)d_arena, d_foff, d_flen, d_sec_base, d_sec_file, d_cand, d_cand_h, d_cand_b, d_cand_cnt, d_cand_occ, d_spec, d_spec_cnt};
     oxh::CdcStitch sti{d_status, d_k0, d_count, d_exit, d_fix, d_out_base};
     if (n_sec) {
         // F1: one wave per section (kScanWaves per workgroup, 128 KiB of LDS); SH when the bits both

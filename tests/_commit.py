@@ -45,3 +45,36 @@ def to_staged(entries):
 
     return {k: [StagedNode(path=p, hash=h, is_dir=isd, status=st, name=nm) for (p, h, isd, st, nm) in v]
             for k, v in entries.items()}
+
+
+def to_cli_input(entries, existing, vnode_size=10_000) -> str:
+    """The staged commit as tests/native/commit_tree_cli reads it (entries in dict order)."""
+    lines = [f"vnode_size\t{vnode_size}"]
+
+    def nodes(v):
+        for (p, h, isd, st, nm) in v:
+            lines.append(f"node\t{p}\t{h:x}\t{int(isd)}\t{st}\t{nm if nm is not None else chr(1)}")
+
+    for d, v in entries.items():
+        lines.append(f"entries\t{d}")
+        nodes(v)
+    for d, v in (existing or {}).items():
+        lines.append(f"existing\t{d}")
+        nodes(v)
+    return "\n".join(lines) + "\n"
+
+
+def parse_cli_output(text: str):
+    """({dir: [(vnode_id, [entry paths])]}, {dir: hash}, {dir: [removed paths]}, best seconds)."""
+    vn, dh, removed, t = {}, {}, {}, None
+    for line in text.splitlines():
+        f = line.split("\t")
+        if f[0] == "vnode":
+            vn.setdefault(f[1], []).append((int(f[3], 16), f[5:5 + int(f[4])]))
+        elif f[0] == "removed":
+            removed.setdefault(f[1], []).append(f[2])
+        elif f[0] == "dir":
+            dh[f[1]] = int(f[2], 16)
+        elif f[0] == "time":
+            t = float(f[1])
+    return vn, dh, removed, t

@@ -1,8 +1,10 @@
 """K2 commit driver timing at config 3's tree shape (200 000 files in 1 000 dirs), GPU box only.
 
-Times merkle.commit_tree (three batched GPU passes) against the same host driver with its hash
-calls answered by the C oracle on the host threads, and the scalar restatement of commit_writer.rs
-(oracle/commit_oracle.py); checks every vnode id and dir hash equal. Prints one JSON line.
+Times the C++ K2 driver (oxen_amd/host/commit_writer.cpp via tests/native/commit_tree_cli, best of 5
+calls in one process) and merkle.commit_tree (the Python driver; both issue three batched GPU passes)
+against the Python driver with its hash calls answered by the C oracle on the host threads, and the
+scalar restatement of commit_writer.rs (oracle/commit_oracle.py); checks every vnode id and dir hash
+equal. Prints one JSON line.
 """
 import json
 import os
@@ -56,10 +58,20 @@ def main():
     t0 = time.perf_counter()
     rvn, rdh = commit_oracle.commit_tree(entries, {}, 10_000, _commit.salt)
     scalar_s = time.perf_counter() - t0
-    exact = ({d: h.value for d, h in dh.items()} == rdh == {d: h.value for d, h in cdh.items()}
-             and all([v.id.value for v in vn[d][0]] == [i for i, _ in rvn[d]] for d in rvn))
+    import subprocess
+
+    from oxen_amd import build
+
+    build.build_host()
+    r = subprocess.run([build.COMMIT_CLI, "--reps", "5"], input=_commit.to_cli_input(entries, {}, 10_000),
+                       capture_output=True, text=True, check=True)
+    nvn, ndh, _, native_s = _commit.parse_cli_output(r.stdout)
+    exact = ({d: h.value for d, h in dh.items()} == rdh == {d: h.value for d, h in cdh.items()} == ndh
+             and all([v.id.value for v in vn[d][0]] == [i for i, _ in rvn[d]] for d in rvn)
+             and all([i for i, _ in nvn[d]] == [i for i, _ in rvn[d]] for d in rvn))
     print(json.dumps({
         "config": "K2 commit at C3 shape: 200 000 files, 1 000 dirs, vnode_size 10 000",
+        "native_cpp_commit_tree_s": round(native_s, 4),
         "gpu_commit_tree_s": round(gpu_s, 3), **stages,
         "host_driver_with_cpu_hash_s": round(cpu_driver_s, 3), "cpu_threads": threads,
         "scalar_restatement_s": round(scalar_s, 3),
