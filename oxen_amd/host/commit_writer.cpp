@@ -5,6 +5,7 @@
 #include <cmath>
 #include <map>
 #include <random>
+#include <thread>
 
 #include "../../include/oxen_hash.h"
 
@@ -27,15 +28,30 @@ std::string join(const std::vector<std::string>& c, size_t n) {
     return r;
 }
 
-// Path's Ord on normalised paths (components joined by '/'): component-wise, i.e. bytewise with '/'
-// below every other byte (a component that ends first sorts first)
-bool path_less(const std::string& a, const std::string& b) {
-    const size_t n = std::min(a.size(), b.size());
-    for (size_t i = 0; i < n; ++i) {
-        const uint8_t x = a[i] == '/' ? 0 : (uint8_t)a[i], y = b[i] == '/' ? 0 : (uint8_t)b[i];
-        if (x != y) return x < y;
+// Path's Ord on a normalised path (components joined by '/') is component-wise: bytewise with '/'
+// below every other byte (a component that ends first sorts first). With '/' mapped to '\0' the plain
+// (memcmp) string order is that order; paths hold no NUL.
+std::string sort_key(const std::string& normalised) {
+    std::string k = normalised;
+    std::replace(k.begin(), k.end(), '/', '\0');
+    return k;
+}
+
+// fn(i) for i in [0, n), split over up to 16 threads in contiguous blocks (each dir is independent)
+template <class F>
+void parallel_for(size_t n, F&& fn) {
+    const size_t hw = std::max<size_t>(1, std::min<size_t>(16, std::thread::hardware_concurrency()));
+    const size_t nt = std::min(hw, n / 64 + 1);
+    if (nt <= 1) {
+        for (size_t i = 0; i < n; ++i) fn(i);
+        return;
     }
-    return a.size() < b.size();
+    std::vector<std::thread> pool;
+    for (size_t t = 0; t < nt; ++t)
+        pool.emplace_back([&, t] {
+            for (size_t i = n * t / nt; i < n * (t + 1) / nt; ++i) fn(i);
+        });
+    for (auto& th : pool) th.join();
 }
 
 }  // namespace
@@ -112,9 +128,9 @@ std::vector<DirVNodes> split_into_vnodes(const StagedDirs& entries, const Existi
                 nodes[it->second] = std::move(n);
                 return;
             }
-            at.emplace(key, nodes.size());
+            keys.push_back(sort_key(key));
+            at.emplace(std::move(key), nodes.size());
             nodes.push_back(std::move(n));
-            keys.push_back(std::move(key));
             alive.push_back(1);
         }
         void drop(const std::string& key) {
@@ -125,12 +141,18 @@ std::vector<DirVNodes> split_into_vnodes(const StagedDirs& entries, const Existi
         }
     };
     std::vector<Dir> dirs(entries.size());
-    for (size_t i = 0; i < entries.size(); ++i) {
+    parallel_for(entries.size(), [&](size_t i) {
         const std::string& directory = entries[i].first;
         const std::vector<std::string> dcomps = path_components(directory);
         const std::string dkey = join(dcomps, dcomps.size());
         Dir& d = dirs[i];
-        if (auto it = existing.find(directory); it != existing.end())
+        const auto ex = existing.find(directory);
+        const size_t expect = entries[i].second.size() + (ex != existing.end() ? ex->second.size() : 0);
+        d.nodes.reserve(expect);
+        d.keys.reserve(expect);
+        d.alive.reserve(expect);
+        d.at.reserve(expect);
+        if (auto it = ex; it != existing.end())
             for (const StagedNode& c : it->second) d.put(normalize(c.path), StagedNode(c));
         std::unordered_map<std::string, size_t> removed_at;  // a later removal of a path replaces it
         for (StagedNode c : entries[i].second) {
@@ -153,11 +175,20 @@ std::vector<DirVNodes> split_into_vnodes(const StagedDirs& entries, const Existi
         }
         for (size_t k = 0; k < d.nodes.size(); ++k)
             if (d.alive[k]) d.order.push_back(k);
-        std::sort(d.order.begin(), d.order.end(), [&](size_t x, size_t y) { return path_less(d.keys[x], d.keys[y]); });
-    }
+        std::sort(d.order.begin(), d.order.end(), [&](size_t x, size_t y) { return d.keys[x] < d.keys[y]; });
+    });
     // bucket = xxh3_128(path) % num_vnodes (:665-681): every child of every dir in one pass
     std::string arena;
     std::vector<uint64_t> offs, lens;
+    size_t n_children = 0, path_bytes = 0;
+    for (const Dir& d : dirs)
+        for (size_t k : d.order) {
+            ++n_children;
+            path_bytes += d.nodes[k].path.size();
+        }
+    arena.reserve(path_bytes);
+    offs.reserve(n_children);
+    lens.reserve(n_children);
     for (const Dir& d : dirs)
         for (size_t k : d.order) {
             offs.push_back(arena.size());
@@ -172,14 +203,19 @@ std::vector<DirVNodes> split_into_vnodes(const StagedDirs& entries, const Existi
         out[i].removed = std::move(dirs[i].removed);
         const uint64_t nv = num_vnodes(dirs[i].order.size(), vnode_size);
         out[i].vnodes.resize(nv);
+        std::vector<uint32_t> b(dirs[i].order.size());
+        std::vector<size_t> per(nv, 0);
+        for (size_t q = 0; q < b.size(); ++q) ++per[b[q] = (uint32_t)(buckets[k + q] % nv)];
+        for (uint64_t j = 0; j < nv; ++j) out[i].vnodes[j].entries.reserve(per[j]);
         // path order in, so every vnode's entries come out sorted (:684-694)
-        for (size_t slot : dirs[i].order)
-            out[i].vnodes[(size_t)(buckets[k++] % nv)].entries.push_back(std::move(dirs[i].nodes[slot]));
+        for (size_t q = 0; q < b.size(); ++q) out[i].vnodes[b[q]].entries.push_back(std::move(dirs[i].nodes[dirs[i].order[q]]));
+        k += b.size();
     }
     // vnode id = xxh3("vnode" || dir || child hashes LE [|| uuid]) (:683-720): every vnode in one pass
     arena.clear();
     offs.clear();
     lens.clear();
+    arena.reserve(n_children * 16 + out.size() * 64);
     for (const DirVNodes& d : out) {
         const bool dir_existed = existing.count(d.dir) != 0;
         for (size_t j = 0; j < d.vnodes.size(); ++j) {
@@ -211,9 +247,14 @@ std::vector<std::pair<std::string, MerkleHash>> compute_dir_hashes(const std::ve
                                                                    const std::vector<std::string>* dirs, oxh_ctx* ctx) {
     // what compute_dir_node feeds for each staged dir's vnodes (:1042-1071)
     std::vector<std::string> segs(vnodes.size());
-    std::unordered_map<std::string, std::vector<size_t>> under;  // ancestor path -> descendants, in order
-    for (size_t i = 0; i < vnodes.size(); ++i) {
+    parallel_for(vnodes.size(), [&](size_t i) {
         std::string& s = segs[i];
+        size_t bytes = 0;
+        for (const EntryVNode& v : vnodes[i].vnodes) {
+            bytes += 16;
+            for (const StagedNode& c : v.entries) bytes += c.node_name().size() + 16;
+        }
+        s.reserve(bytes);
         for (const EntryVNode& v : vnodes[i].vnodes) {
             put_le(s, v.id.to_u128());
             for (const StagedNode& c : v.entries) {
@@ -221,6 +262,9 @@ std::vector<std::pair<std::string, MerkleHash>> compute_dir_hashes(const std::ve
                 put_le(s, c.hash);
             }
         }
+    });
+    std::unordered_map<std::string, std::vector<size_t>> under;  // ancestor path -> descendants, in order
+    for (size_t i = 0; i < vnodes.size(); ++i) {
         const std::vector<std::string> comps = path_components(vnodes[i].dir);
         for (size_t d = 0; d <= comps.size(); ++d) under[join(comps, d)].push_back(i);
     }
@@ -231,15 +275,28 @@ std::vector<std::pair<std::string, MerkleHash>> compute_dir_hashes(const std::ve
             if (!path_components(v.dir).empty()) dflt.push_back(v.dir);
         dirs = &dflt;
     }
+    // each dir's descendants (looked up once), then one arena of the exact size
+    std::vector<const std::vector<size_t>*> desc(dirs->size(), nullptr);
+    size_t total = 0;
+    for (size_t q = 0; q < dirs->size(); ++q) {
+        const std::vector<std::string> comps = path_components((*dirs)[q]);
+        if (auto it = under.find(join(comps, comps.size())); it != under.end()) desc[q] = &it->second;
+        total += 3 + (*dirs)[q].size();
+        if (desc[q])
+            for (size_t i : *desc[q]) total += segs[i].size();
+    }
     std::string arena;
+    arena.reserve(total);
     std::vector<uint64_t> offs, lens;
-    for (const std::string& d : *dirs) {
+    offs.reserve(dirs->size());
+    lens.reserve(dirs->size());
+    for (size_t q = 0; q < dirs->size(); ++q) {
+        const std::string& d = (*dirs)[q];
         const size_t start = arena.size();
         arena += "dir";
         arena += d;
-        const std::vector<std::string> comps = path_components(d);
-        if (auto it = under.find(join(comps, comps.size())); it != under.end())
-            for (size_t i : it->second) arena += segs[i];
+        if (desc[q])
+            for (size_t i : *desc[q]) arena += segs[i];
         offs.push_back(start);
         lens.push_back(arena.size() - start);
     }
