@@ -157,6 +157,10 @@ __device__ __forceinline__ uint32_t byte_of(const uint4& v, int j) {
 // 48 matter). When the bits both masks share are all >= 16 they then sit in the high 32-bit word and
 // the per-byte test is one AND; otherwise (avg < ~2 KiB) the low word is tested too (v_and_or).
 constexpr int kScanWaves = 8;
+#ifndef OXH_SCAN_DMA_AUX
+#define OXH_SCAN_DMA_AUX 2
+#endif
+constexpr int kScanDmaAux = OXH_SCAN_DMA_AUX;  // cache policy of the scan's LDS-DMA loads (2 = nt)
 
 template <bool SH>
 __global__ __launch_bounds__(64 * kScanWaves) void cdc_scan_kernel(CdcFiles f, CdcParams prm, uint64_t n_sec) {
@@ -221,7 +225,7 @@ __global__ __launch_bounds__(64 * kScanWaves) void cdc_scan_kernel(CdcFiles f, C
             const uint32_t piece = (uint32_t)(dj - (int)((r >> 1) & 7)) & 7;
             // the whole offset in the VGPR operand, so the range check sees it
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(slot + 64 * k), 16,
-                                                     pre + r * unit + t * 128 + 16 * piece, 0, 0, 0);
+                                                     pre + r * unit + t * 128 + 16 * piece, 0, 0, kScanDmaAux);
         }
     };
     dma_round(0);
