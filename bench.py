@@ -87,7 +87,41 @@ def cpu_baseline(da, gpu_digests: np.ndarray, seed: int, budget_s: float = 10.0)
     return {"value": round(gib / dt, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": f"{nsample} of {da.n} items x {item_len} B ({nsample * item_len / 2**20:.0f} MiB), "
                       f"{passes} passes in {dt:.1f} s, oracle/xxh3_oracle.c scalar C, {threads} threads, {cpu_model}",
-            "digests_bit_exact_on_sample": exact}
+            "digests_bit_exact_on_sample": exact,
+            "oxen_add_c1": cpu_oxen_add_c1(threads)}
+
+
+def cpu_oxen_add_c1(threads: int, reps: int = 3) -> dict:
+    """The reference's own CPU-runnable case (BASELINE configs[0]: `oxen init; oxen add .` on the
+    1 000-file text repo of benchmark/generate_text_repo.py), timed in the same run: no `oxen` binary
+    exists here, so it is the add loop restated in C (oracle/: stat, read, XXH3-128, then
+    store_version_from_reader's re-read, verify hash, write, fsync of blob and parent, rename)."""
+    import shutil
+    import tempfile
+
+    from oracle import oracle
+    from oxen_amd.workloads import write_text_repo
+
+    d = tempfile.mkdtemp(prefix="oxh_c1_")
+    try:
+        paths = write_text_repo(d, 1000)
+        nbytes = sum(os.path.getsize(p) for p in paths)
+        root = os.path.join(d, ".oxen", "versions", "files")
+        best, ok = None, True
+        for _ in range(reps):
+            shutil.rmtree(os.path.join(d, ".oxen"), ignore_errors=True)
+            t0 = time.perf_counter()
+            out, _, status, stored = oracle.add_files(paths, root, threads)
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+            ok = ok and bool((status == 0).all()) and int(stored.sum()) == len(paths)
+        # the known answer of texts/file_0.txt ("File content 0", SURVEY §8c)
+        ok = ok and format((int(out[0][1]) << 64) | int(out[0][0]), "x") == "393ba5849f5590fc5985c4bbcec0003f"
+        return {"ms": round(best * 1e3, 2), "files": len(paths), "bytes": nbytes, "cores": threads, "kind": "port",
+                "what": "oxen add . restated (hash + verify-before-publish + durable blob write), best of %d" % reps,
+                "ok": ok}
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def load_traffic(workload: str):
