@@ -86,7 +86,7 @@ def cpu_baseline(da, gpu_digests: np.ndarray, seed: int, budget_s: float = 10.0)
         pass
     return {"value": round(gib / dt, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": f"{nsample} of {da.n} items x {item_len} B ({nsample * item_len / 2**20:.0f} MiB), "
-                      f"{passes} passes in {dt:.1f} s, oracle/xxh3_oracle.c scalar C, {threads} threads, {cpu_model}",
+                      f"{passes} passes in {dt:.1f} s, oracle/xxh3_oracle.c (SSE2 stripes, as xxhash-rust on x86-64), {threads} threads, {cpu_model}",
             "digests_bit_exact_on_sample": exact,
             "oxen_add_c1": cpu_oxen_add_c1(threads)}
 
