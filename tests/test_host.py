@@ -155,3 +155,13 @@ def test_utf8_oracles_agree():
     assert oracle.is_utf8_prefix(b"") and oracle.is_utf8_prefix(b"\xe2\x82")
     assert not oracle.is_utf8_prefix(b"\xe2\x28")
     assert oracle.is_utf8_prefix(b"a" * 4096 + b"\xff")  # only the first 4 KiB count
+
+
+def test_bench_reference_add_c1(oracle_lib):
+    """bench.py's same-run CPU timing of the reference's own case (configs[0]: `oxen add .` on the
+    1 001-file text repo, the add loop restated in oracle/): every blob stored, the known answer of
+    texts/file_0.txt matched."""
+    import bench
+
+    r = bench.cpu_oxen_add_c1(threads=2, reps=1)
+    assert r["ok"] and r["files"] == 1001 and r["ms"] > 0
