@@ -9,11 +9,12 @@
 //
 // The walk is serial per file (each cut decides where the next chunk's hash starts). The GPU
 // formulation splits it into three kernels:
-//   F1 cdc_scan_kernel    chip-wide, one wave per section (>= 512 KiB): the FULL-window gear
-//                         hash at every byte (all mask bits are below bit 48, so only the last 48
-//                         bytes matter and the hash of position p is a function of b[p-47 .. p]) and
-//                         a compact, position-ordered list of candidate positions per section
-//                         (flag bit 0: hash & mask_s == 0, bit 1: hash & mask_l == 0).
+//   F1 cdc_scan_kernel    chip-wide, one wave per section (>= 512 KiB), lane-major: lane l rolls
+//                         the gear hash through unit l (section / 64 bytes) from 48 bytes before it,
+//                         so it has the FULL-window hash at every byte (all mask bits are below bit
+//                         48: the hash of position p is a function of b[p-47 .. p]), and records a
+//                         position-ordered list of candidate 16-byte groups per unit (a position with
+//                         none of the bits both masks share clear).
 //   F2 cdc_walk_kernel    one lane per section: a speculative walk that starts 4 max-sized chunks
 //                         before the section (by then it has almost surely met the true walk) and
 //                         cuts chunks from the candidate lists until it passes the section end,
