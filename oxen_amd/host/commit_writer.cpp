@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <exception>
 #include <map>
 #include <random>
 #include <thread>
@@ -47,11 +48,18 @@ void parallel_for(size_t n, F&& fn) {
         return;
     }
     std::vector<std::thread> pool;
+    std::vector<std::exception_ptr> err(nt);
     for (size_t t = 0; t < nt; ++t)
         pool.emplace_back([&, t] {
-            for (size_t i = n * t / nt; i < n * (t + 1) / nt; ++i) fn(i);
+            try {
+                for (size_t i = n * t / nt; i < n * (t + 1) / nt; ++i) fn(i);
+            } catch (...) {
+                err[t] = std::current_exception();  // rethrown in the caller (e.g. std::bad_alloc)
+            }
         });
     for (auto& th : pool) th.join();
+    for (auto& e : err)
+        if (e) std::rethrow_exception(e);
 }
 
 }  // namespace
