@@ -75,3 +75,50 @@ def test_native_commit_driver_image_repo_shape(cuda, cli):
     """C3's tree: 200 000 files in 1 000 dirs."""
     entries, _ = _commit.staged_commit(n_files=200_000, n_dirs=1000)
     _check(_run(cli, entries, {}, 10_000), entries, {}, 10_000)
+
+
+def _odd_paths_commit():
+    """Paths the way a caller may hand them over: leading "./", doubled and trailing slashes, "."
+    components, a child staged under a dir whose name prefixes a sibling's ("img" vs "img2"), the same
+    path staged twice (the later one wins), and a removal that is re-added."""
+    rand = iter(range(1, 10_000))
+    h = lambda: (next(rand) * 0x9E3779B97F4A7C15) & ((1 << 128) - 1)
+    entries = {
+        "": [("README.md", h(), False, "added", "README.md"), ("./data", h(), True, "added", "data")],
+        "data": [("data/img/", h(), True, "added", "data/img"), ("data//img2", h(), True, "added", "data/img2"),
+                 ("data/./a.csv", h(), False, "added", "data/a.csv"), ("b.csv", h(), False, "added", "b.csv")],
+        "data/img": [("data/img/x.png", h(), False, "added", "data/img/x.png"),
+                     ("data/img/x.png", h(), False, "modified", "data/img/x.png"),
+                     ("data/img/y.png", h(), False, "removed", "data/img/y.png"),
+                     ("data/img/y.png", h(), False, "added", "data/img/y.png"),
+                     ("z.png", h(), False, "added", "z.png")],
+        "data/img2": [("data/img2/q.png", h(), False, "added", "data/img2/q.png")],
+    }
+    existing = {"data/img": [("data/img/old.png", h(), False, "unmodified", "data/img/old.png"),
+                             ("data/img/gone.png", h(), False, "unmodified", "data/img/gone.png")]}
+    entries["data/img"].append(("data/img/gone.png", h(), False, "removed", "data/img/gone.png"))
+    return entries, existing
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("vnode_size", [10_000, 2])
+def test_native_commit_driver_odd_paths(cuda, cli, vnode_size):
+    entries, existing = _odd_paths_commit()
+    vn, removed = _check(_run(cli, entries, existing, vnode_size), entries, existing, vnode_size)
+    assert "data/img" in removed
+
+
+def test_odd_paths_python_driver_matches_oracle(monkeypatch, oracle_lib):
+    """The same odd-path commit through the Python driver (hash calls answered by the oracle on the
+    CPU): the reference point the native driver is held to above."""
+    from oracle import commit_oracle
+    from oxen_amd import hasher, merkle
+
+    monkeypatch.setattr(hasher, "hash_streams_128bit", lambda s, ctx=None: [oracle_lib.xxh3_128_int(x) for x in s])
+    entries, existing = _odd_paths_commit()
+    for vnode_size in (10_000, 2):
+        vn, dh = merkle.commit_tree(_commit.to_staged(entries), _commit.to_staged(existing), vnode_size, _commit.salt)
+        rvn, rdh = commit_oracle.commit_tree(entries, existing, vnode_size, _commit.salt)
+        for d in rvn:
+            assert [v.id.value for v in vn[d][0]] == [i for i, _ in rvn[d]], d
+        assert {d: x.value for d, x in dh.items()} == rdh
