@@ -64,6 +64,8 @@ static constexpr uint64_t kCdcMasks[26] = {
 
 constexpr uint32_t kSecDefault = 512 * 1024;  // minimum section bytes (F1 wave / F2 lane unit)
 constexpr int kHashSpan = 47;          // positions after a chunk's start index with a truncated window
+constexpr int kEntryShift = 47;        // candidate entry: group index (17 bits: units up to 2 MiB) << 47 | hash
+constexpr uint64_t kEntryHash = (1ull << kEntryShift) - 1;
 
 struct CdcParams {
     uint64_t min, avg, max;
@@ -81,8 +83,9 @@ struct CdcFiles {
     const uint64_t* flen;      // [n]
     const uint64_t* sec_base;  // [n+1] first global section of each file
     const uint32_t* sec_file;  // [n_sec] file of each section
-    uint32_t* cand;            // [n_sec * 64 * cap] candidate groups per unit: offset in the unit (16-aligned), in order
-    uint64_t* cand_h;          // [n_sec * 64 * cap] full-window hash before each group's first byte (mod 2^48)
+    uint64_t* cand_e;          // [n_sec * 64 * cap] candidate groups per unit, in order: group index in the unit
+                               // << 47 | the full-window hash before its first byte mod 2^47 (bit 47 and up
+                               // never reach a masked bit once the walk shifts it, so 47 bits suffice)
     uint4* cand_b;             // [n_sec * 64 * cap] the group's 16 bytes (the walk resolves flags from these)
     uint32_t* cand_cnt;        // [n_sec * 64] true count per unit (> cap: list truncated, dense fallback)
     uint64_t* cand_occ;        // [n_sec] bit u: unit u of the section has a non-empty list
@@ -196,8 +199,7 @@ __global__ __launch_bounds__(64 * kScanWaves) void cdc_scan_kernel(CdcFiles f, C
         return *(const uint64_t*)(tab + a);
     };
     const uint64_t ubase = sec * 64 + (uint64_t)lane;  // global unit index
-    uint32_t* __restrict__ out = f.cand + ubase * prm.cap;
-    uint64_t* __restrict__ out_h = f.cand_h + ubase * prm.cap;
+    uint64_t* __restrict__ out_e = f.cand_e + ubase * prm.cap;
     uint4* __restrict__ out_b = f.cand_b + ubase * prm.cap;
     uint32_t count = 0;  // per lane
 
@@ -262,6 +264,9 @@ __global__ __launch_bounds__(64 * kScanWaves) void cdc_scan_kernel(CdcFiles f, C
 #pragma unroll
             for (int b = 0; b < 4; ++b) G[i][b] = gear(wv[i], b);
         uint64_t hb = h;  // the hash before the current group
+        // opaque copy: kept in two VGPRs (otherwise hipcc may re-derive it inside the rare record
+        // branch from the rolled hashes, which costs hundreds of extra shift-adds per round)
+        asm volatile("" : "+v"(hb));
         uint32_t anyz = 0xFFFFFFFFu;
 #pragma unroll
         for (int i = 0; i < 32; ++i) {
@@ -284,8 +289,7 @@ __global__ __launch_bounds__(64 * kScanWaves) void cdc_scan_kernel(CdcFiles f, C
                     const uint32_t g = rb + 16 * (uint32_t)(i >> 2);  // the group, section-relative
                     if (anyz == 0 && g < sec_len) {
                         if (count < prm.cap) {
-                            out[count] = g - us;
-                            out_h[count] = SH ? (hb >> 16) : hb;
+                            out_e[count] = ((uint64_t)((g - us) >> 4) << kEntryShift) | ((SH ? (hb >> 16) : hb) & kEntryHash);
                             out_b[count] = make_uint4(wv[i - 3], wv[i - 2], wv[i - 1], wv[i]);
                         }
                         ++count;
@@ -293,6 +297,7 @@ __global__ __launch_bounds__(64 * kScanWaves) void cdc_scan_kernel(CdcFiles f, C
                 }
                 anyz = 0xFFFFFFFFu;
                 hb = h;
+                asm volatile("" : "+v"(hb));
             }
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -389,16 +394,16 @@ __device__ uint64_t first_cand(const CdcFiles& f, const CdcParams& prm, uint64_t
         }
         const uint64_t sec_start = (cur.sec - u0) * prm.unit;  // the unit's start, file-relative
         if (sec_start >= hi) return hi;
-        const uint32_t* list = f.cand + cur.sec * prm.cap;
-        const uint64_t* hs = f.cand_h + cur.sec * prm.cap;
+        const uint64_t* es = f.cand_e + cur.sec * prm.cap;
         const uint32_t cnt = f.cand_cnt[cur.sec];
         const uint32_t stored = cnt < prm.cap ? cnt : prm.cap;
         while (cur.idx < stored) {
-            const uint64_t g = sec_start + list[cur.idx];
+            const uint64_t e = es[cur.idx];
+            const uint64_t g = sec_start + (e >> kEntryShift) * 16;
             if (g >= hi) return hi;
             if (g + 16 > lo) {  // the group overlaps [lo, hi)
                 if (cur.rsec != cur.sec || cur.rsec_idx != cur.idx) {
-                    resolve_group(f.cand_b[cur.sec * prm.cap + cur.idx], g, hs[cur.idx], flen, prm, gear, cur.rfs, cur.rfl);
+                    resolve_group(f.cand_b[cur.sec * prm.cap + cur.idx], g, e & kEntryHash, flen, prm, gear, cur.rfs, cur.rfl);
                     cur.rsec = cur.sec;
                     cur.rsec_idx = cur.idx;
                 }
@@ -416,7 +421,7 @@ __device__ uint64_t first_cand(const CdcFiles& f, const CdcParams& prm, uint64_t
         const uint64_t sec_end = sec_start + prm.unit;
         if (cnt > prm.cap) {
             // overflowed list: positions after the last stored group were not recorded
-            const uint64_t after = stored ? sec_start + list[stored - 1] + 16 : sec_start;
+            const uint64_t after = stored ? sec_start + (es[stored - 1] >> kEntryShift) * 16 + 16 : sec_start;
             const uint64_t a = lo > after ? lo : after;
             const uint64_t b = hi < sec_end ? hi : sec_end;
             if (a < b) {
@@ -805,6 +810,10 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     if (prm.sec < max_rounded) prm.sec = max_rounded;
     if (!getenv("OXH_CDC_SECTION_BYTES") && prm.sec < 8 * max_rounded) prm.sec = 8 * max_rounded;
     prm.sec = (prm.sec + 8191) / 8192 * 8192;  // 64 F1 units of whole 128-byte rounds
+    // a candidate entry holds the group index in 17 bits: units of at most 2 MiB (sections of 128 MiB,
+    // 8 chunks of the crate's largest max); the test-only section override is clamped to that
+    prm.sec = std::min<uint64_t>(prm.sec, 128ull << 20);
+    if (prm.sec < max_rounded) return cdc_fail(OXH_ERR_INVALID, "section override below max_size");
     prm.unit = prm.sec / 64;
     if (const char* e = getenv("OXH_CDC_WARMUP_BYTES")) prm.warmup = strtoull(e, nullptr, 10);  // tests
     prm.cap = (uint32_t)std::min<double>(prm.unit / 16, 8.0 * dens * prm.unit + 8);
@@ -822,16 +831,15 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     auto since = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(); };
     Scratch sc(st);
     uint64_t *d_foff, *d_flen, *d_sec_base, *d_first, *d_exit, *d_out_base;
-    uint32_t *d_sec_file, *d_cand, *d_cand_cnt, *d_spec, *d_spec_cnt, *d_status, *d_k0, *d_count, *d_fix;
-    uint64_t *d_cand_h, *d_cand_occ;
+    uint32_t *d_sec_file, *d_cand_cnt, *d_spec, *d_spec_cnt, *d_status, *d_k0, *d_count, *d_fix;
+    uint64_t *d_cand_e, *d_cand_occ;
     uint4* d_cand_b;
     sc.want(&d_foff, n);
     sc.want(&d_flen, n);
     sc.want(&d_sec_base, n + 1);
     sc.want(&d_first, n + 1);
     sc.want(&d_sec_file, n_sec);
-    sc.want(&d_cand, n_sec * 64 * prm.cap);
-    sc.want(&d_cand_h, n_sec * 64 * prm.cap);
+    sc.want(&d_cand_e, n_sec * 64 * prm.cap);
     sc.want(&d_cand_b, n_sec * 64 * prm.cap);
     sc.want(&d_cand_cnt, n_sec * 64);
     sc.want(&d_cand_occ, n_sec);
@@ -855,7 +863,7 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     }
 
     const double t_alloc = since();
-    oxh::CdcFiles f{(const uint8_t*)d_arena, d_foff, d_flen, d_sec_base, d_sec_file, d_cand, d_cand_h, d_cand_b, d_cand_cnt, d_cand_occ, d_spec, d_spec_cnt};
+    oxh::CdcFiles f{(const uint8_t*)d_arena, d_foff, d_flen, d_sec_base, d_sec_file, d_cand_e, d_cand_b, d_cand_cnt, d_cand_occ, d_spec, d_spec_cnt};
     oxh::CdcStitch sti{d_status, d_k0, d_count, d_exit, d_fix, d_out_base};
     if (n_sec) {
         // F1: one wave per section (kScanWaves per workgroup, 128 KiB of LDS); SH when the bits both
