@@ -2,7 +2,11 @@
 #include "commit_writer.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <exception>
 #include <map>
 #include <random>
@@ -32,8 +36,7 @@ std::string join(const std::vector<std::string>& c, size_t n) {
 // Path's Ord on a normalised path (components joined by '/') is component-wise: bytewise with '/'
 // below every other byte (a component that ends first sorts first). With '/' mapped to '\0' the plain
 // (memcmp) string order is that order; paths hold no NUL.
-std::string sort_key(const std::string& normalised) {
-    std::string k = normalised;
+std::string sort_key(std::string k) {
     std::replace(k.begin(), k.end(), '/', '\0');
     return k;
 }
@@ -61,6 +64,18 @@ void parallel_for(size_t n, F&& fn) {
     for (auto& e : err)
         if (e) std::rethrow_exception(e);
 }
+
+// OXH_TRACE=1: wall time of each driver stage on stderr
+struct StageClock {
+    const bool on = std::getenv("OXH_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void mark(const char* what) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[commit] %-16s %.4fs\n", what, std::chrono::duration<double>(now - t).count());
+        t = now;
+    }
+};
 
 }  // namespace
 
@@ -122,32 +137,19 @@ std::vector<DirVNodes> split_into_vnodes(const StagedDirs& entries, const Existi
                                          const SaltFn& salt, oxh_ctx* ctx) {
     if (vnode_size == 0) throw OxenError::basic_str("vnode_size must be positive");
     // the child set of every staged dir (:561-638): HEAD's children, then the staged changes (a
-    // removal drops the child), keyed by the normalised path; ordered by Path's Ord at the end
-    struct Dir {
-        std::vector<StagedNode> nodes;
-        std::vector<std::string> keys;
-        std::vector<char> alive;
-        std::unordered_map<std::string, size_t> at;  // key -> live slot
-        std::vector<StagedNode> removed;
-        std::vector<size_t> order;  // live slots in path order
-        void put(std::string key, StagedNode&& n) {
-            auto it = at.find(key);
-            if (it != at.end()) {
-                nodes[it->second] = std::move(n);
-                return;
-            }
-            keys.push_back(sort_key(key));
-            at.emplace(std::move(key), nodes.size());
-            nodes.push_back(std::move(n));
-            alive.push_back(1);
-        }
-        void drop(const std::string& key) {
-            auto it = at.find(key);
-            if (it == at.end()) return;
-            alive[it->second] = 0;
-            at.erase(it);
-        }
+    // removal drops the child), keyed by the normalised path. Only the last operation on a path
+    // counts, so each dir's operations are sorted by (Path's Ord, arrival) and the last one of every
+    // path kept: the surviving children come out in path order with one sort and no hash map.
+    struct Op {
+        std::string key;  // sort_key of the normalised (possibly prefixed) path
+        const StagedNode* src;
+        bool put, prefixed;
     };
+    struct Dir {
+        std::vector<StagedNode> live;  // surviving children in path order
+        std::vector<StagedNode> removed;
+    };
+    StageClock clk;
     std::vector<Dir> dirs(entries.size());
     parallel_for(entries.size(), [&](size_t i) {
         const std::string& directory = entries[i].first;
@@ -155,97 +157,134 @@ std::vector<DirVNodes> split_into_vnodes(const StagedDirs& entries, const Existi
         const std::string dkey = join(dcomps, dcomps.size());
         Dir& d = dirs[i];
         const auto ex = existing.find(directory);
-        const size_t expect = entries[i].second.size() + (ex != existing.end() ? ex->second.size() : 0);
-        d.nodes.reserve(expect);
-        d.keys.reserve(expect);
-        d.alive.reserve(expect);
-        d.at.reserve(expect);
-        if (auto it = ex; it != existing.end())
-            for (const StagedNode& c : it->second) d.put(normalize(c.path), StagedNode(c));
+        std::vector<Op> ops;
+        ops.reserve(entries[i].second.size() + (ex != existing.end() ? ex->second.size() : 0));
+        if (ex != existing.end())
+            for (const StagedNode& c : ex->second) ops.push_back({sort_key(normalize(c.path)), &c, true, false});
         std::unordered_map<std::string, size_t> removed_at;  // a later removal of a path replaces it
-        for (StagedNode c : entries[i].second) {
+        for (const StagedNode& c : entries[i].second) {
             std::string ckey = normalize(c.path);
             if (ckey.empty()) continue;  // child_path != "" (:589)
+            bool prefixed = false;
             if (!dkey.empty() && !(ckey.size() > dkey.size() && ckey.compare(0, dkey.size(), dkey) == 0 &&
                                    ckey[dkey.size()] == '/') && ckey != dkey) {  // defensive prefixing (:591-612)
                 ckey = dkey + "/" + ckey;
-                c.path = ckey;
-                c.name = ckey;
+                prefixed = true;
             }
-            if (c.status == StagedStatus::Removed) {
-                d.drop(ckey);
+            const bool put = c.status != StagedStatus::Removed;
+            if (!put) {
+                StagedNode r = c;
+                if (prefixed) {
+                    r.path = ckey;
+                    r.name = ckey;
+                }
                 auto [it, fresh] = removed_at.emplace(ckey, d.removed.size());
-                if (fresh) d.removed.push_back(std::move(c));
-                else d.removed[it->second] = std::move(c);
-            } else {
-                d.put(std::move(ckey), std::move(c));
+                if (fresh) d.removed.push_back(std::move(r));
+                else d.removed[it->second] = std::move(r);
+            }
+            ops.push_back({sort_key(std::move(ckey)), &c, put, prefixed});
+        }
+        std::stable_sort(ops.begin(), ops.end(), [](const Op& x, const Op& y) { return x.key < y.key; });
+        d.live.reserve(ops.size());
+        for (size_t k = 0; k < ops.size(); ++k) {
+            if ((k + 1 < ops.size() && ops[k + 1].key == ops[k].key) || !ops[k].put) continue;
+            d.live.push_back(*ops[k].src);
+            if (ops[k].prefixed) {
+                std::string p = std::move(ops[k].key);
+                std::replace(p.begin(), p.end(), '\0', '/');
+                d.live.back().name = p;
+                d.live.back().path = std::move(p);
             }
         }
-        for (size_t k = 0; k < d.nodes.size(); ++k)
-            if (d.alive[k]) d.order.push_back(k);
-        std::sort(d.order.begin(), d.order.end(), [&](size_t x, size_t y) { return d.keys[x] < d.keys[y]; });
     });
-    // bucket = xxh3_128(path) % num_vnodes (:665-681): every child of every dir in one pass
-    std::string arena;
-    std::vector<uint64_t> offs, lens;
-    size_t n_children = 0, path_bytes = 0;
-    for (const Dir& d : dirs)
-        for (size_t k : d.order) {
-            ++n_children;
-            path_bytes += d.nodes[k].path.size();
+    clk.mark("child sets");
+    // bucket = xxh3_128(path) % num_vnodes (:665-681): every child of every dir in one pass; each
+    // dir writes its own slice of the stream arena
+    const size_t nd = dirs.size();
+    std::vector<size_t> first(nd + 1, 0), at(nd + 1, 0);
+    parallel_for(nd, [&](size_t i) {
+        for (const StagedNode& c : dirs[i].live) at[i + 1] += c.path.size();
+    });
+    for (size_t i = 0; i < nd; ++i) {
+        first[i + 1] = first[i] + dirs[i].live.size();
+        at[i + 1] += at[i];
+    }
+    std::string arena(at[nd], '\0');
+    std::vector<uint64_t> offs(first[nd]), lens(first[nd]);
+    parallel_for(nd, [&](size_t i) {
+        size_t o = at[i], q = first[i];
+        for (const StagedNode& c : dirs[i].live) {
+            offs[q] = o;
+            lens[q++] = c.path.size();
+            std::memcpy(&arena[o], c.path.data(), c.path.size());
+            o += c.path.size();
         }
-    arena.reserve(path_bytes);
-    offs.reserve(n_children);
-    lens.reserve(n_children);
-    for (const Dir& d : dirs)
-        for (size_t k : d.order) {
-            offs.push_back(arena.size());
-            lens.push_back(d.nodes[k].path.size());
-            arena += d.nodes[k].path;
-        }
+    });
+    clk.mark("bucket streams");
     const std::vector<u128> buckets = hash_streams(arena, offs, lens, ctx);
-    std::vector<DirVNodes> out(entries.size());
-    size_t k = 0;
-    for (size_t i = 0; i < dirs.size(); ++i) {
+    clk.mark("bucket hash");
+    std::vector<DirVNodes> out(nd);
+    std::vector<size_t> vfirst(nd + 1, 0);
+    parallel_for(nd, [&](size_t i) {
         out[i].dir = entries[i].first;
         out[i].removed = std::move(dirs[i].removed);
-        const uint64_t nv = num_vnodes(dirs[i].order.size(), vnode_size);
+        const uint64_t nv = num_vnodes(dirs[i].live.size(), vnode_size);
         out[i].vnodes.resize(nv);
-        std::vector<uint32_t> b(dirs[i].order.size());
+        vfirst[i + 1] = nv;
+        std::vector<uint32_t> b(dirs[i].live.size());
         std::vector<size_t> per(nv, 0);
-        for (size_t q = 0; q < b.size(); ++q) ++per[b[q] = (uint32_t)(buckets[k + q] % nv)];
+        for (size_t q = 0; q < b.size(); ++q) ++per[b[q] = (uint32_t)(buckets[first[i] + q] % nv)];
         for (uint64_t j = 0; j < nv; ++j) out[i].vnodes[j].entries.reserve(per[j]);
         // path order in, so every vnode's entries come out sorted (:684-694)
-        for (size_t q = 0; q < b.size(); ++q) out[i].vnodes[b[q]].entries.push_back(std::move(dirs[i].nodes[dirs[i].order[q]]));
-        k += b.size();
-    }
-    // vnode id = xxh3("vnode" || dir || child hashes LE [|| uuid]) (:683-720): every vnode in one pass
-    arena.clear();
-    offs.clear();
-    lens.clear();
-    arena.reserve(n_children * 16 + out.size() * 64);
-    for (const DirVNodes& d : out) {
+        for (size_t q = 0; q < b.size(); ++q) out[i].vnodes[b[q]].entries.push_back(std::move(dirs[i].live[q]));
+    });
+    for (size_t i = 0; i < nd; ++i) vfirst[i + 1] += vfirst[i];
+    clk.mark("vnode fill");
+    // vnode id = xxh3("vnode" || dir || child hashes LE [|| uuid]) (:683-720): every vnode in one
+    // pass. Stream sizes first (a vnode of a dir HEAD holds is salted when one of its entries
+    // changed, :713-716), then every dir fills its slice; the salts are drawn afterwards, on this
+    // thread, in vnode order.
+    const size_t nvn = vfirst[nd];
+    std::vector<char> salted(nvn, 0);
+    offs.assign(nvn + 1, 0);
+    lens.assign(nvn, 0);
+    parallel_for(nd, [&](size_t i) {
+        const DirVNodes& d = out[i];
         const bool dir_existed = existing.count(d.dir) != 0;
         for (size_t j = 0; j < d.vnodes.size(); ++j) {
-            const size_t start = arena.size();
-            arena += "vnode";
-            arena += d.dir;
             bool changed = false;
-            for (const StagedNode& c : d.vnodes[j].entries) {
-                put_le(arena, c.hash);
-                changed = changed || c.status != StagedStatus::Unmodified;
-            }
-            if (dir_existed && changed) {  // :713-716
-                uint8_t s[16];
-                salt(d.dir, j, s);
-                arena.append(reinterpret_cast<const char*>(s), 16);
-            }
-            offs.push_back(start);
-            lens.push_back(arena.size() - start);
+            for (const StagedNode& c : d.vnodes[j].entries) changed = changed || c.status != StagedStatus::Unmodified;
+            salted[vfirst[i] + j] = dir_existed && changed;
+            lens[vfirst[i] + j] = 5 + d.dir.size() + 16 * d.vnodes[j].entries.size() + (salted[vfirst[i] + j] ? 16 : 0);
         }
-    }
+    });
+    for (size_t v = 0; v < nvn; ++v) offs[v + 1] = offs[v] + lens[v];
+    arena.assign(offs[nvn], '\0');
+    offs.pop_back();
+    parallel_for(nd, [&](size_t i) {
+        const DirVNodes& d = out[i];
+        for (size_t j = 0; j < d.vnodes.size(); ++j) {
+            char* p = &arena[offs[vfirst[i] + j]];
+            std::memcpy(p, "vnode", 5);
+            std::memcpy(p + 5, d.dir.data(), d.dir.size());
+            p += 5 + d.dir.size();
+            for (const StagedNode& c : d.vnodes[j].entries) {
+                for (int b = 0; b < 16; ++b) p[b] = (char)(uint8_t)(c.hash >> (8 * b));
+                p += 16;
+            }
+        }
+    });
+    for (size_t i = 0; i < nd; ++i)
+        for (size_t j = 0; j < out[i].vnodes.size(); ++j)
+            if (salted[vfirst[i] + j]) {
+                uint8_t s16[16];
+                salt(out[i].dir, j, s16);
+                std::memcpy(&arena[offs[vfirst[i] + j] + lens[vfirst[i] + j] - 16], s16, 16);
+            }
+    clk.mark("vnode streams");
     const std::vector<u128> ids = hash_streams(arena, offs, lens, ctx);
-    k = 0;
+    clk.mark("vnode hash");
+    size_t k = 0;
     for (DirVNodes& d : out)
         for (EntryVNode& v : d.vnodes) v.id = MerkleHash(ids[k++]);
     return out;
@@ -253,6 +292,7 @@ std::vector<DirVNodes> split_into_vnodes(const StagedDirs& entries, const Existi
 
 std::vector<std::pair<std::string, MerkleHash>> compute_dir_hashes(const std::vector<DirVNodes>& vnodes,
                                                                    const std::vector<std::string>* dirs, oxh_ctx* ctx) {
+    StageClock clk;
     // what compute_dir_node feeds for each staged dir's vnodes (:1042-1071)
     std::vector<std::string> segs(vnodes.size());
     parallel_for(vnodes.size(), [&](size_t i) {
@@ -271,6 +311,7 @@ std::vector<std::pair<std::string, MerkleHash>> compute_dir_hashes(const std::ve
             }
         }
     });
+    clk.mark("dir segments");
     std::unordered_map<std::string, std::vector<size_t>> under;  // ancestor path -> descendants, in order
     for (size_t i = 0; i < vnodes.size(); ++i) {
         const std::vector<std::string> comps = path_components(vnodes[i].dir);
@@ -308,7 +349,9 @@ std::vector<std::pair<std::string, MerkleHash>> compute_dir_hashes(const std::ve
         offs.push_back(start);
         lens.push_back(arena.size() - start);
     }
+    clk.mark("dir streams");
     const std::vector<u128> h = hash_streams(arena, offs, lens, ctx);
+    clk.mark("dir hash");
     std::vector<std::pair<std::string, MerkleHash>> r;
     r.reserve(dirs->size());
     for (size_t i = 0; i < dirs->size(); ++i) r.emplace_back((*dirs)[i], MerkleHash(h[i]));
