@@ -45,6 +45,9 @@ extern "C" {
 #define OXH_MODE_WAVE 1     /* force K1: one 64-lane wave per buffer */
 #define OXH_MODE_LANE 2     /* force K1s: one lane per buffer (short items, parent-node streams) */
 #define OXH_MODE_WAVE_SHORT 3 /* K1 shaped for items of <= ~16 KiB (more resident waves) */
+#define OXH_MODE_WAVE_PACKED 4 /* K1 shaped for items packed back to back at arbitrary byte offsets
+                                  (FastCDC chunks of one buffer): each wave-instruction reads a
+                                  whole 1 KiB block */
 
 typedef struct oxh_ctx oxh_ctx;
 

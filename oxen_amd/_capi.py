@@ -23,6 +23,7 @@ OXH_MODE_AUTO = 0
 OXH_MODE_WAVE = 1
 OXH_MODE_LANE = 2
 OXH_MODE_WAVE_SHORT = 3
+OXH_MODE_WAVE_PACKED = 4
 OXH_MAX_STAGING_BYTES = 2147483392  # 2 GiB - 256 (include/oxen_hash.h)
 
 _u64 = ctypes.c_uint64

@@ -903,8 +903,9 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
         CDC_HIP(hipGetLastError());
     }
     if (d_digests && total) {
-        const int mode = avg_size <= 16384 ? OXH_MODE_WAVE_SHORT : OXH_MODE_WAVE;
-        rc = oxh_xxh3_128_batch_device(d_arena, d_chunk_offsets, d_chunk_lens, total, d_digests, mode, stream);
+        // chunks sit back to back at arbitrary byte offsets: the block-wise K1 (OXH_MODE_WAVE_PACKED)
+        rc = oxh_xxh3_128_batch_device(d_arena, d_chunk_offsets, d_chunk_lens, total, d_digests, OXH_MODE_WAVE_PACKED,
+                                       stream);
         if (rc) return cdc_fail(rc, std::string("chunk digests: ") + oxh_last_error());
     }
     CDC_HIP(hipStreamSynchronize(st));

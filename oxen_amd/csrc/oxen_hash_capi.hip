@@ -101,6 +101,9 @@ WaveKernel wave_kernel_for(int variant) {
         case 12: return oxh::xxh3_wave_kernel<DESC, 12>;
         case 64: return oxh::xxh3_wave_kernel<DESC, 64>;
         case 72: return oxh::xxh3_wave_kernel<DESC, 72>;
+        case 74: return oxh::xxh3_wave_kernel<DESC, 74>;
+        case 40: return oxh::xxh3_wave_kernel<DESC, 40>;
+        case 104: return oxh::xxh3_wave_kernel<DESC, 104>;
         default: return oxh::xxh3_wave_kernel<DESC, 0>;
     }
 }
@@ -111,22 +114,33 @@ WaveKernel wave_kernel_for(int variant) {
 // 201 VGPRs, 2 waves/SIMD) matches it on equal 64 KiB items but loses 13 % on ragged, packed items
 // (FastCDC chunks: tools/k1_align_probe.py) and 4 % of the C2 step rate. An explicit
 // oxh_set_kernel_variant() overrides the choice.
+//
+// Items packed back to back (FastCDC chunks) start at arbitrary byte offsets: a row-wise
+// instruction (256 B per row) then touches 3 lines where an aligned one touches 2, 12 lines per KiB
+// instead of 8, which costs 6-8 % at 8-64 KiB items; the block-wise layout (variant bit 5) reads a
+// whole KiB per instruction, 9 lines. tools/k1_small_probe.py (profiles/r02_k1_small_probe.json):
+// packed [4, 16) KiB items 6.17-6.23 TB/s block-wise vs 5.90-5.93 row-wise, packed [4, 128) KiB
+// 6.72 vs 6.25; on aligned items the row-wise variants stay ahead (6.75 vs 6.66 at 8 KiB).
 constexpr uint64_t kShortItemBytes = 16384;
-constexpr int kVariantShort = 72;  // Cfg: depth 2, keys in LDS
-constexpr int kVariantLong = 8;    // Cfg: depth 2, keys from the constant table
+constexpr int kVariantShort = 72;    // Cfg: row-wise, depth 2, keys in LDS
+constexpr int kVariantLong = 8;      // Cfg: row-wise, depth 2, keys from the constant table
+constexpr int kVariantPacked = 104;  // Cfg: block-wise, depth 2, keys in LDS
 
-int pick_variant(bool short_items) {
+enum class ItemShape { Long, Short, Packed };
+
+int pick_variant(ItemShape shape) {
     const int v = g_variant.load();
     if (v != 0) return v;
-    return short_items ? kVariantShort : kVariantLong;
+    return shape == ItemShape::Packed ? kVariantPacked : shape == ItemShape::Short ? kVariantShort : kVariantLong;
 }
+int pick_variant(bool short_items) { return pick_variant(short_items ? ItemShape::Short : ItemShape::Long); }
 
 // K1 over a descriptor table: one 64-lane wave per item, 4 waves per 256-thread workgroup.
 int launch_wave(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens, uint64_t n, uint64_t* out,
-                hipStream_t st, bool short_items = false) {
+                hipStream_t st, ItemShape shape = ItemShape::Long) {
     if (n == 0) return OXH_OK;
     const uint64_t blocks = (n + 3) / 4;
-    hipLaunchKernelGGL(wave_kernel_for<true>(pick_variant(short_items)), dim3((unsigned)blocks), dim3(256), 0, st, arena, offs,
+    hipLaunchKernelGGL(wave_kernel_for<true>(pick_variant(shape)), dim3((unsigned)blocks), dim3(256), 0, st, arena, offs,
                        lens, n, (uint64_t)0, (uint64_t)0, out);
     HIP_TRY(hipGetLastError());
     return OXH_OK;
@@ -367,7 +381,7 @@ int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_
                                 short_items)
              : any_short_only ? launch_lane(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->stream)
                               : launch_wave(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->stream,
-                                            short_items);
+                                            short_items ? ItemShape::Short : ItemShape::Long);
     if (rc) return rc;
     STEP("launched s=%d", s);
     HIP_TRY(hipMemcpyAsync(c->h_out[s], c->d_out[s], cnt * 16, hipMemcpyDeviceToHost, c->stream));
@@ -865,7 +879,8 @@ int oxh_xxh3_128_batch_device(const void* d_arena, const uint64_t* d_offsets, co
     const uint8_t* a = (const uint8_t*)d_arena;
     if (mode == OXH_MODE_LANE) return launch_lane(a, d_offsets, d_lens, n, d_out, st);
     if (mode == OXH_MODE_AUTO || mode == OXH_MODE_WAVE) return launch_wave(a, d_offsets, d_lens, n, d_out, st);
-    if (mode == OXH_MODE_WAVE_SHORT) return launch_wave(a, d_offsets, d_lens, n, d_out, st, true);
+    if (mode == OXH_MODE_WAVE_SHORT) return launch_wave(a, d_offsets, d_lens, n, d_out, st, ItemShape::Short);
+    if (mode == OXH_MODE_WAVE_PACKED) return launch_wave(a, d_offsets, d_lens, n, d_out, st, ItemShape::Packed);
     return fail(OXH_ERR_INVALID, "unknown mode");
 }
 

@@ -89,6 +89,12 @@ __device__ __forceinline__ void bcast_rows64(uint64_t x, uint64_t t[4], int lane
 //   bit 1     0 = non-temporal (nt) loads for the once-read input stream, 1 = default-policy loads
 //   bits 2-3  rounds in flight per wave (software pipeline depth): 0 -> 4, 1 -> 3, 2 -> 2, 3 -> 5
 //   bit 4     1 = stagger: waves of the first resident generation start 0..15 x ~1 us apart
+//   bit 5     1 = block-wise layout: load j of a round reads block j whole (1 KiB contiguous per
+//             wave-instruction; lane l holds stripe l/4, piece l%4 of every block, so its keys are
+//             fixed), and a reduce-scatter across rows (permlane32/16 swaps) hands row g block g's
+//             partial sums before the usual in-row fold. 0 = row-wise: row g reads block g, 256 B per
+//             instruction. At a start that is not 128-B aligned a row-wise instruction touches 12
+//             lines per KiB, a block-wise one 9 (tools/k1_small_probe.py).
 //   bit 6     1 = stripe keys read from an LDS copy of the secret at each use (fewer VGPRs)
 // Measured on MI355X (C2, tools/readbw.py, profiles/r01_readbw*.json): nt loads ~+11 % over
 // default-policy loads; 4 rounds in flight (2 waves/SIMD at 180 VGPRs) ~+4 % over 2 rounds (5 waves/SIMD).
@@ -99,6 +105,7 @@ struct Cfg {
     static constexpr int DEPTH = ((V >> 2) & 3) == 0 ? 4 : ((V >> 2) & 3) == 1 ? 3 : ((V >> 2) & 3) == 2 ? 2 : 5;
     static constexpr bool KEYS_LDS = ((V >> 6) & 1) != 0;
     static constexpr bool STAGGER = ((V >> 4) & 1) != 0;
+    static constexpr bool BLOCKWISE = ((V >> 5) & 1) != 0;
 };
 
 template <bool ALIGNED, bool NT = false>
@@ -167,6 +174,26 @@ __device__ __forceinline__ void fold_round(uint64_t s0, uint64_t s1, uint64_t& a
     }
 }
 
+// Block-wise layout: lane (g, q, k) holds, for each block j of the round, the partial sum of
+// stripe 4g+q (v[j]). Two swap-and-add steps leave row g with block g's sum over the four rows
+// (still split by q; fold_round's in-row adds finish it):
+//   permlane32_swap(v0, v2) -> (v0 lower half, v2 lower half), (v0 upper, v2 upper): the sum holds
+//   block 0 in rows 0-1 and block 2 in rows 2-3 (likewise blocks 1 / 3); permlane16_swap of those
+//   two then leaves (block 0, block 1, block 2, block 3) in rows (0, 1, 2, 3).
+__device__ __forceinline__ uint64_t swap32_add(uint64_t a, uint64_t b) {
+    const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)a, (uint32_t)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(a >> 32), (uint32_t)(b >> 32), false, false);
+    return (((uint64_t)hi[0] << 32) | lo[0]) + (((uint64_t)hi[1] << 32) | lo[1]);
+}
+__device__ __forceinline__ uint64_t swap16_add(uint64_t a, uint64_t b) {
+    const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)a, (uint32_t)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(a >> 32), (uint32_t)(b >> 32), false, false);
+    return (((uint64_t)hi[0] << 32) | lo[0]) + (((uint64_t)hi[1] << 32) | lo[1]);
+}
+__device__ __forceinline__ uint64_t rows_from_blocks(const uint64_t (&v)[4]) {
+    return swap16_add(swap32_add(v[0], v[2]), swap32_add(v[1], v[3]));
+}
+
 // Buffer resource over one item: loads at voffset >= num_records are dropped by the hardware range
 // check (no memory traffic, zeros returned), which lets the pipeline issue every prefetch
 // unconditionally -- no branch around a load, so the register ring never needs a phi/copy.
@@ -194,11 +221,14 @@ template <int VARIANT, bool TEXT, bool BS>
 __device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_t len,
                                           uint64_t* __restrict__ out, int lane, const uint64_t* lds_sec,
                                           uint64_t* __restrict__ counts, uint32_t bs = 0) {
+    constexpr bool BW = Cfg<VARIANT>::BLOCKWISE;
+    constexpr uint32_t JSTRIDE = BW ? 1024u : 256u;  // bytes between a lane's loads j and j+1
     const int g = lane >> 4, q = (lane >> 2) & 3, k = lane & 3;
     uint32_t n_nl = 0, n_cont = 0;  // TEXT only
-    // stripe keys: secret words (4j + q + 2k, +1)
+    // stripe keys: secret words (stripe + 2k, +1); the lane's stripe in load j is 4j + q (row-wise)
+    // or 4g + q (block-wise, the same for every j)
     auto keys = [&](int j, uint64_t& k0, uint64_t& k1) {
-        int idx = 4 * j + q + 2 * k;
+        int idx = (BW ? 4 * g : 4 * j) + q + 2 * k;
         if constexpr (Cfg<VARIANT>::KEYS_LDS) {
             asm volatile("" : "+v"(idx));  // opaque: keep the LDS reads inside the loop
             k0 = lds_sec[idx];
@@ -213,7 +243,7 @@ __device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_
 
     const uint64_t nb = (len - 1) >> 10;  // blocks followed by a scramble
     const uint64_t nr = nb >> 2;          // full rounds (4 scrambled blocks each)
-    const uint32_t lane_off = (uint32_t)(g * 1024 + q * 64 + k * 16);
+    const uint32_t lane_off = (uint32_t)(g * (BW ? 256 : 1024) + q * 64 + k * 16);
     // round rr lives in 1 GiB window rr >> 18; descriptor over that window (wave-uniform, SALU work)
     auto window_rsrc = [&](uint64_t rr) {
         const uint64_t base = (rr >> 18) << 30;
@@ -222,15 +252,17 @@ __device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_
                                                  (int)(rem < 0x7FFFFFFFull ? rem : 0x7FFFFFFFull), kRsrcFlags);
     };
     // Rounds 0 .. nr-1 are full (4 scrambled blocks); round nr is the partial final round: blocks
-    // 4nr .. nb-1 full, block nb with `ns` stripes. Stripe s = 4j + q of row g is live in round rr
-    // if rr < nr, or rr == nr and (b < nb or (b == nb and s < ns)) with b = 4nr + g.
+    // 4nr .. nb-1 full, block nb with `ns` stripes. The lane's piece of load j (block b, stripe s:
+    // row-wise b = 4nr + g, s = 4j + q; block-wise b = 4nr + j, s = 4g + q) is live in round rr if
+    // rr < nr, or rr == nr and (b < nb or (b == nb and s < ns)).
     const uint64_t ns = ((len - 1) - (nb << 10)) >> 6;
-    const uint64_t bfin = nr * 4 + g;
     // branch-free (bitwise) so that no load ends up inside control flow
-    const bool fin_row_full = bfin < nb;
-    const bool fin_row_part = bfin == nb;
+    auto fin_full = [&](int j) -> bool { return nr * 4 + (uint64_t)(BW ? j : g) < nb; };
+    auto fin_part = [&](int j) -> bool { return nr * 4 + (uint64_t)(BW ? j : g) == nb; };
+    auto stripe_of = [&](int j) -> uint64_t { return (uint64_t)((BW ? 4 * g : 4 * j) + q); };
     auto live_j = [&](uint64_t rr, int j) -> bool {
-        const bool in_part = fin_row_full | (fin_row_part & ((uint64_t)(4 * j + q) < ns));
+        const bool fp = fin_part(j), ff = fin_full(j);
+        const bool in_part = ff | (fp & (stripe_of(j) < ns));
         return (rr < nr) | ((rr == nr) & in_part);
     };
     auto load_round = [&](uint64_t rr, uint4 (&dst)[4], uint32_t& ext) {
@@ -240,13 +272,15 @@ __device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_
         for (int j = 0; j < 4; ++j) {
             // BS: the first lane of the stripe after a partial block's last live stripe loads too (its
             // first dword completes the last live piece; dwords past the item read as 0)
-            const bool extra = BS && (rr == nr) & fin_row_part & ((uint64_t)(4 * j + q) == ns) & (k == 0);
-            dst[j] = bload16<Cfg<VARIANT>::NT>(rsrc, (live_j(rr, j) | extra) ? vo + j * 256 : kOOB);
+            const bool fp = fin_part(j);
+            const bool extra = BS && (rr == nr) & fp & (stripe_of(j) == ns) & (k == 0);
+            dst[j] = bload16<Cfg<VARIANT>::NT>(rsrc, (live_j(rr, j) | extra) ? vo + j * JSTRIDE : kOOB);
         }
         if constexpr (BS) {
-            // the dword right after the row's block, for the row's last lane (lanes 15, 31, 47, 63)
-            const bool l15 = (lane & 15) == 15;
-            ext = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (l15 && live_j(rr, 3)) ? vo + 3 * 256 + 16 : kOOB, 0,
+            // the dword right after the last piece of load 3, for the lane that holds that piece
+            // (row-wise: each row's last lane, 15 / 31 / 47 / 63; block-wise: lane 63)
+            const bool tail = BW ? lane == 63 : (lane & 15) == 15;
+            ext = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (tail && live_j(rr, 3)) ? vo + 3 * JSTRIDE + 16 : kOOB, 0,
                                                        Cfg<VARIANT>::NT ? 2 : 0);
         } else {
             ext = 0;
@@ -255,13 +289,16 @@ __device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_
     // BS: item bytes [o, o+16) of every piece from the aligned pieces (see above)
     auto realign = [&](uint4 (&src)[4], uint32_t ext) {
         if constexpr (BS) {
-            const bool l15 = (lane & 15) == 15;
+            // the next lane's first dword: row_ror:15 inside a row (row-wise), wave_rol:1 (block-wise);
+            // the lane holding a load's last piece takes it from load j+1 (lane 0 of its row / wave)
+            const bool tail = BW ? lane == 63 : (lane & 15) == 15;
             uint32_t nb[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) nb[j] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)src[j].x, 0x12F, 0xf, 0xf, false);
+            for (int j = 0; j < 4; ++j)
+                nb[j] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)src[j].x, BW ? 0x134 : 0x12F, 0xf, 0xf, false);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const uint32_t n0 = l15 ? (j < 3 ? nb[j + 1] : ext) : nb[j];
+                const uint32_t n0 = tail ? (j < 3 ? nb[j + 1] : ext) : nb[j];
                 const uint4 a = src[j];
                 src[j] = make_uint4(__builtin_amdgcn_alignbyte(a.y, a.x, bs), __builtin_amdgcn_alignbyte(a.z, a.y, bs),
                                     __builtin_amdgcn_alignbyte(a.w, a.z, bs), __builtin_amdgcn_alignbyte(n0, a.w, bs));
@@ -271,13 +308,28 @@ __device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_
     auto fold4 = [&](uint4 (&src)[4], uint32_t ext, uint64_t rr, bool partial) {
         realign(src, ext);
         uint64_t s0 = 0, s1 = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        if constexpr (BW) {
+            uint64_t v0[4] = {0, 0, 0, 0}, v1[4] = {0, 0, 0, 0};
             uint64_t k0, k1;
-            keys(j, k0, k1);
-            if (!partial || live_j(rr, j)) {
-                accum16(src[j], k0, k1, s0, s1);
-                if constexpr (TEXT) count16(src[j], n_nl, n_cont);
+            keys(0, k0, k1);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (!partial || live_j(rr, j)) {
+                    accum16(src[j], k0, k1, v0[j], v1[j]);
+                    if constexpr (TEXT) count16(src[j], n_nl, n_cont);
+                }
+            }
+            s0 = rows_from_blocks(v0);
+            s1 = rows_from_blocks(v1);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint64_t k0, k1;
+                keys(j, k0, k1);
+                if (!partial || live_j(rr, j)) {
+                    accum16(src[j], k0, k1, s0, s1);
+                    if constexpr (TEXT) count16(src[j], n_nl, n_cont);
+                }
             }
         }
         fold_round<Cfg<VARIANT>::BCAST>(s0, s1, a0, a1, sk0, sk1, partial ? (int)(nb - nr * 4) : 4, lane);
@@ -772,6 +824,12 @@ template __global__ void xxh3_wave_kernel<true, 64>(const uint8_t*, const uint64
 template __global__ void xxh3_wave_kernel<false, 64>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 template __global__ void xxh3_wave_kernel<true, 72>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 template __global__ void xxh3_wave_kernel<false, 72>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<true, 40>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<false, 40>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<true, 104>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<false, 104>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<true, 74>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<false, 74>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 template __global__ void xxh3_text_wave_kernel<0>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t*, uint64_t*);
 template __global__ void xxh3_text_wave_kernel<72>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t*, uint64_t*);
 template __global__ void xxh3_text_wave_kernel<8>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t*, uint64_t*);

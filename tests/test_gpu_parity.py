@@ -39,7 +39,7 @@ def _mismatch(got, want, lens):
     return [int(lens[i]) for i in bad[:20]]
 
 
-VARIANTS = [0, 1, 2, 4, 8, 12, 64, 72]  # K1 variants (xxh3_kernels.hip Cfg); 0 is the shipped path
+VARIANTS = [0, 1, 2, 4, 8, 12, 40, 64, 72, 74, 104]  # K1 variants (xxh3_kernels.hip Cfg); 0 is the shipped path
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2, 3])
@@ -756,10 +756,10 @@ def test_hash_files_given_metadata(oracle_lib, tmp_path, cuda):
     assert d[-2] is None and d[-1] is None
 
 
-@pytest.mark.parametrize("mode", ["short", "auto"])
+@pytest.mark.parametrize("mode", ["short", "packed", "auto"])
 def test_k1_many_ragged_items(cuda, oracle_lib, mode):
     """Many ragged, byte-packed items (FastCDC-chunk-like, with short-path items mixed in): the
-    short-item and the default K1 dispatch against the oracle."""
+    short-item, packed (block-wise) and default K1 dispatch against the oracle."""
     import torch
 
     from oxen_amd import _capi
@@ -774,7 +774,7 @@ def test_k1_many_ragged_items(cuda, oracle_lib, mode):
     fill_splitmix(arena, 1234)
     o = torch.from_numpy(offs.view(np.int64)).to(cuda)
     ln = torch.from_numpy(lens.view(np.int64)).to(cuda)
-    m = _capi.OXH_MODE_WAVE_SHORT if mode == "short" else _capi.OXH_MODE_AUTO
+    m = {"short": _capi.OXH_MODE_WAVE_SHORT, "packed": _capi.OXH_MODE_WAVE_PACKED}.get(mode, _capi.OXH_MODE_AUTO)
     got = _u64(xxh3_128_batch_device(arena, o, ln, mode=m))
     want = oracle_lib.batch(arena.cpu().numpy(), offs, lens, threads=8)
     assert np.array_equal(got, want)

@@ -72,7 +72,7 @@ def main():
     splits = [int(k) for k in args.cu_split.split(",")]
     for chunk in [int(c) for c in args.chunks.split(",")]:
         mn, av, mx = 4096, chunk, 2 * chunk
-        mode = _capi.OXH_MODE_WAVE_SHORT if av <= 16384 else _capi.OXH_MODE_WAVE
+        mode = _capi.OXH_MODE_WAVE_PACKED
         out = fastcdc_outputs(arena, lens, mn)
         times = []
         for r in range(args.reps + 1):
