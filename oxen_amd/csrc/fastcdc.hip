@@ -395,15 +395,26 @@ __device__ uint64_t first_cand(const CdcFiles& f, const CdcParams& prm, uint64_t
         const uint64_t sec_start = (cur.sec - u0) * prm.unit;  // the unit's start, file-relative
         if (sec_start >= hi) return hi;
         const uint64_t* es = f.cand_e + cur.sec * prm.cap;
+        const uint4* bs = f.cand_b + cur.sec * prm.cap;
+        // an entry and its 16 bytes are loaded together (the bytes before the entry says whether they
+        // are needed), and the first pair together with the count (speculatively: slots past the
+        // count are scratch, read but never used)
         const uint32_t cnt = f.cand_cnt[cur.sec];
+        uint64_t e_nx = cur.idx < prm.cap ? es[cur.idx] : 0;
+        uint4 b_nx = cur.idx < prm.cap ? bs[cur.idx] : make_uint4(0, 0, 0, 0);
         const uint32_t stored = cnt < prm.cap ? cnt : prm.cap;
-        while (cur.idx < stored) {
-            const uint64_t e = es[cur.idx];
+        for (bool first = true; cur.idx < stored; first = false) {
+            if (!first) {
+                e_nx = es[cur.idx];
+                b_nx = bs[cur.idx];
+            }
+            const uint64_t e = e_nx;
+            const uint4 bv = b_nx;
             const uint64_t g = sec_start + (e >> kEntryShift) * 16;
             if (g >= hi) return hi;
             if (g + 16 > lo) {  // the group overlaps [lo, hi)
                 if (cur.rsec != cur.sec || cur.rsec_idx != cur.idx) {
-                    resolve_group(f.cand_b[cur.sec * prm.cap + cur.idx], g, e & kEntryHash, flen, prm, gear, cur.rfs, cur.rfl);
+                    resolve_group(bv, g, e & kEntryHash, flen, prm, gear, cur.rfs, cur.rfl);
                     cur.rsec = cur.sec;
                     cur.rsec_idx = cur.idx;
                 }
