@@ -15,7 +15,7 @@
 //                         48: the hash of position p is a function of b[p-47 .. p]), and records a
 //                         position-ordered list of candidate 16-byte groups per unit (a position with
 //                         none of the bits both masks share clear).
-//   F2 cdc_walk_kernel    one lane per section: a speculative walk that starts 4 max-sized chunks
+//   F2 cdc_walk_kernel    one lane per section: a speculative walk that starts 6 max-sized chunks
 //                         before the section (by then it has almost surely met the true walk) and
 //                         cuts chunks from the candidate lists until it passes the section end,
 //                         recording the starts inside the section. The first 47 positions after a chunk's `min` see a hash
@@ -811,13 +811,15 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     }
     // sections of at least `max` bytes: a chunk never spans a whole section (F3's invariant)
     // Speculative walks meet the true walk after ~1.5 chunks (median) and within 6 chunks in 99 % of
-    // random starts (measured with the oracle). Warm-up: 4 max-sized chunks, at least 128 KiB;
+    // random starts (measured with the oracle). Warm-up: 6 max-sized chunks, at least 128 KiB (r02
+    // sweep, walk + fixup: 64 KiB chunks 2.57 / 2.09 / 2.18 ms at 512 / 768 / 1024 KiB; 8 KiB chunks
+    // 3.95 / 3.89 / 4.06 / 4.43 ms at 96 / 128 / 192 / 256 KiB);
     // sections: at least 8 max-sized chunks and 512 KiB. Every section whose walk has not met the
     // true one is re-walked serially by F3, so at small chunk sizes the longer warm-up pays for itself
     // (C5 at 8 KiB: 57.2 ms vs 63.8 ms with 256 KiB sections and 64 KiB of warm-up; at 64 KiB: 53.8
     // vs 54.9 ms with 1 MiB sections; tools/bench_fastcdc.py sweeps).
     const uint64_t max_rounded = ((uint64_t)max_size + 1023) / 1024 * 1024;
-    prm.warmup = std::max<uint64_t>(4 * (uint64_t)max_size, 128 * 1024);
+    prm.warmup = std::max<uint64_t>(6 * (uint64_t)max_size, 128 * 1024);
     if (prm.sec < max_rounded) prm.sec = max_rounded;
     if (!getenv("OXH_CDC_SECTION_BYTES") && prm.sec < 8 * max_rounded) prm.sec = 8 * max_rounded;
     prm.sec = (prm.sec + 8191) / 8192 * 8192;  // 64 F1 units of whole 128-byte rounds
