@@ -69,3 +69,19 @@ def test_staging_limit_is_rejected_before_any_device_work(built_lib):
         with pytest.raises(_capi.OxenError) as e:
             _capi.Context(0, staging_bytes=bad)
         assert e.value.code == _capi.OXH_ERR_INVALID, e.value
+
+
+def test_python_constants_match_the_header():
+    """Every OXH_* integer #define in include/oxen_hash.h has the same value in oxen_amd._capi."""
+    import os
+    import re
+
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "oxen_hash.h")).read()
+    defines = {m.group(1): int(m.group(2), 0) for m in re.finditer(r"^#define\s+(OXH_[A-Z0-9_]+)\s+(-?(?:0x)?[0-9A-Fa-f]+)\b",
+                                                                  hdr, re.M)}
+    assert "OXH_MODE_WAVE_PACKED" in defines
+    bound = {k: v for k, v in vars(_capi).items() if k.startswith("OXH_") and isinstance(v, int)}
+    mismatched = {k: (v, bound[k]) for k, v in defines.items() if k in bound and bound[k] != v}
+    assert not mismatched, mismatched
+    modes = {k for k in defines if k.startswith("OXH_MODE_")}
+    assert modes <= set(bound), modes - set(bound)
