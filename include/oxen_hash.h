@@ -73,7 +73,9 @@ void* oxh_ctx_stream(oxh_ctx* ctx);
  * already resident in HBM: item i is d_arena[d_offsets[i] .. d_offsets[i] + d_lens[i]).
  * d_offsets / d_lens / d_out are device pointers; d_out receives 2*n u64. Asynchronous on `stream`.
  * Any start offset and length; starts off a dword boundary are loaded dword-aligned and re-aligned
- * in registers. */
+ * in registers. `mode` (OXH_MODE_*) only picks the kernel shape, never the result: AUTO / WAVE for
+ * items placed at 128-B (or coarser) aligned offsets, WAVE_SHORT when they are mostly <= 16 KiB,
+ * WAVE_PACKED for items packed back to back at arbitrary offsets (chunks of one buffer). */
 int oxh_xxh3_128_batch_device(const void* d_arena, const uint64_t* d_offsets, const uint64_t* d_lens,
                               uint64_t n, uint64_t* d_out, int mode, void* stream);
 
