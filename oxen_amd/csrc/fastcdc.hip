@@ -151,7 +151,7 @@ __device__ __forceinline__ uint32_t byte_of(const uint4& v, int j) {
 // the 64 banks exactly once. The gear table is stored 32 times (entry k of copy c at byte 256 k + 8 c,
 // lane l reads copy l % 32): the 32 lanes of a ds_read_b64 group never share a bank.
 // LDS: 64 KiB table + one 8 KiB slot per wave (the round being rolled sits in VGPRs while the next
-// round's DMA is in flight). tools/cdc_segment_probe.hip has the variants this was chosen from.
+// round's DMA is in flight): 160 KiB at 12 waves per workgroup. tools/cdc_segment_probe.hip has the variants this was chosen from.
 //
 // Candidates: a lane records a 16-byte group of its unit when one of its positions has none of the
 // bits both masks share (offset in the unit, the hash before the group, its 16 bytes); the walk
@@ -160,22 +160,27 @@ __device__ __forceinline__ uint32_t byte_of(const uint4& v, int j) {
 // SH: the whole hash runs 16 bits to the left (table entries GEAR << 16, masks << 16; only bits below
 // 48 matter). When the bits both masks share are all >= 16 they then sit in the high 32-bit word and
 // the per-byte test is one AND; otherwise (avg < ~2 KiB) the low word is tested too (v_and_or).
-constexpr int kScanWaves = 8;
+// 12 waves per workgroup: the 64 KiB table + 12 x 8 KiB slots fill the 160 KiB of LDS, 3 waves per
+// SIMD (119 VGPRs) instead of 2. The roll is one dependent v_lshl_add_u64 chain per lane, so the
+// third wave's chain fills issue slots (C5 at 8 KiB: F1 26.6 vs 28.2 ms with 8 waves, r02). 16 waves
+// with 64-byte rounds (4 KiB slots, half-line DMA) measured far slower (73 vs 52 ms end to end).
+// OXH_CDC_SCAN_WAVES=8 selects the 8-wave form for A/B.
+constexpr int kScanWaves = 12;
 #ifndef OXH_SCAN_DMA_AUX
 #define OXH_SCAN_DMA_AUX 2
 #endif
 constexpr int kScanDmaAux = OXH_SCAN_DMA_AUX;  // cache policy of the scan's LDS-DMA loads (2 = nt)
 
-template <bool SH>
-__global__ __launch_bounds__(64 * kScanWaves) void cdc_scan_kernel(CdcFiles f, CdcParams prm, uint64_t n_sec) {
+template <bool SH, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void cdc_scan_kernel(CdcFiles f, CdcParams prm, uint64_t n_sec) {
     // one LDS block: the table at address 0 (a gather address is then a single v_perm), slots after it
-    __shared__ __attribute__((aligned(16))) uint64_t lds[256 * 32 + kScanWaves * 1024];
+    __shared__ __attribute__((aligned(16))) uint64_t lds[256 * 32 + WAVES * 1024];
     for (int i = threadIdx.x; i < 256 * 32; i += blockDim.x) lds[i] = kGear[i >> 5] << (SH ? 16 : 0);
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint4* const slot = (uint4*)(lds + 256 * 32) + w * 512;
-    const uint64_t sec = (uint64_t)blockIdx.x * kScanWaves + (uint64_t)w;
+    const uint64_t sec = (uint64_t)blockIdx.x * WAVES + (uint64_t)w;
     if (sec >= n_sec) return;
     const uint32_t file = f.sec_file[sec];
     const uint64_t flen = f.flen[file];
@@ -879,12 +884,14 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     oxh::CdcFiles f{(const uint8_t*)d_arena, d_foff, d_flen, d_sec_base, d_sec_file, d_cand_e, d_cand_b, d_cand_cnt, d_cand_occ, d_spec, d_spec_cnt};
     oxh::CdcStitch sti{d_status, d_k0, d_count, d_exit, d_fix, d_out_base};
     if (n_sec) {
-        // F1: one wave per section (kScanWaves per workgroup, 128 KiB of LDS); SH when the bits both
+        // F1: one wave per section (kScanWaves per workgroup, 160 KiB of LDS); SH when the bits both
         // masks share are all >= 16
         const bool sh = (((prm.mask_s & prm.mask_l) << 16) & 0xFFFFFFFFull) == 0;
-        auto scan = sh ? oxh::cdc_scan_kernel<true> : oxh::cdc_scan_kernel<false>;
-        constexpr int waves = oxh::kScanWaves;
-        hipLaunchKernelGGL(scan, dim3((unsigned)((n_sec + waves - 1) / waves)), dim3(64 * waves), 0, st, f, prm, n_sec);
+        static const int waves = getenv("OXH_CDC_SCAN_WAVES") ? atoi(getenv("OXH_CDC_SCAN_WAVES")) : oxh::kScanWaves;
+        auto scan = waves == 8 ? (sh ? oxh::cdc_scan_kernel<true, 8> : oxh::cdc_scan_kernel<false, 8>)
+                               : (sh ? oxh::cdc_scan_kernel<true, 12> : oxh::cdc_scan_kernel<false, 12>);
+        const int wv = waves == 8 ? 8 : 12;
+        hipLaunchKernelGGL(scan, dim3((unsigned)((n_sec + wv - 1) / wv)), dim3(64 * wv), 0, st, f, prm, n_sec);
         CDC_HIP(hipGetLastError());
         hipLaunchKernelGGL(oxh::cdc_walk_kernel, dim3((unsigned)((n_sec + 255) / 256)), dim3(256), 0, st, f, prm, n_sec);
         CDC_HIP(hipGetLastError());

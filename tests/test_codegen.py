@@ -52,6 +52,7 @@ def test_kernels_do_not_spill(built_lib, tmp_path):
     # SGPR spills go to VGPR lanes (no memory traffic) and are tolerated; VGPR spills and scratch are not
     bad = {n: v for n, v in k.items() if v.get("vgpr_spill_count", 0) or v.get("private_segment_fixed_size", 0)}
     assert not bad, bad
-    # the lane-major scan runs 8 waves per workgroup (2 per SIMD): it must stay within 256 VGPRs with room
+    # the lane-major scan runs 12 waves per workgroup (3 per SIMD): at most 168 VGPRs (512 / 3, in
+    # granules of 8), or the workgroup cannot launch
     scan = [v for n, v in k.items() if "cdc_scan_kernel" in n]
-    assert all(v["vgpr_count"] <= 192 for v in scan), scan
+    assert all(v["vgpr_count"] <= 168 for v in scan), scan
