@@ -180,6 +180,24 @@ int oxh_hash_files_text(oxh_ctx* ctx, const char* const* paths, uint64_t n, uint
  * mime/data-type decision of add.rs:809-810 then needs no third read of the file. */
 int oxh_hash_files_text_utf8(oxh_ctx* ctx, const char* const* paths, uint64_t n, uint64_t* out,
                              uint64_t* sizes, int32_t* status, uint64_t* counts, int32_t* is_utf8);
+
+/* The modified check of `oxen status` (core/v_latest/status.rs:710,734), add (add.rs:723) and
+ * checkout (branches.rs:524,548): util::fs::classify_modified_from_node_with_metadata
+ * (util/fs.rs:1580-1619) x n, behind LocalRepository::is_modified_from_node_with_metadata
+ * (model/repository/local_repository.rs:601-615). Per item, from the caller's walk: sizes[i] =
+ * metadata.len(), node_bytes[i] = node.num_bytes(), mtime_matched[i] = mtime_matches(...) (the
+ * caller's tolerance rule), node_hashes[2i..2i+1] = node.hash() (lo, hi).
+ *   sizes[i] != node_bytes[i]  -> modified[i] = 1, file not read;
+ *   else mtime_matched[i]      -> modified[i] = 0, file not read;
+ *   else modified[i] = (get_hash_given_metadata(path) != node.hash()); every such file is hashed in
+ *        one engine request (oxh_hash_files_meta semantics, read to EOF).
+ * The reference's metadata-hash comparison between the last two steps is a shortcut whose verdict
+ * the content comparison repeats (metadata is extracted from the content) and is not taken.
+ * status[i] = OXH_OK, or the read error of a file that had to be hashed (modified[i] = 0 then; the
+ * reference returns that error). status and n_hashed (the count of files read) may be NULL. */
+int oxh_files_modified(oxh_ctx* ctx, const char* const* paths, const uint64_t* sizes, const uint64_t* node_bytes,
+                       const uint8_t* mtime_matched, const uint64_t* node_hashes, uint64_t n, uint8_t* modified,
+                       int32_t* status, uint64_t* n_hashed);
 /* Device-resident is_utf8 sniff: d_flags[i] (int32) for item i of the arena (first 4 KiB). */
 int oxh_utf8_prefix_device(const void* d_arena, const uint64_t* d_offsets, const uint64_t* d_lens, uint64_t n,
                            int32_t* d_flags, void* stream);

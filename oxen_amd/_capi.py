@@ -53,6 +53,7 @@ SIGNATURES = {
     "oxh_hash_files_text": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64, _u64p, _u64p, _i32p, _u64p]),
     "oxh_xxh3_128_text_batch_device": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
     "oxh_hash_files_text_utf8": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64, _u64p, _u64p, _i32p, _u64p, _i32p]),
+    "oxh_files_modified": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64p, _u64p, _vp, _u64p, _u64, _vp, _i32p, _u64p]),
     "oxh_utf8_prefix_device": (_int, [_vp, _vp, _vp, _u64, _vp, _vp]),
     "oxh_combined_hash_device": (_int, [_vp, _vp, _u64, _vp, _vp]),
     "oxh_hash_streams": (_int, [_vp, _vp, _u64p, _u64p, _u64, _u64p]),

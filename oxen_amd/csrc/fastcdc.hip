@@ -647,13 +647,23 @@ __global__ __launch_bounds__(64) void cdc_fixup_kernel(CdcFiles f, CdcParams prm
     }
 }
 
-// F3c: exclusive prefix of the per-section counts (one block; n_sec is ~ bytes / 512 KiB).
+// F3c: exclusive prefix of the per-section counts (one block; n_sec is ~ bytes / 512 KiB). Every
+// thread owns a run of `per` counts (a multiple of 4, so the run starts 16-B aligned: count is a
+// 256-B aligned scratch part) and sums it with independent 16-byte loads; one load per count, each
+// waiting on the one before through the running sum, took 0.43 ms for C5's 262 144 sections.
 __global__ __launch_bounds__(1024) void cdc_prefix_kernel(CdcStitch s, uint64_t n_sec) {
     __shared__ uint64_t part[1024];
-    const uint64_t per = (n_sec + 1023) / 1024;
-    const uint64_t b = threadIdx.x * per, e = b + per < n_sec ? b + per : n_sec;
-    uint64_t sum = 0;
-    for (uint64_t i = b; i < e; ++i) sum += s.count[i];
+    const uint64_t per = ((n_sec + 1023) / 1024 + 3) & ~3ull;
+    const uint64_t b = (uint64_t)threadIdx.x * per < n_sec ? (uint64_t)threadIdx.x * per : n_sec;
+    const uint64_t e = b + per < n_sec ? b + per : n_sec;
+    const uint4* __restrict__ c4 = (const uint4*)s.count;
+    uint64_t sum = 0, i = b;
+#pragma unroll 8
+    for (; i + 4 <= e; i += 4) {
+        const uint4 v = c4[i >> 2];
+        sum += (uint64_t)v.x + v.y + v.z + v.w;
+    }
+    for (; i < e; ++i) sum += s.count[i];
     part[threadIdx.x] = sum;
     __syncthreads();
     for (int o = 1; o < 1024; o <<= 1) {
@@ -663,7 +673,18 @@ __global__ __launch_bounds__(1024) void cdc_prefix_kernel(CdcStitch s, uint64_t 
         __syncthreads();
     }
     uint64_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-    for (uint64_t i = b; i < e; ++i) {
+    // four counts per 16-byte load, four bases per two 16-byte stores (out_base + b is 32-B aligned)
+    ulonglong2* __restrict__ o2 = (ulonglong2*)s.out_base;
+    i = b;
+#pragma unroll 4
+    for (; i + 4 <= e; i += 4) {
+        const uint4 v = c4[i >> 2];
+        const uint64_t r1 = run + v.x, r2 = r1 + v.y, r3 = r2 + v.z;
+        o2[i >> 1] = make_ulonglong2(run, r1);
+        o2[(i >> 1) + 1] = make_ulonglong2(r2, r3);
+        run = r3 + v.w;
+    }
+    for (; i < e; ++i) {
         s.out_base[i] = run;
         run += s.count[i];
     }

@@ -1867,6 +1867,41 @@ int oxh_hash_files_text_utf8(oxh_ctx* c, const char* const* paths, uint64_t n, u
     return hash_files_impl(c, paths, n, out, sizes, status, counts, nullptr, is_utf8);
 }
 
+// util::fs::classify_modified_from_node_with_metadata (util/fs.rs:1580-1619) x n: the size and mtime
+// verdicts are decided on the host from what the caller's walk holds; only the items that reach the
+// content-hash comparison are read, all of them in ONE engine request (oxh_hash_files_meta semantics).
+int oxh_files_modified(oxh_ctx* c, const char* const* paths, const uint64_t* sizes, const uint64_t* node_bytes,
+                       const uint8_t* mtime_matched, const uint64_t* node_hashes, uint64_t n, uint8_t* modified,
+                       int32_t* status, uint64_t* n_hashed) {
+    if (!c || (n && (!paths || !sizes || !node_bytes || !mtime_matched || !node_hashes || !modified)))
+        return fail(OXH_ERR_INVALID, "bad arguments");
+    std::vector<uint64_t> idx;
+    for (uint64_t i = 0; i < n; ++i) {
+        modified[i] = sizes[i] != node_bytes[i] ? 1 : 0;  // fs.rs:1589-1592: no hashing needed
+        if (status) status[i] = OXH_OK;
+        if (!modified[i] && !mtime_matched[i]) idx.push_back(i);  // fs.rs:1595-1597: a matched mtime is trusted
+    }
+    if (n_hashed) *n_hashed = idx.size();
+    if (idx.empty()) return OXH_OK;
+    const uint64_t m = idx.size();
+    std::vector<const char*> p(m);
+    std::vector<uint64_t> ms(m), out(2 * m);
+    std::vector<int32_t> st(m, OXH_OK);
+    for (uint64_t k = 0; k < m; ++k) p[k] = paths[idx[k]], ms[k] = sizes[idx[k]];
+    const int rc = hash_files_impl(c, p.data(), m, out.data(), nullptr, st.data(), nullptr, nullptr, nullptr, ms.data());
+    if (rc) return rc;
+    for (uint64_t k = 0; k < m; ++k) {
+        const uint64_t i = idx[k];
+        if (st[k] != OXH_OK) {  // the reference returns the read error for this path
+            if (status) status[i] = st[k];
+            continue;
+        }
+        // fs.rs:1616-1618: node.hash() against get_hash_given_metadata(path, metadata)
+        modified[i] = (out[2 * k] != node_hashes[2 * i] || out[2 * k + 1] != node_hashes[2 * i + 1]) ? 1 : 0;
+    }
+    return OXH_OK;
+}
+
 namespace {
 
 // mkdir -p (std::fs::create_dir_all)

@@ -131,6 +131,47 @@ def hash_files_given_metadata_128bit(paths: Sequence[str], meta_sizes: Sequence[
                                                 status.ctypes.data_as(_capi._i32p)), "oxh_hash_files_meta")
     return _u128_list(out, status), [int(s) for s in sizes], [int(s) for s in status]
 
+
+def files_modified(paths: Sequence[str], sizes: Sequence[int], node_bytes: Sequence[int],
+                   mtime_matched: Sequence[bool], node_hashes: Sequence[int],
+                   ctx: Optional[_capi.Context] = None):
+    """`classify_modified_from_node_with_metadata` (util/fs.rs:1580-1619) over many working-tree files
+    (oxh_files_modified): the modified check `oxen status` runs per tracked file
+    (core/v_latest/status.rs:710,734). sizes = the walk's metadata.len(), node_bytes / node_hashes =
+    the committed FileNode's num_bytes / hash (u128), mtime_matched = the caller's mtime verdict.
+    Returns (modified, status, n_hashed): only files with an equal size and a drifted mtime are read,
+    all in one GPU pass; status[i] != 0 is that file's read error (the reference returns it)."""
+    ctx = ctx or default_context()
+    n = len(paths)
+    if not (len(sizes) == len(node_bytes) == len(mtime_matched) == len(node_hashes) == n):
+        raise _capi.OxenError("files_modified: argument lengths differ", _capi.OXH_ERR_INVALID)
+    if n == 0:
+        return [], [], 0
+    arr = (ctypes.c_char_p * n)(*[os.fsencode(str(p)) for p in paths])
+    sz = np.ascontiguousarray(sizes, dtype=np.uint64)
+    nb = np.ascontiguousarray(node_bytes, dtype=np.uint64)
+    mm = np.ascontiguousarray([1 if m else 0 for m in mtime_matched], dtype=np.uint8)
+    nh = np.array([(int(h) & 0xFFFFFFFFFFFFFFFF, int(h) >> 64) for h in node_hashes], dtype=np.uint64).reshape(n, 2)
+    modified = np.zeros(n, dtype=np.uint8)
+    status = np.zeros(n, dtype=np.int32)
+    hashed = (ctypes.c_uint64 * 1)()
+    _capi.check(_capi.lib().oxh_files_modified(ctx.handle, arr, sz.ctypes.data_as(_capi._u64p),
+                                               nb.ctypes.data_as(_capi._u64p), mm.ctypes.data,
+                                               nh.ctypes.data_as(_capi._u64p), n, modified.ctypes.data,
+                                               status.ctypes.data_as(_capi._i32p), hashed), "oxh_files_modified")
+    return [bool(m) for m in modified], [int(s) for s in status], int(hashed[0])
+
+
+def classify_modified_from_node_with_metadata(path, node_num_bytes: int, node_hash: int,
+                                              metadata: os.stat_result, mtime_matched: bool) -> bool:
+    """util/fs.rs:1580-1619 for one file (the batched form is files_modified); a read error raises
+    OxenError like the reference's `?` on get_hash_given_metadata."""
+    modified, status, _ = files_modified([path], [metadata.st_size], [node_num_bytes], [mtime_matched], [node_hash])
+    if status[0] != 0:
+        raise OxenError("Could not read file for hashing", _capi.OXH_ERR_IO)
+    return modified[0]
+
+
 def add_files(paths: Sequence[str], versions_root: str, ctx: Optional[_capi.Context] = None):
     """Fused hash + version-store publish (oxh_add_files): returns (digests, sizes, status, stored).
     stored[i] is True when the blob {versions_root}/{hex[:2]}/{hex[2:]}/data was written now."""

@@ -756,6 +756,70 @@ def test_hash_files_given_metadata(oracle_lib, tmp_path, cuda):
     assert d[-2] is None and d[-1] is None
 
 
+def test_files_modified_status_check(oracle_lib, tmp_path, cuda):
+    """oxh_files_modified = classify_modified_from_node_with_metadata (util/fs.rs:1580-1619) per
+    tracked file, against that function restated here over oracle digests: size differs -> modified
+    (not read); mtime matched -> clean (not read); else content hash vs node hash. Covers edited files
+    of the same size, untouched files with a drifted mtime, empty files, a file larger than a staging
+    slot, a file removed after the walk and a directory (read errors: status != 0)."""
+    from oxen_amd import _capi, hasher
+    from oxen_amd.workloads import splitmix_bytes
+
+    rng = np.random.default_rng(7)
+    blobs = [splitmix_bytes(300 + k, 0, int(s)).tobytes() for k, s in enumerate(rng.integers(0, 200_000, 300))]
+    blobs += [b"", splitmix_bytes(9, 0, (3 << 20) + 5).tobytes()]  # empty; larger than the 1 MiB staging slot
+    paths = []
+    for k, b in enumerate(blobs):
+        p = tmp_path / f"f{k}.bin"
+        p.write_bytes(b)
+        paths.append(str(p))
+    node_hashes = [oracle_lib.xxh3_128_int(b) for b in blobs]  # the committed FileNode hashes
+    node_bytes = [len(b) for b in blobs]
+    mtime_matched = [bool(x) for x in rng.integers(0, 2, len(blobs))]
+    mtime_matched[-1] = mtime_matched[-2] = False
+    # edit the working tree: same-size rewrites, grown files, shrunk files
+    for k in range(0, len(blobs), 3):
+        b = bytearray(blobs[k])
+        if b:
+            b[int(rng.integers(0, len(b)))] ^= 0x5A
+        open(paths[k], "wb").write(bytes(b))
+    for k in range(1, len(blobs) - 2, 17):
+        open(paths[k], "ab").write(b"+")
+    mtime_matched[-1] = False
+    big = bytearray(blobs[-1])
+    big[-1] ^= 1
+    open(paths[-1], "wb").write(bytes(big))
+    sizes = [os.stat(p).st_size for p in paths]
+    # a file removed after the walk and a directory, both with a size equal to the node's
+    os.mkdir(tmp_path / "adir")
+    paths += [str(tmp_path / "gone.bin"), str(tmp_path / "adir")]
+    sizes += [11, 4096]
+    node_bytes += [11, 4096]
+    node_hashes += [1, 2]
+    mtime_matched += [False, False]
+
+    def want_of(i):
+        if sizes[i] != node_bytes[i]:
+            return True, 0, False
+        if mtime_matched[i]:
+            return False, 0, False
+        try:
+            data = open(paths[i], "rb").read()
+        except OSError:
+            return False, 1, True
+        return oracle_lib.xxh3_128_int(data) != node_hashes[i], 0, True
+
+    want = [want_of(i) for i in range(len(paths))]
+    with _capi.Context(0, staging_bytes=1 << 20) as c:
+        modified, status, n_hashed = hasher.files_modified(paths, sizes, node_bytes, mtime_matched, node_hashes, c)
+        assert hasher.files_modified([], [], [], [], [], c) == ([], [], 0)
+    assert modified == [w[0] for w in want]
+    assert [s != 0 for s in status] == [w[1] != 0 for w in want]
+    assert n_hashed == sum(w[2] for w in want)
+    assert any(m for m, w in zip(modified, want) if w[2]) and any(not m for m, w in zip(modified, want) if w[2])
+    assert modified[-3] is True  # the oversize file with one changed byte
+
+
 @pytest.mark.parametrize("mode", ["short", "packed", "auto"])
 def test_k1_many_ragged_items(cuda, oracle_lib, mode):
     """Many ragged, byte-packed items (FastCDC-chunk-like, with short-path items mixed in): the
