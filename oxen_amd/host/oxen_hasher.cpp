@@ -205,4 +205,47 @@ u128 Xxh3::digest128() const {
 void Xxh3::reset() { check(oxh_xxh3_stream_reset(s_), "oxh_xxh3_stream_reset"); }
 
 }  // namespace util::hasher
+
+namespace util::fs {
+
+std::vector<Modified> classify_modified_batch(const std::vector<TrackedFile>& files, oxh_ctx* ctx, uint64_t* n_hashed) {
+    ctx = ctx ? ctx : hasher::default_context();
+    const size_t n = files.size();
+    std::vector<const char*> cp(n);
+    std::vector<uint64_t> sizes(n), node_bytes(n), node_hashes(2 * n);
+    std::vector<uint8_t> mtime(n), modified(n);
+    std::vector<int32_t> status(n);
+    for (size_t i = 0; i < n; ++i) {
+        cp[i] = files[i].path.c_str();
+        sizes[i] = files[i].size;
+        node_bytes[i] = files[i].node_num_bytes;
+        node_hashes[2 * i] = (uint64_t)files[i].node_hash;
+        node_hashes[2 * i + 1] = (uint64_t)(files[i].node_hash >> 64);
+        mtime[i] = files[i].mtime_matched ? 1 : 0;
+    }
+    uint64_t hashed = 0;
+    check(oxh_files_modified(ctx, cp.data(), sizes.data(), node_bytes.data(), mtime.data(), node_hashes.data(), n,
+                             modified.data(), status.data(), &hashed),
+          "oxh_files_modified");
+    if (n_hashed) *n_hashed = hashed;
+    std::vector<Modified> r(n);
+    for (size_t i = 0; i < n; ++i) {
+        r[i].modified = modified[i] != 0;
+        if (status[i] != OXH_OK) {
+            r[i].ok = false;
+            r[i].error = "Could not read file for hashing";  // hasher.rs:136-139
+        }
+    }
+    return r;
+}
+
+bool classify_modified_from_node_with_metadata(const std::string& path, uint64_t node_num_bytes, u128 node_hash,
+                                               const struct stat& metadata, bool mtime_matched) {
+    const std::vector<Modified> r =
+        classify_modified_batch({TrackedFile{path, (uint64_t)metadata.st_size, node_num_bytes, node_hash, mtime_matched}});
+    if (!r[0].ok) throw OxenError::basic_str(r[0].error, OXH_ERR_IO);
+    return r[0].modified;
+}
+
+}  // namespace util::fs
 }  // namespace liboxen

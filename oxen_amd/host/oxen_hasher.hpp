@@ -154,4 +154,31 @@ class HashingWriter {
 };
 
 }  // namespace util::hasher
+
+namespace util::fs {
+
+// One tracked working-tree file as `oxen status`'s walk holds it (core/v_latest/status.rs:690-745):
+// metadata.len(), the committed FileNode's num_bytes and hash, and the caller's mtime verdict
+// (LocalRepository::mtime_matches, model/repository/local_repository.rs:601-615).
+struct TrackedFile {
+    std::string path;
+    uint64_t size = 0;
+    uint64_t node_num_bytes = 0;
+    u128 node_hash = 0;
+    bool mtime_matched = false;
+};
+struct Modified {
+    bool ok = true;         // false: the file had to be hashed and could not be read
+    bool modified = false;
+    std::string error;
+};
+// classify_modified_from_node_with_metadata (util/fs.rs:1580-1619) x n through oxh_files_modified:
+// only files of an unchanged size with a drifted mtime are read, all in one GPU request.
+std::vector<Modified> classify_modified_batch(const std::vector<TrackedFile>& files, oxh_ctx* ctx = nullptr,
+                                              uint64_t* n_hashed = nullptr);
+// One file; a read error throws OxenError, as the reference's `?` does.
+bool classify_modified_from_node_with_metadata(const std::string& path, uint64_t node_num_bytes, u128 node_hash,
+                                               const struct stat& metadata, bool mtime_matched);
+
+}  // namespace util::fs
 }  // namespace liboxen

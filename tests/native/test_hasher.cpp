@@ -213,6 +213,33 @@ static void long_stream() {
     CHECK(h.digest128() == hex("b5e9c1ad071b3e7fc779cfaa5e523818"));
 }
 
+// util::fs::classify_modified_from_node_with_metadata (util/fs.rs:1580-1619) over oxh_files_modified:
+// size differs -> modified without a read; matched mtime -> clean without a read; else content hash.
+static void modified_check(const std::string& golden) {
+    namespace fs = liboxen::util::fs;
+    const std::string hello = golden + "/data_test/text/hello.txt";  // 5 bytes, KAT below
+    const u128 h = hex("1bfd09d1a433fb78117b4c7b1583d16d");
+    std::vector<fs::TrackedFile> t = {
+        {hello, 5, 5, h, false},          // same content, drifted mtime: hashed, clean
+        {hello, 5, 5, h + 1, false},      // node hash differs: hashed, modified
+        {hello, 5, 5, h + 1, true},       // matched mtime is trusted: not read, clean
+        {hello, 5, 6, h, false},          // size differs: not read, modified
+        {golden + "/no/such/file", 3, 3, h, false},  // must be hashed, cannot be read
+    };
+    uint64_t hashed = 0;
+    const std::vector<fs::Modified> r = fs::classify_modified_batch(t, nullptr, &hashed);
+    CHECK(r.size() == 5 && hashed == 3);
+    CHECK(r[0].ok && !r[0].modified);
+    CHECK(r[1].ok && r[1].modified);
+    CHECK(r[2].ok && !r[2].modified);
+    CHECK(r[3].ok && r[3].modified);
+    CHECK(!r[4].ok && !r[4].modified && r[4].error == "Could not read file for hashing");
+    struct stat sb;
+    CHECK(stat(hello.c_str(), &sb) == 0 && !fs::classify_modified_from_node_with_metadata(hello, 5, h, sb, false));
+    CHECK(throws_oxen([&] { fs::classify_modified_from_node_with_metadata(golden + "/no/such/file", (uint64_t)sb.st_size, h, sb, false); },
+                      "Could not read file for hashing"));
+}
+
 int main(int argc, char** argv) {
     const std::string golden = argc > 1 ? argv[1] : "tests/golden";
     try {
@@ -222,6 +249,7 @@ int main(int argc, char** argv) {
         file_errors(golden);
         merkle_hash();
         long_stream();
+        modified_check(golden);
     } catch (const std::exception& e) {
         fprintf(stderr, "FAIL: unexpected exception: %s\n", e.what());
         ++g_fail;
