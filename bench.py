@@ -148,6 +148,9 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm); gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--dist", action="store_true",
+                    help="take the N>1 path (process group, pipelined RCCL gather) even at WORLD_SIZE=1: "
+                         "rehearses the multi-GPU step on a one-GPU box under torch.distributed.run")
     args = ap.parse_args()
 
     import torch
@@ -159,7 +162,8 @@ def main() -> None:
     ndev = max(1, torch.cuda.device_count())
     dev = torch.device(f"cuda:{local_rank % ndev}")
     torch.cuda.set_device(dev)
-    if world > 1:
+    multi = world > 1 or args.dist  # the distributed step (barriers, gather, max over ranks)
+    if multi:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -173,7 +177,7 @@ def main() -> None:
 
     if rank == 0:
         hb.build()
-    if world > 1:
+    if multi:
         dist.barrier()
     _capi.lib().oxh_set_kernel_variant(args.variant)
 
@@ -190,7 +194,7 @@ def main() -> None:
     # N > 1 over RCCL: each step's digest gather runs on the collective's stream while the next step
     # hashes into the other of two digest tables (shard.PipelinedGather: the gather of step k overlaps
     # the hash of k+1; a table is rewritten only after the gather that read it has finished)
-    pipe = PipelinedGather(n_items, world, dev) if world > 1 and args.backend == "nccl" else None
+    pipe = PipelinedGather(n_items, world, dev) if multi and args.backend == "nccl" else None
 
     def step():
         if pipe is not None:
@@ -198,7 +202,7 @@ def main() -> None:
             da.hash(local)
             return pipe.gather(b), local
         da.hash(out)
-        if world > 1:
+        if multi:
             return gather_digest_table(out.cpu(), counts), out  # gloo rehearsal: host tables
         return out, out
 
@@ -210,7 +214,7 @@ def main() -> None:
         step()
     drain()
     torch.cuda.synchronize()
-    if world > 1:
+    if multi:
         dist.barrier()
     torch.cuda.synchronize()
     ev0 = torch.cuda.Event(enable_timing=True)
@@ -224,7 +228,7 @@ def main() -> None:
     t_enq = time.perf_counter() - t0
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    if world > 1:
+    if multi:
         dist.barrier()
     torch.cuda.synchronize()
     gpu_s = ev0.elapsed_time(ev1) / 1e3
@@ -242,7 +246,7 @@ def main() -> None:
     log(f"[bench] rank {rank}: wall {wall * 1e3:.3f} ms, events {gpu_s * 1e3:.3f} ms, enqueue {t_enq * 1e3:.3f} ms, "
         f"kernel {kernel_s * 1e3:.4f} ms x {args.steps} = {kernel_s * args.steps * 1e3:.3f} ms")
     t = torch.tensor([elapsed, kernel_s], dtype=torch.float64, device=dev)
-    if world > 1:
+    if multi:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kernel_max = float(t[0]), float(t[1])
 
@@ -253,7 +257,7 @@ def main() -> None:
     result = None
     if rank == 0:
         digests = to_numpy_u64(last).reshape(-1, 2)
-        if world > 1:
+        if multi:
             assert table.shape[0] == n_items * world
             assert np.array_equal(to_numpy_u64(table[:n_items]).reshape(-1, 2), digests)
             # every rank's shard digests arrived: rank r's first item is regenerated and checked
@@ -282,13 +286,13 @@ def main() -> None:
             "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (splitmix64 byte stream, seed %d+rank), device-resident in HBM" % args.seed,
             "config": {"workload": desc, "items_per_gpu": n_items, "item_bytes": item_len,
-                       "bytes_per_gpu": bytes_per_rank, "parallelism": f"files sharded x{world}, RCCL all-gather of digests" if world > 1 else "single GPU",
+                       "bytes_per_gpu": bytes_per_rank, "parallelism": f"files sharded x{world}, RCCL all-gather of digests" if multi else "single GPU",
                        "kernel_variant": args.variant or "auto (8: 2-round ring, items > 16 KiB)"},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if multi:
         dist.barrier()
         dist.destroy_process_group()
 
