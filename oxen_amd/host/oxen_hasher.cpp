@@ -1,9 +1,13 @@
 // oxen_amd/host/oxen_hasher.cpp -- liboxen `util::hasher` mirror over the C ABI (see the header).
 #include "oxen_hasher.hpp"
 
+#include <errno.h>
+#include <fcntl.h>
 #include <unistd.h>
 
 #include <chrono>
+#include <cstring>
+#include <random>
 #include <cstdlib>
 #include <mutex>
 #include <thread>
@@ -247,5 +251,166 @@ bool classify_modified_from_node_with_metadata(const std::string& path, uint64_t
     return r[0].modified;
 }
 
+namespace {
+
+constexpr size_t kStreamingBufSize = 10 * 1024 * 1024;  // constants::STREAMING_BUF_SIZE (constants.rs:196)
+
+std::string parent_of(const std::string& p) {
+    const size_t k = p.find_last_of('/');
+    return k == std::string::npos ? std::string() : p.substr(0, k);
+}
+
+bool mkdir_all(const std::string& dir) {  // std::fs::create_dir_all
+    if (dir.empty()) return true;
+    struct stat sb;
+    if (stat(dir.c_str(), &sb) == 0) return S_ISDIR(sb.st_mode);
+    if (!mkdir_all(parent_of(dir))) return false;
+    return mkdir(dir.c_str(), 0755) == 0 || errno == EEXIST;
+}
+
+// AtomicTempFile (atomic_file.rs:54-159): `<target>.oxentmp.<random>` beside the target, unlinked
+// unless committed.
+class TempFile {
+   public:
+    explicit TempFile(const std::string& target) : target_(target) {
+        const size_t slash = target.find_last_of('/');
+        const std::string name = slash == std::string::npos ? target : target.substr(slash + 1);
+        if (name.empty())
+            throw OxenError::basic_str("Could not create file \"" + target + "\": target path has no filename component", OXH_ERR_IO);
+        const std::string parent = parent_of(target);
+        if (!mkdir_all(parent)) throw OxenError::basic_str("Could not create directory \"" + parent + "\"", OXH_ERR_IO);
+        static const char kAlnum[] = "0123456789ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz";
+        thread_local std::mt19937_64 rng{std::random_device{}()};
+        for (int attempt = 0; attempt < 64; ++attempt) {
+            std::string rnd(6, 'x');
+            for (char& c : rnd) c = kAlnum[rng() % (sizeof(kAlnum) - 1)];
+            path_ = (parent.empty() ? std::string() : parent + "/") + name + ".oxentmp." + rnd;
+            fd_ = open(path_.c_str(), O_CREAT | O_EXCL | O_WRONLY | O_CLOEXEC, 0600);
+            if (fd_ >= 0 || errno != EEXIST) break;
+        }
+        if (fd_ < 0) throw OxenError::basic_str("Could not create file \"" + path_ + "\": " + strerror(errno), OXH_ERR_IO);
+    }
+    ~TempFile() {
+        if (fd_ >= 0) close(fd_);
+        if (!committed_) unlink(path_.c_str());
+    }
+    TempFile(const TempFile&) = delete;
+    TempFile& operator=(const TempFile&) = delete;
+
+    void write_all(const uint8_t* p, size_t n) {
+        while (n) {
+            const ssize_t w = ::write(fd_, p, n);
+            if (w < 0 && errno == EINTR) continue;
+            if (w <= 0) throw OxenError::basic_str("Could not write file \"" + path_ + "\": " + strerror(errno), OXH_ERR_IO);
+            p += w;
+            n -= (size_t)w;
+        }
+    }
+    // sync_all, rename over the target, best-effort fsync of the parent (:116-159)
+    void commit() {
+        if (fsync(fd_) != 0) throw OxenError::basic_str("Could not sync file \"" + path_ + "\": " + strerror(errno), OXH_ERR_IO);
+        close(fd_);
+        fd_ = -1;
+        if (rename(path_.c_str(), target_.c_str()) != 0)
+            throw OxenError::basic_str("Could not rename file from \"" + path_ + "\" to \"" + target_ + "\": " + strerror(errno),
+                                       OXH_ERR_IO);
+        committed_ = true;
+        const std::string parent = parent_of(target_);
+        const int dfd = open(parent.empty() ? "." : parent.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+        if (dfd >= 0) {
+            (void)fsync(dfd);
+            close(dfd);
+        }
+    }
+
+   private:
+    std::string target_, path_;
+    int fd_ = -1;
+    bool committed_ = false;
+};
+
+OxenError hash_mismatch(const std::string& path, MerkleHash expected, MerkleHash actual) {  // error.rs:463-471
+    return OxenError(OxenError::Kind::HashMismatch,
+                     "Hash mismatch writing \"" + path + "\": expected " + expected.to_string() + ", got " + actual.to_string(),
+                     OXH_ERR_IO);
+}
+
+}  // namespace
+
+void AtomicFile::stream(const Reader& reader) {
+    TempFile tmp(target_);
+    std::optional<hasher::Xxh3> h;
+    if (verify_) h.emplace(ctx_);
+    std::vector<uint8_t> buf(kStreamingBufSize);
+    for (;;) {
+        const size_t k = reader(buf.data(), buf.size());
+        if (k == 0) break;
+        if (h) h->update(buf.data(), k);
+        tmp.write_all(buf.data(), k);
+    }
+    if (h) {
+        const MerkleHash actual(h->digest128());
+        if (actual != expected_) throw hash_mismatch(target_, expected_, actual);  // tmp unlinked
+    }
+    tmp.commit();
+}
+
+void AtomicFile::write(const void* data, size_t len) {
+    TempFile tmp(target_);
+    tmp.write_all((const uint8_t*)data, len);
+    if (verify_) {
+        const MerkleHash actual(hasher::hash_buffers_128bit({std::string_view((const char*)data, len)}, ctx_)[0]);
+        if (actual != expected_) throw hash_mismatch(target_, expected_, actual);
+    }
+    tmp.commit();
+}
+
 }  // namespace util::fs
+
+namespace storage {
+
+std::string LocalVersionStore::version_dir(const std::string& hash) const {
+    if (hash.size() < 3) throw OxenError::basic_str("invalid version hash \"" + hash + "\"", OXH_ERR_INVALID);
+    return root_ + "/" + hash.substr(0, 2) + "/" + hash.substr(2);
+}
+
+std::string LocalVersionStore::version_path(const std::string& hash) const { return version_dir(hash) + "/data"; }
+
+bool LocalVersionStore::version_exists(const std::string& hash) const {
+    struct stat sb;
+    return stat(version_path(hash).c_str(), &sb) == 0;
+}
+
+void LocalVersionStore::store_version(const std::string& hash, const void* data, size_t len) const {
+    if (version_exists(hash)) return;
+    util::fs::AtomicFile(version_path(hash), ctx_).with_hash(MerkleHash::from_str(hash)).write(data, len);
+}
+
+void LocalVersionStore::store_version_from_reader(const std::string& hash, const util::fs::AtomicFile::Reader& reader,
+                                                  uint64_t size) const {
+    (void)size;  // `_size` in the reference too
+    if (version_exists(hash)) return;
+    const MerkleHash expected = MerkleHash::from_str(hash);
+    util::fs::AtomicFile(version_path(hash), ctx_).with_hash(expected).stream(reader);
+}
+
+std::vector<std::string> LocalVersionStore::store_versions(const std::vector<std::string>& hashes,
+                                                           const std::vector<std::string_view>& datas) const {
+    if (hashes.size() != datas.size()) throw OxenError::basic_str("hashes and datas differ in length", OXH_ERR_INVALID);
+    const std::vector<u128> got = util::hasher::hash_buffers_128bit(datas, ctx_);  // one GPU pass
+    std::vector<std::string> err(hashes.size());
+    for (size_t i = 0; i < hashes.size(); ++i) {
+        try {
+            if (version_exists(hashes[i])) continue;
+            const MerkleHash expected = MerkleHash::from_str(hashes[i]);
+            if (MerkleHash(got[i]) != expected) throw util::fs::hash_mismatch(version_path(hashes[i]), expected, MerkleHash(got[i]));
+            util::fs::AtomicFile(version_path(hashes[i]), ctx_).write(datas[i].data(), datas[i].size());  // verified above
+        } catch (const OxenError& e) {
+            err[i] = e.what();
+        }
+    }
+    return err;
+}
+
+}  // namespace storage
 }  // namespace liboxen

@@ -180,5 +180,57 @@ std::vector<Modified> classify_modified_batch(const std::vector<TrackedFile>& fi
 bool classify_modified_from_node_with_metadata(const std::string& path, uint64_t node_num_bytes, u128 node_hash,
                                                const struct stat& metadata, bool mtime_matched);
 
+// util/fs/atomic_file.rs: AtomicFile with an expected hash -- verify-before-publish. Bytes go to an
+// AtomicTempFile sibling `<target>.oxentmp.<random>` (:54-159) while a GPU Xxh3 stream (oxh_xxh3_stream)
+// hashes them; on a digest other than the expected one the temp is unlinked and OxenError
+// HashMismatch is thrown (:396-431), else the temp's data is fsynced, renamed over the target and
+// the parent fsynced (commit, :116-159). Without with_hash nothing is hashed.
+class AtomicFile {
+   public:
+    // reads up to n bytes into buf, returns 0 at EOF, throws on error
+    using Reader = std::function<size_t(uint8_t* buf, size_t n)>;
+    explicit AtomicFile(std::string target, oxh_ctx* ctx = nullptr) : target_(std::move(target)), ctx_(ctx) {}
+    AtomicFile& with_hash(MerkleHash expected) {
+        expected_ = expected;
+        verify_ = true;
+        return *this;
+    }
+    void stream(const Reader& reader);          // AtomicFile::stream / stream_async (:271-318, :363-463)
+    void write(const void* data, size_t len);   // AtomicFile::write (:161-...)
+
+   private:
+    std::string target_;
+    oxh_ctx* ctx_;
+    MerkleHash expected_;
+    bool verify_ = false;
+};
+
 }  // namespace util::fs
+
+namespace storage {
+
+// storage/local.rs: LocalVersionStore's content-addressed writes, verified on the GPU.
+class LocalVersionStore {
+   public:
+    explicit LocalVersionStore(std::string root, oxh_ctx* ctx = nullptr) : root_(std::move(root)), ctx_(ctx) {}
+    std::string version_dir(const std::string& hash) const;   // {root}/{hash[..2]}/{hash[2..]} (:66-70)
+    std::string version_path(const std::string& hash) const;  // + /data (:72-75)
+    bool version_exists(const std::string& hash) const;       // (:259-261)
+    // (:123-139) skipped when the blob exists; the bytes must hash to `hash` (HashMismatch otherwise)
+    void store_version(const std::string& hash, const void* data, size_t len) const;
+    // (:104-121) streamed in STREAMING_BUF_SIZE (10 MiB) reads, verified as it streams
+    void store_version_from_reader(const std::string& hash, const util::fs::AtomicFile::Reader& reader,
+                                   uint64_t size) const;
+    // Many received blobs at once (pull / clone downloads, api/client/versions.rs): every buffer hashed
+    // in ONE batched GPU pass (oxh_hash_buffers), each verified blob published as store_version
+    // would; result i is empty on success, else the error store_version would have thrown.
+    std::vector<std::string> store_versions(const std::vector<std::string>& hashes,
+                                            const std::vector<std::string_view>& datas) const;
+
+   private:
+    std::string root_;
+    oxh_ctx* ctx_;
+};
+
+}  // namespace storage
 }  // namespace liboxen

@@ -1,0 +1,195 @@
+"""Verify-before-publish writes of liboxen's version store, with the content hash on the GPU.
+
+Mirrors `util::fs::atomic_file` (crates/liboxen/src/util/fs/atomic_file.rs) -- `AtomicFile::with_hash`
++ `stream` / `stream_async` / `write` -- and the content-addressed writes of `LocalVersionStore`
+(storage/local.rs:104-139): bytes go to an `AtomicTempFile` sibling `<target>.oxentmp.<random>`
+(:54-159) while a GPU `Xxh3` stream hashes them; a digest other than the expected one unlinks the
+temp and raises `HashMismatchError` (:396-431, error.rs:463-471), otherwise the temp's data is
+fsynced, renamed over the target and the parent directory fsynced (:116-159). There is no CPU
+hashing here: every digest comes from the HIP kernels through the C ABI.
+
+`LocalVersionStore.store_versions` is the batched receive (pull / clone downloads,
+api/client/versions.rs): every buffer hashed in ONE GPU pass, then each verified blob published.
+"""
+from __future__ import annotations
+
+import os
+import secrets
+import string
+from typing import Optional, Sequence
+
+from . import _capi, hasher
+from ._capi import OxenError
+
+STREAMING_BUF_SIZE = 10 * 1024 * 1024  # constants.rs:196
+ATOMIC_TEMP_INFIX = ".oxentmp."        # atomic_file.rs:25
+VERSION_FILE_NAME = "data"
+
+
+class HashMismatchError(OxenError):
+    """OxenError::HashMismatch { path, expected, actual } (error.rs:463-471)."""
+
+    def __init__(self, path: str, expected: int, actual: int):
+        self.path, self.expected, self.actual = path, expected, actual
+        super().__init__(f'Hash mismatch writing "{path}": expected {expected:x}, got {actual:x}', _capi.OXH_ERR_IO)
+
+
+class _TempFile:
+    """AtomicTempFile (atomic_file.rs:54-159): unlinked unless committed."""
+
+    _ALNUM = string.ascii_letters + string.digits
+
+    def __init__(self, target: str):
+        name = os.path.basename(target)
+        if not name:
+            raise OxenError(f"Could not create file {target!r}: target path has no filename component", _capi.OXH_ERR_IO)
+        parent = os.path.dirname(target)
+        if parent:
+            os.makedirs(parent, exist_ok=True)
+        self.target = target
+        for _ in range(64):
+            rnd = "".join(secrets.choice(self._ALNUM) for _ in range(6))
+            self.path = os.path.join(parent, name + ATOMIC_TEMP_INFIX + rnd)
+            try:
+                self.fd = os.open(self.path, os.O_CREAT | os.O_EXCL | os.O_WRONLY | os.O_CLOEXEC, 0o600)
+                break
+            except FileExistsError:
+                continue
+        else:
+            raise OxenError(f"Could not create file {self.path!r}", _capi.OXH_ERR_IO)
+        self.committed = False
+
+    def write_all(self, data) -> None:
+        mv = memoryview(data).cast("B")
+        while mv.nbytes:
+            n = os.write(self.fd, mv)
+            mv = mv[n:]
+
+    def commit(self) -> None:
+        os.fsync(self.fd)
+        os.close(self.fd)
+        self.fd = -1
+        os.rename(self.path, self.target)
+        self.committed = True
+        try:  # best-effort parent fsync
+            dfd = os.open(os.path.dirname(self.target) or ".", os.O_RDONLY | os.O_DIRECTORY)
+            try:
+                os.fsync(dfd)
+            finally:
+                os.close(dfd)
+        except OSError:
+            pass
+
+    def discard(self) -> None:
+        if self.fd >= 0:
+            os.close(self.fd)
+            self.fd = -1
+        if not self.committed:
+            try:
+                os.unlink(self.path)
+            except FileNotFoundError:
+                pass
+
+
+class AtomicFile:
+    """AtomicFile::new(target)[.with_hash(expected)] (atomic_file.rs:161-463)."""
+
+    def __init__(self, target, ctx: Optional[_capi.Context] = None):
+        self.target = str(target)
+        self.expected: Optional[int] = None
+        self.ctx = ctx
+
+    def with_hash(self, expected: int) -> "AtomicFile":
+        self.expected = int(expected)
+        return self
+
+    def stream(self, reader) -> None:
+        """stream / stream_async: `reader.read(n)` (b"" at EOF) in STREAMING_BUF_SIZE pieces."""
+        tmp = _TempFile(self.target)
+        try:
+            h = hasher.Xxh3(self.ctx) if self.expected is not None else None
+            while True:
+                chunk = reader.read(STREAMING_BUF_SIZE)
+                if not chunk:
+                    break
+                if h is not None:
+                    h.update(chunk)
+                tmp.write_all(chunk)
+            if h is not None:
+                actual = h.digest128()
+                h.close()
+                if actual != self.expected:
+                    raise HashMismatchError(self.target, self.expected, actual)
+            tmp.commit()
+        finally:
+            tmp.discard()
+
+    def write(self, data: bytes) -> None:
+        tmp = _TempFile(self.target)
+        try:
+            tmp.write_all(data)
+            if self.expected is not None:
+                actual = hasher.hash_buffers_128bit([bytes(data)], self.ctx)[0]
+                if actual != self.expected:
+                    raise HashMismatchError(self.target, self.expected, actual)
+            tmp.commit()
+        finally:
+            tmp.discard()
+
+
+def _parse_hash(h: str) -> int:
+    """MerkleHash::from_str (merkle_hash.rs:54-61): u128 radix 16."""
+    try:
+        v = int(h, 16)
+    except ValueError:
+        raise OxenError(f"invalid digit found in string: {h!r}", _capi.OXH_ERR_INVALID) from None
+    if v >> 128:
+        raise OxenError("number too large to fit in target type", _capi.OXH_ERR_INVALID)
+    return v
+
+
+class LocalVersionStore:
+    """storage/local.rs: version paths and the verified content-addressed writes."""
+
+    def __init__(self, root_path, ctx: Optional[_capi.Context] = None):
+        self.root_path = str(root_path)
+        self.ctx = ctx
+
+    def version_dir(self, hash: str) -> str:  # :66-70
+        return os.path.join(self.root_path, hash[:2], hash[2:])
+
+    def version_path(self, hash: str) -> str:  # :72-75
+        return os.path.join(self.version_dir(hash), VERSION_FILE_NAME)
+
+    def version_exists(self, hash: str) -> bool:  # :259-261
+        return os.path.exists(self.version_path(hash))
+
+    def store_version(self, hash: str, data: bytes) -> None:  # :123-139
+        if self.version_exists(hash):
+            return
+        AtomicFile(self.version_path(hash), self.ctx).with_hash(_parse_hash(hash)).write(data)
+
+    def store_version_from_reader(self, hash: str, reader, size: int) -> None:  # :104-121
+        del size  # `_size` in the reference too
+        if self.version_exists(hash):
+            return
+        AtomicFile(self.version_path(hash), self.ctx).with_hash(_parse_hash(hash)).stream(reader)
+
+    def store_versions(self, hashes: Sequence[str], datas: Sequence[bytes]) -> list:
+        """Many received blobs: one batched GPU hash of every buffer, then each verified blob is
+        published as store_version would. Returns, per item, None or the OxenError it raised."""
+        if len(hashes) != len(datas):
+            raise OxenError("hashes and datas differ in length", _capi.OXH_ERR_INVALID)
+        got = hasher.hash_buffers_128bit(list(datas), self.ctx)
+        errs: list = [None] * len(hashes)
+        for i, (h, d) in enumerate(zip(hashes, datas)):
+            try:
+                if self.version_exists(h):
+                    continue
+                expected = _parse_hash(h)
+                if got[i] != expected:
+                    raise HashMismatchError(self.version_path(h), expected, got[i])
+                AtomicFile(self.version_path(h), self.ctx).write(d)  # verified above
+            except OxenError as e:
+                errs[i] = e
+        return errs

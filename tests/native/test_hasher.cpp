@@ -5,10 +5,15 @@
 //
 // Built by oxen_amd/build.py (g++ against liboxen_hasher.so + liboxen_hash.so); run by
 // tests/test_native_mirror.py on the GPU box. argv[1] = tests/golden. Exit status 0 = all passed.
+#include <dirent.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <cstdio>
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -240,6 +245,103 @@ static void modified_check(const std::string& golden) {
                       "Could not read file for hashing"));
 }
 
+static std::vector<std::string> list_dir(const std::string& d) {
+    std::vector<std::string> r;
+    if (DIR* dp = opendir(d.c_str())) {
+        while (dirent* e = readdir(dp))
+            if (strcmp(e->d_name, ".") && strcmp(e->d_name, "..")) r.push_back(e->d_name);
+        closedir(dp);
+    }
+    return r;
+}
+static std::string read_file(const std::string& p) {
+    std::string out;
+    if (FILE* f = fopen(p.c_str(), "rb")) {
+        char b[65536];
+        size_t k;
+        while ((k = fread(b, 1, sizeof b, f)) > 0) out.append(b, k);
+        fclose(f);
+    }
+    return out;
+}
+// a reader over a byte string, in pieces of at most `piece` bytes; throws after `fail_after` bytes
+struct StrReader {
+    std::string data;
+    size_t pos = 0, piece = 1 << 30, fail_after = (size_t)-1;
+    size_t operator()(uint8_t* buf, size_t n) {
+        if (pos >= fail_after) throw OxenError::basic_str("simulated read failure");
+        const size_t k = std::min({n, piece, data.size() - pos, fail_after - pos});
+        memcpy(buf, data.data() + pos, k);
+        pos += k;
+        return k;
+    }
+};
+
+// util/fs/atomic_file.rs tests (verified stream / write: commits on match, aborts on mismatch with
+// HashMismatch and nothing left behind, cleans up on read failure) and storage/version_store.rs's
+// verify_suite::assert_rejects_mismatched_content, over the GPU-verified mirror.
+static void verified_publish(const std::string& scratch) {
+    namespace fs = liboxen::util::fs;
+    using liboxen::storage::LocalVersionStore;
+    std::string payload;  // (0..50_000u32).flat_map(u32::to_le_bytes)
+    for (uint32_t i = 0; i < 50000; ++i) payload.append((const char*)&i, 4);
+    const MerkleHash want(hex("290ee6c54069340c8a3c8891ce6b2d9"));  // xxh3_128(payload), oracle + libxxhash
+    const MerkleHash bogus((u128)0xdeadbeefdeadbeefull << 64 | 0xdeadbeefdeadbeefull);
+    const std::string d1 = scratch + "/commit", d2 = scratch + "/abort", d3 = scratch + "/readfail", d4 = scratch + "/write";
+    for (const auto& d : {d1, d2, d3, d4}) mkdir(d.c_str(), 0755);
+
+    StrReader r1{payload, 0, 7777};
+    fs::AtomicFile(d1 + "/blob.bin").with_hash(want).stream(std::ref(r1));
+    CHECK(read_file(d1 + "/blob.bin") == payload && list_dir(d1).size() == 1);
+
+    StrReader r2{payload};
+    bool mism = false;
+    try {
+        fs::AtomicFile(d2 + "/blob.bin").with_hash(bogus).stream(std::ref(r2));
+    } catch (const OxenError& e) {
+        mism = e.kind() == OxenError::Kind::HashMismatch && strstr(e.what(), "expected deadbeefdeadbeefdeadbeefdeadbeef") &&
+               strstr(e.what(), "got 290ee6c54069340c8a3c8891ce6b2d9");
+    }
+    CHECK(mism && list_dir(d2).empty());
+
+    StrReader r3{payload, 0, 4096, 100000};
+    CHECK(throws_oxen([&] { fs::AtomicFile(d3 + "/blob.bin").with_hash(want).stream(std::ref(r3)); }, "simulated read failure"));
+    CHECK(list_dir(d3).empty());
+
+    CHECK(throws_oxen([&] { fs::AtomicFile(d4 + "/blob.bin").with_hash(bogus).write(payload.data(), payload.size()); }, "Hash mismatch"));
+    CHECK(list_dir(d4).empty());
+    fs::AtomicFile(d4 + "/blob.bin").with_hash(want).write(payload.data(), payload.size());
+    CHECK(read_file(d4 + "/blob.bin") == payload && list_dir(d4).size() == 1);
+
+    // verify_suite: DATA under WRONG_HASH is rejected by both content-addressed writes
+    const std::string data = "the quick brown fox jumps over the lazy dog";
+    const std::string wrong = "deadbeefdeadbeefdeadbeefdeadbeef", right = "e9a1932627d7f46d15c21eead63fa21f";
+    LocalVersionStore store(scratch + "/versions");
+    CHECK(hasher::hash_buffer(data.data(), data.size()) == right);
+    CHECK(throws_oxen([&] { store.store_version(wrong, data.data(), data.size()); }, "mismatch"));
+    CHECK(!store.version_exists(wrong));
+    StrReader r4{data};
+    CHECK(throws_oxen([&] { store.store_version_from_reader(wrong, std::ref(r4), data.size()); }, "mismatch"));
+    CHECK(!store.version_exists(wrong));
+    StrReader r5{data, 0, 5};
+    store.store_version_from_reader(right, std::ref(r5), data.size());
+    CHECK(store.version_exists(right) && read_file(store.version_path(right)) == data);
+    CHECK(store.version_path(right) == scratch + "/versions/e9/a1932627d7f46d15c21eead63fa21f/data");
+    store.store_version(right, "ignored: the blob exists", 24);  // local.rs:127-129
+    CHECK(read_file(store.version_path(right)) == data);
+
+    // batched receive: one GPU pass over every buffer
+    const std::vector<std::string> hs = {hasher::hash_buffer(payload.data(), payload.size()), wrong, right,
+                                         hasher::hash_buffer("", 0), hasher::hash_buffer(payload.data(), payload.size())};
+    const std::vector<std::string_view> ds = {payload, data, data, std::string_view(), payload};
+    const std::vector<std::string> err = store.store_versions(hs, ds);
+    CHECK(err.size() == 5 && err[0].empty() && err[1].find("Hash mismatch") != std::string::npos && err[2].empty() &&
+          err[3].empty() && err[4].empty());
+    CHECK(read_file(store.version_path(hs[0])) == payload && store.version_exists(hs[3]) &&
+          read_file(store.version_path(hs[3])).empty() && !store.version_exists(wrong));
+    CHECK(list_dir(store.version_dir(hs[0])).size() == 1);  // no .oxentmp. leftovers
+}
+
 int main(int argc, char** argv) {
     const std::string golden = argc > 1 ? argv[1] : "tests/golden";
     try {
@@ -250,6 +352,12 @@ int main(int argc, char** argv) {
         merkle_hash();
         long_stream();
         modified_check(golden);
+        char tmpl[] = "/tmp/oxh_native_XXXXXX";
+        const char* scratch = mkdtemp(tmpl);
+        if (!scratch) throw std::runtime_error("mkdtemp failed");
+        verified_publish(scratch);
+        const std::string rm = std::string("rm -rf ") + scratch;
+        if (system(rm.c_str()) != 0) fprintf(stderr, "could not remove %s\n", scratch);
     } catch (const std::exception& e) {
         fprintf(stderr, "FAIL: unexpected exception: %s\n", e.what());
         ++g_fail;
