@@ -113,14 +113,16 @@ __device__ __forceinline__ uint32_t min3_u32(uint32_t a, uint32_t b, uint32_t c)
 }
 
 // 16 bytes at p[pos .. pos+16) of a file of length flen as four little-endian words (zeros past the
-// end): one raw buffer load (gfx950 buffer loads take any alignment) instead of 16 dependent byte
-// loads -- the walk's latency is made of these.
+// end): one unaligned global_load_dwordx4 (gfx950 runs in unaligned-access mode) instead of 16
+// dependent byte loads -- the walk's latency is made of these. Not a buffer load: every lane of the
+// walk has its own address, and a buffer resource built from a per-lane pointer is not wave-uniform,
+// so the compiler wrapped each such load in a readfirstlane loop that issued it once per lane (64x;
+// the walk took 3.7 ms of C5 at 8 KiB chunks with it).
 __device__ __forceinline__ uint4 load16_file(const uint8_t* __restrict__ fbase, uint64_t pos, uint64_t flen) {
     if (pos >= flen) return make_uint4(0, 0, 0, 0);
     if (flen - pos >= 16) {
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(fbase + pos), (short)0, 16, 0x00020000);
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, 0u, 0, 0);
+        typedef unsigned int u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+        const u32x4u v = *(const u32x4u*)(fbase + pos);
         return make_uint4(v.x, v.y, v.z, v.w);
     }
     uint32_t w[4] = {0, 0, 0, 0};
@@ -477,15 +479,18 @@ __device__ uint64_t cdc_cut(const CdcFiles& f, const CdcParams& prm, uint64_t se
         h = (h << 1) + gear_of(gear, b);
         if ((h & (q < eS ? prm.mask_s : prm.mask_l)) == 0) return q;
     }
+    // [qs, eS) against mask_s, then [max(qs, eS), eL) against mask_l, through ONE first_cand site: the
+    // lanes of a wave in either range run it together, and the walk's code (and its register
+    // pressure) is half the size of two inlined copies
     const uint64_t qs = a0 + kHashSpan;
-    if (qs < eS) {
-        const uint64_t p = first_cand(f, prm, sec0, nsec_file, fbase, flen, cur, s + qs, s + eS, 1u, gear);
-        if (p < s + eS) return p - s;
-    }
-    const uint64_t ql = qs > eS ? qs : eS;
-    if (ql < eL) {
-        const uint64_t p = first_cand(f, prm, sec0, nsec_file, fbase, flen, cur, s + ql, s + eL, 2u, gear);
-        if (p < s + eL) return p - s;
+#pragma unroll 1
+    for (uint32_t flag = 1; flag <= 2; ++flag) {
+        const uint64_t lo = flag == 1 ? qs : (qs > eS ? qs : eS);
+        const uint64_t hi = flag == 1 ? eS : eL;
+        if (lo < hi) {
+            const uint64_t p = first_cand(f, prm, sec0, nsec_file, fbase, flen, cur, s + lo, s + hi, flag, gear);
+            if (p < s + hi) return p - s;
+        }
     }
     return rem;
 }
@@ -507,14 +512,17 @@ __global__ __launch_bounds__(256) void cdc_walk_kernel(CdcFiles f, CdcParams prm
     uint32_t* out = f.spec + sec * prm.speccap;
     // warm up over the `warmup` bytes before the section (unrecorded): a walk started anywhere meets
     // the true walk within a few chunks, so the recorded starts are almost always the true ones
+    // One loop for the warm-up and the recorded part (one cdc_cut site): each lane moves from one to
+    // the other on its own, instead of the wave finishing every lane's warm-up first.
     uint64_t s = sec_start > prm.warmup ? sec_start - prm.warmup : 0;
     CandCursor cur{64 * sec0 + s / prm.unit, 0};
-    while (s < sec_start) s += cdc_cut(f, prm, sec0, nsec_file, fbase, flen, s, cur, lds_gear);
     uint32_t n = 0;
     while (true) {
-        if (n < prm.speccap) out[n] = (uint32_t)(s - sec_start);
-        ++n;
-        if ((s >= sec_end && n > 1) || s >= flen) break;
+        if (s >= sec_start) {
+            if (n < prm.speccap) out[n] = (uint32_t)(s - sec_start);
+            ++n;
+            if ((s >= sec_end && n > 1) || s >= flen) break;
+        }
         s += cdc_cut(f, prm, sec0, nsec_file, fbase, flen, s, cur, lds_gear);
     }
     f.spec_cnt[sec] = n;
