@@ -323,7 +323,7 @@ struct CandCursor {
     uint32_t rsec_idx = 0xFFFFFFFFu;  // the last resolved group (unit + idx) and its flags
     uint64_t rsec = ~0ull;
     uint64_t occ_sec = ~0ull, occ = 0;  // the occupancy mask of section occ_sec (F1's ballot)
-    uint32_t rfs = 0, rfl = 0;
+    uint32_t rflag = 0, rbits = 0;  // the flag the resolved group's bits are for, and the bits
 };
 
 // Full-window hash test of positions [lo, hi) (all inside one file, lo >= 47) by direct byte scan:
@@ -346,24 +346,35 @@ __device__ uint64_t scan_bytes(const uint8_t* __restrict__ fbase, uint64_t lo, u
     return hi;
 }
 
-// Exact mask_s / mask_l flags (bit j = position g + j) of a candidate group: roll the 16 bytes F1
-// stored with it from the hash F1 recorded before it (no re-read of the file: the walk is
-// latency-bound and the lists stay in the L2 / Infinity Cache).
-__device__ __forceinline__ void resolve_group(const uint4 v, uint64_t g, uint64_t H, uint64_t flen,
-                                              const CdcParams& prm, const uint64_t* __restrict__ gear,
-                                              uint32_t& fs, uint32_t& fl) {
-    fs = fl = 0;
+// Exact flags of a candidate group for ONE mask (bit j: position g + j has (hash & mask) == 0): roll
+// the 16 bytes F1 stored with it from the hash F1 recorded before it (no re-read of the file: the
+// walk is latency-bound and the lists stay in the L2 / Infinity Cache). The tests fold into one
+// minimum first; the bits are assembled only when some position hit (always for mask_l, whose bits
+// are the ones F1 filtered on; rarely for the stricter mask_s).
+__device__ __forceinline__ uint32_t and_or_v(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ uint32_t resolve_group(const uint4 v, uint64_t g, uint64_t H, uint64_t flen, uint64_t mask,
+                                                  const uint64_t* __restrict__ gear) {
+    const uint32_t mlo = (uint32_t)mask, mhi = (uint32_t)(mask >> 32);
     uint64_t h = H;
-    const uint32_t live = flen - g < 16 ? (uint32_t)(flen - g) : 16u;
+    uint32_t t[16];
+    uint32_t z = 0xFFFFFFFFu;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         h = (h << 1) + gear_of(gear, byte_of(v, j));
-        fs |= ((h & prm.mask_s) == 0 ? 1u : 0u) << j;
-        fl |= ((h & prm.mask_l) == 0 ? 1u : 0u) << j;
+        t[j] = and_or_v((uint32_t)h, mlo, (uint32_t)(h >> 32) & mhi);
+        if (j & 1) z = min3_u32(z, t[j - 1], t[j]);
     }
-    const uint32_t keep = live >= 16 ? 0xFFFFu : ((1u << live) - 1u);
-    fs &= keep;
-    fl &= keep;
+    uint32_t bits = 0;
+    if (z == 0) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) bits |= (t[j] == 0 ? 1u : 0u) << j;
+    }
+    const uint32_t live = flen - g < 16 ? (uint32_t)(flen - g) : 16u;
+    return live >= 16 ? bits : bits & ((1u << live) - 1u);
 }
 
 // First position in [lo, hi) (file-relative) whose full-window hash matches `flag` (1: mask_s,
@@ -420,12 +431,13 @@ __device__ uint64_t first_cand(const CdcFiles& f, const CdcParams& prm, uint64_t
             const uint64_t g = sec_start + (e >> kEntryShift) * 16;
             if (g >= hi) return hi;
             if (g + 16 > lo) {  // the group overlaps [lo, hi)
-                if (cur.rsec != cur.sec || cur.rsec_idx != cur.idx) {
-                    resolve_group(bv, g, e & kEntryHash, flen, prm, gear, cur.rfs, cur.rfl);
+                if (cur.rsec != cur.sec || cur.rsec_idx != cur.idx || cur.rflag != flag) {
+                    cur.rbits = resolve_group(bv, g, e & kEntryHash, flen, flag == 1 ? prm.mask_s : prm.mask_l, gear);
                     cur.rsec = cur.sec;
                     cur.rsec_idx = cur.idx;
+                    cur.rflag = flag;
                 }
-                uint32_t m = flag == 1 ? cur.rfs : cur.rfl;
+                uint32_t m = cur.rbits;
                 if (lo > g) m &= ~0u << (uint32_t)(lo - g);                  // positions >= lo
                 if (hi < g + 16) m &= (1u << (uint32_t)(hi - g)) - 1u;       // positions < hi
                 if (m) return g + (uint64_t)__builtin_ctz(m);
@@ -466,18 +478,40 @@ __device__ uint64_t cdc_cut(const CdcFiles& f, const CdcParams& prm, uint64_t se
     else if (rem < center) center = rem;
     const uint64_t a0 = (prm.min / 2) * 2, eS = (center / 2) * 2, eL = (rem / 2) * 2;
     // truncated window: the hash restarts from 0 at a0
-    uint64_t h = 0;
-    const uint64_t tend = a0 + kHashSpan < eL ? a0 + kHashSpan : eL;
     // the 47 bytes from a0: three 16-byte loads issued together
     const uint4 t0 = load16_file(fbase, s + a0, flen), t1 = load16_file(fbase, s + a0 + 16, flen),
                 t2 = load16_file(fbase, s + a0 + 32, flen);
+    bool exact = true;
+    if (a0 + kHashSpan <= eS) {
+        // Common case: all 47 positions test mask_s. Roll them with no branch per position (the
+        // table reads do not depend on the hash, so they go out ahead) and fold the tests into one
+        // minimum; only lanes with a zero test (2^-popcount(mask_s) per position) run the exact loop
+        // below to find the first one. The per-position branch with two masks cost ~16 VALU and an
+        // LDS round trip per position.
+        const uint32_t mlo = (uint32_t)prm.mask_s, mhi = (uint32_t)(prm.mask_s >> 32);
+        uint64_t hh = 0;
+        uint32_t anyz = 0xFFFFFFFFu, tprev = 0xFFFFFFFFu;
 #pragma unroll
-    for (int k = 0; k < kHashSpan; ++k) {
-        const uint64_t q = a0 + (uint64_t)k;
-        if (q >= tend) break;
-        const uint32_t b = k < 16 ? byte_of(t0, k) : k < 32 ? byte_of(t1, k - 16) : byte_of(t2, k - 32);
-        h = (h << 1) + gear_of(gear, b);
-        if ((h & (q < eS ? prm.mask_s : prm.mask_l)) == 0) return q;
+        for (int k = 0; k < kHashSpan; ++k) {
+            const uint32_t b = k < 16 ? byte_of(t0, k) : k < 32 ? byte_of(t1, k - 16) : byte_of(t2, k - 32);
+            hh = (hh << 1) + gear_of(gear, b);
+            const uint32_t t = and_or((uint32_t)hh, mlo, (uint32_t)(hh >> 32) & mhi);
+            if (k & 1) anyz = min3_u32(anyz, tprev, t);
+            else tprev = t;
+        }
+        exact = min_u32(anyz, tprev) == 0;
+    }
+    if (exact) {
+        uint64_t h = 0;
+        const uint64_t tend = a0 + kHashSpan < eL ? a0 + kHashSpan : eL;
+#pragma unroll
+        for (int k = 0; k < kHashSpan; ++k) {
+            const uint64_t q = a0 + (uint64_t)k;
+            if (q >= tend) break;
+            const uint32_t b = k < 16 ? byte_of(t0, k) : k < 32 ? byte_of(t1, k - 16) : byte_of(t2, k - 32);
+            h = (h << 1) + gear_of(gear, b);
+            if ((h & (q < eS ? prm.mask_s : prm.mask_l)) == 0) return q;
+        }
     }
     // [qs, eS) against mask_s, then [max(qs, eS), eL) against mask_l, through ONE first_cand site: the
     // lanes of a wave in either range run it together, and the walk's code (and its register
