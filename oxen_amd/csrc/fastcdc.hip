@@ -228,18 +228,32 @@ __global__ __launch_bounds__(64 * WAVES) void cdc_scan_kernel(CdcFiles f, CdcPar
     }
     // round t of every unit into this wave's slot (DMA k, lane 8m + j: unit 8k + m, rotated piece)
     const int dm = lane >> 3, dj = lane & 7;
-    auto dma_round = [&](uint32_t t) {
+    // the round moves the resource (SGPR arithmetic: its base by 128 B, its size down by as much) rather
+    // than the 8 per-lane offsets (8 VALU adds per round); the whole offset stays in the VGPR operand,
+    // so the range check sees it: a piece at or past the section's last whole 16 bytes reads zeros
+    uint32_t voff[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const uint32_t r = 8 * k + dm;
-            const uint32_t piece = (uint32_t)(dj - (int)((r >> 1) & 7)) & 7;
-            // the whole offset in the VGPR operand, so the range check sees it
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(slot + 64 * k), 16,
-                                                     pre + r * unit + t * 128 + 16 * piece, 0, 0, kScanDmaAux);
-        }
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t r = 8 * k + dm;
+        voff[k] = pre + r * unit + 16 * ((uint32_t)(dj - (int)((r >> 1) & 7)) & 7);
+    }
+    auto dma_round = [&](uint32_t t) {
+        // wave-uniform by construction; readfirstlane keeps the compiler from treating the resource
+        // as per-lane (which would wrap every DMA in a readfirstlane loop)
+        const int left = __builtin_amdgcn_readfirstlane((int)(pre + full16 > t * 128 ? pre + full16 - t * 128 : 0u));
+        const uint64_t a = (uint64_t)(base - pre) + (uint64_t)t * 128;
+        const uint64_t au = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32);
+        const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc((void*)au, (short)0, left, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (__attribute__((address_space(3))) void*)(slot + 64 * k), 16, voff[k],
+                                                     0, 0, kScanDmaAux);
     };
     dma_round(0);
     const int rot = (lane >> 1) & 7;
+    // the round (if any) whose 128 B hold the section's partial last 16 bytes, for this lane
+    const uint32_t t_part = (sec_len != full16 && us <= full16 && full16 < us + unit) ? (full16 - us) >> 7 : 0xFFFFFFFFu;
 #pragma unroll 1
     for (uint32_t t = 0; t < rounds; ++t) {
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this round's DMA has landed
@@ -253,7 +267,7 @@ __global__ __launch_bounds__(64 * WAVES) void cdc_scan_kernel(CdcFiles f, CdcPar
         if (t + 1 < rounds) dma_round(t + 1);
         const uint32_t rb = us + t * 128;  // section-relative start of this lane's 128 B
         // the section's partial last 16 B (outside the resource): byte loads, in the one lane that has it
-        if (sec_len != full16 && rb <= full16 && full16 < rb + 128) {
+        if (t == t_part) {
             const int pi = (int)((full16 - rb) >> 4);
             uint32_t pw[4] = {0, 0, 0, 0};
 #pragma unroll
