@@ -9,6 +9,9 @@ Writes the C3 image repo (benchmark/generate_image_repo.py layout: 200 000 noise
              ring, overlapped with K1 on the compute stream) -> D2H digests
   cpu_ref    the reference's per-file loop restated in C (oracle/): stat, read whole file, one-shot
              XXH3-128 (hasher.rs:126-148), one worker per host thread
+  gpu_procsP oxen_amd.procpool.ShardedFileHasher: the list split over P worker processes, each with
+             its own context and threads/P readers (the open/close floor is per process)
+  cpu_procsP the restated reference loop in P processes of threads/P threads, for the same split
 with the page cache warm, and cold (pages dropped with posix_fadvise DONTNEED). Also reports the
 pinned H2D copy rate. Every GPU digest is checked against the CPU one.
 """
@@ -36,6 +39,48 @@ def drop_cache(paths):
             pass
 
 
+def sharded(a, paths, meta, nbytes, cpu_call, drop_cache):
+    """The same files through P reader processes (GPU engines, then the CPU loop), warm alternating
+    rounds + one cold run each; digests checked against the one-process CPU loop."""
+    import numpy as np
+
+    from oxen_amd.procpool import ShardedFileHasher, pack_paths
+
+    res = {}
+    _, want, _ = cpu_call()
+    blob, offs = pack_paths(paths)  # packed once, outside the timing (as c_paths is)
+    for P in [int(x) for x in a.procs.split(",") if x]:
+        th = max(1, a.threads // P)
+        pools = {"gpu": ShardedFileHasher(procs=P, threads=th), "cpu": ShardedFileHasher(procs=P, threads=th, mode="cpu")}
+        try:
+            ts = {"gpu": [], "cpu": []}
+            ok = True
+            for k in pools:
+                pools[k].hash_files_packed(blob, offs, meta)  # warm-up
+            for _ in range(5):
+                for k in ("gpu", "cpu"):
+                    t0 = time.perf_counter()
+                    out, _, st = pools[k].hash_files_packed(blob, offs, meta)
+                    ts[k].append(time.perf_counter() - t0)
+                    ok = ok and bool((st == 0).all()) and np.array_equal(out, want)
+            for k in ("gpu", "cpu"):
+                med = float(np.median(ts[k]))
+                res[f"{k}_procs{P}_warm_s"] = round(med, 3)
+                res[f"{k}_procs{P}_warm_GiBs"] = round(nbytes / med / 2**30, 2)
+                res[f"{k}_procs{P}_warm_s_all"] = [round(x, 3) for x in ts[k]]
+                drop_cache(paths)
+                t0 = time.perf_counter()
+                out, _, st = pools[k].hash_files_packed(blob, offs, meta)
+                res[f"{k}_procs{P}_cold_s"] = round(time.perf_counter() - t0, 3)
+                ok = ok and bool((st == 0).all()) and np.array_equal(out, want)
+            res[f"procs{P}_threads_each"] = th
+            res[f"procs{P}_bit_exact"] = ok
+        finally:
+            for p in pools.values():
+                p.close()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--images", type=int, default=200_000)
@@ -43,6 +88,8 @@ def main():
     ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--keep", action="store_true")
     ap.add_argument("--staging-mib", default="16,64,256", help="staging slot sizes to sweep (warm cache)")
+    ap.add_argument("--procs", default="2,4", help="reader process counts for the sharded runs")
+    ap.add_argument("--only-procs", action="store_true", help="skip the add / fsck / staging parts")
     a = ap.parse_args()
 
     import numpy as np
@@ -114,56 +161,57 @@ def main():
                          st.ctypes.data_as(oracle._i32p), a.threads)
         return time.perf_counter() - t0, out, st
 
-    # fused add (hash + version-store publish from the same pinned bytes, one syncfs per slot before
-    # the renames and one after) vs the reference loop restated (hash, then re-read + re-hash + write +
-    # fsync + rename + parent fsync per new file), warm cache, fresh stores
-    vroot = os.path.join(a.dir, ".oxen_gpu", "versions", "files")
-    rroot = os.path.join(a.dir, ".oxen_ref", "versions", "files")
-    oracle.hash_files(paths[: min(len(paths), 1000)], a.threads)
-    t0 = time.perf_counter()
-    gd, _, gst, gstored = hasher.add_files(paths, vroot, ctx)
-    res["gpu_add_fused_s"] = round(time.perf_counter() - t0, 3)
-    t0 = time.perf_counter()
-    rout, _, rst, rstored = oracle.add_files(paths, rroot, a.threads)  # AtomicTempFile fsyncs per blob
-    res["cpu_ref_add_s"] = round(time.perf_counter() - t0, 3)
-    # the same loop without the per-blob fsyncs (the r01 restatement), for the A/B
-    nroot = os.path.join(a.dir, ".oxen_nosync", "versions", "files")
-    t0 = time.perf_counter()
-    oracle.add_files(paths, nroot, a.threads, sync=False)
-    res["cpu_ref_add_nosync_s"] = round(time.perf_counter() - t0, 3)
-    shutil.rmtree(os.path.join(a.dir, ".oxen_nosync"), ignore_errors=True)
-    res["gpu_add_fused_GiBs"] = round(nbytes / res["gpu_add_fused_s"] / 2**30, 2)
-    res["cpu_ref_add_GiBs"] = round(nbytes / res["cpu_ref_add_s"] / 2**30, 2)
-    res["add_blobs_written"] = [int(sum(gstored)), int(rstored.sum())]
-    res["add_digests_bit_exact"] = [(int(hi) << 64) | int(lo) for lo, hi in rout] == gd
-    # `oxen fsck` over the store the add just built (dry run: counts only), GPU vs the restated loop
-    t0 = time.perf_counter()
-    gf = hasher.clean_corrupted_versions(vroot, dry_run=True, ctx=ctx)
-    res["gpu_fsck_s"] = round(time.perf_counter() - t0, 3)
-    t0 = time.perf_counter()
-    rf = oracle.clean_corrupted_versions(rroot, dry_run=True, threads=a.threads)
-    res["cpu_ref_fsck_s"] = round(time.perf_counter() - t0, 3)
-    res["fsck_counts"] = [{k: gf[k] for k in rf}, rf]
-    shutil.rmtree(os.path.join(a.dir, ".oxen_gpu"), ignore_errors=True)
-    shutil.rmtree(os.path.join(a.dir, ".oxen_ref"), ignore_errors=True)
+    if not a.only_procs:
+        # fused add (hash + version-store publish from the same pinned bytes, one syncfs per slot before
+        # the renames and one after) vs the reference loop restated (hash, then re-read + re-hash + write +
+        # fsync + rename + parent fsync per new file), warm cache, fresh stores
+        vroot = os.path.join(a.dir, ".oxen_gpu", "versions", "files")
+        rroot = os.path.join(a.dir, ".oxen_ref", "versions", "files")
+        oracle.hash_files(paths[: min(len(paths), 1000)], a.threads)
+        t0 = time.perf_counter()
+        gd, _, gst, gstored = hasher.add_files(paths, vroot, ctx)
+        res["gpu_add_fused_s"] = round(time.perf_counter() - t0, 3)
+        t0 = time.perf_counter()
+        rout, _, rst, rstored = oracle.add_files(paths, rroot, a.threads)  # AtomicTempFile fsyncs per blob
+        res["cpu_ref_add_s"] = round(time.perf_counter() - t0, 3)
+        # the same loop without the per-blob fsyncs (the r01 restatement), for the A/B
+        nroot = os.path.join(a.dir, ".oxen_nosync", "versions", "files")
+        t0 = time.perf_counter()
+        oracle.add_files(paths, nroot, a.threads, sync=False)
+        res["cpu_ref_add_nosync_s"] = round(time.perf_counter() - t0, 3)
+        shutil.rmtree(os.path.join(a.dir, ".oxen_nosync"), ignore_errors=True)
+        res["gpu_add_fused_GiBs"] = round(nbytes / res["gpu_add_fused_s"] / 2**30, 2)
+        res["cpu_ref_add_GiBs"] = round(nbytes / res["cpu_ref_add_s"] / 2**30, 2)
+        res["add_blobs_written"] = [int(sum(gstored)), int(rstored.sum())]
+        res["add_digests_bit_exact"] = [(int(hi) << 64) | int(lo) for lo, hi in rout] == gd
+        # `oxen fsck` over the store the add just built (dry run: counts only), GPU vs the restated loop
+        t0 = time.perf_counter()
+        gf = hasher.clean_corrupted_versions(vroot, dry_run=True, ctx=ctx)
+        res["gpu_fsck_s"] = round(time.perf_counter() - t0, 3)
+        t0 = time.perf_counter()
+        rf = oracle.clean_corrupted_versions(rroot, dry_run=True, threads=a.threads)
+        res["cpu_ref_fsck_s"] = round(time.perf_counter() - t0, 3)
+        res["fsck_counts"] = [{k: gf[k] for k in rf}, rf]
+        shutil.rmtree(os.path.join(a.dir, ".oxen_gpu"), ignore_errors=True)
+        shutil.rmtree(os.path.join(a.dir, ".oxen_ref"), ignore_errors=True)
 
-    # staging-slot size sweep (warm cache): small slots stay in the host L3, so the pread copy and
-    # the H2D DMA read do not both go through DRAM
-    sweep = {}
-    for mib in [int(x) for x in a.staging_mib.split(",") if x]:
-        cs = _capi.Context(0, staging_bytes=mib << 20)
-        ts = []
-        for _ in range(3):
-            out = np.zeros((n, 2), dtype=np.uint64)
-            sz = np.zeros(n, dtype=np.uint64)
-            stt = np.zeros(n, dtype=np.int32)
-            t0 = time.perf_counter()
-            _capi.check(L.oxh_hash_files(cs.handle, c_paths, n, out.ctypes.data_as(_capi._u64p),
-                                         sz.ctypes.data_as(_capi._u64p), stt.ctypes.data_as(_capi._i32p)), "sweep")
-            ts.append(time.perf_counter() - t0)
-        cs.close()
-        sweep[f"staging_{mib}MiB_GiBs"] = round(nbytes / min(ts) / 2**30, 2)
-    res["gpu_e2e_warm_staging_sweep"] = sweep
+        # staging-slot size sweep (warm cache): small slots stay in the host L3, so the pread copy and
+        # the H2D DMA read do not both go through DRAM
+        sweep = {}
+        for mib in [int(x) for x in a.staging_mib.split(",") if x]:
+            cs = _capi.Context(0, staging_bytes=mib << 20)
+            ts = []
+            for _ in range(3):
+                out = np.zeros((n, 2), dtype=np.uint64)
+                sz = np.zeros(n, dtype=np.uint64)
+                stt = np.zeros(n, dtype=np.int32)
+                t0 = time.perf_counter()
+                _capi.check(L.oxh_hash_files(cs.handle, c_paths, n, out.ctypes.data_as(_capi._u64p),
+                                             sz.ctypes.data_as(_capi._u64p), stt.ctypes.data_as(_capi._i32p)), "sweep")
+                ts.append(time.perf_counter() - t0)
+            cs.close()
+            sweep[f"staging_{mib}MiB_GiBs"] = round(nbytes / min(ts) / 2**30, 2)
+        res["gpu_e2e_warm_staging_sweep"] = sweep
 
     runs = {}
     # warm: GPU and CPU alternate, 5 rounds (host timings on a shared box vary by +-20 % run to run)
@@ -189,6 +237,7 @@ def main():
         res[f"{who}_cold_GiBs"] = round(nbytes / dt / 2**30, 2)
     res["digests_bit_exact"] = (all(np.array_equal(runs[("gpu_e2e", c)], runs[("cpu_ref", c)]) for c in ("warm", "cold"))
                                 and np.array_equal(runs[("gpu_e2e_meta", "warm")], runs[("cpu_ref", "warm")]))
+    res.update(sharded(a, paths, meta, nbytes, cpu_call, drop_cache))
     # the Python mirror (hasher.hash_files_128bit) on warm cache, for its wrapper overhead
     t0 = time.perf_counter()
     d, _, _ = hasher.hash_files_128bit(paths, ctx)

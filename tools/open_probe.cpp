@@ -9,6 +9,8 @@
 //   dirfd_nostat  both
 //   openclose     open(path) + close                               (path walk + fd only)
 //   dirfd_oc      openat(dirfd, basename) + close
+// PROCS=P in the environment splits the list into P contiguous parts read by P forked processes of
+// T/P threads each (separate file tables and address spaces): does the floor belong to one process?
 // Prints one JSON line per run.
 //   g++ -O2 -std=c++17 -pthread tools/open_probe.cpp -o tools/open_probe
 //   find DIR -type f | tools/open_probe 16 full dirfd nostat dirfd_nostat openclose dirfd_oc
@@ -16,6 +18,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <sys/stat.h>
+#include <sys/wait.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -58,18 +61,34 @@ int main(int argc, char** argv) {
         const bool at = mode.rfind("dirfd", 0) == 0;
         const bool nostat = mode.find("nostat") != std::string::npos;
         const bool oc = mode == "openclose" || mode == "dirfd_oc";
+        const int P = getenv("PROCS") ? std::max(1, atoi(getenv("PROCS"))) : 1;
+        const int TP = std::max(1, T / P);
         std::atomic<size_t> next{0};
         std::atomic<uint64_t> bytes{0}, errors{0};
         const double t0 = now();
+        size_t lo = 0, hi = n;
+        std::vector<pid_t> kids;
+        for (int p = 1; p < P; ++p) {  // process p reads part p; this process reads part 0
+            const pid_t pid = fork();
+            if (pid == 0) {
+                lo = n * p / P;
+                hi = n * (p + 1) / P;
+                kids.clear();
+                break;
+            }
+            kids.push_back(pid);
+            hi = n / P;
+        }
+        next = lo;
         std::vector<std::thread> th;
-        for (int t = 0; t < T; ++t)
+        for (int t = 0; t < (P > 1 ? TP : T); ++t)
             th.emplace_back([&] {
                 std::vector<char> buf(1 << 20);
                 uint64_t mine = 0, err = 0;
                 for (;;) {
                     const size_t i0 = next.fetch_add(8);
-                    if (i0 >= n) break;
-                    for (size_t i = i0; i < i0 + 8 && i < n; ++i) {
+                    if (i0 >= hi) break;
+                    for (size_t i = i0; i < i0 + 8 && i < hi; ++i) {
                         const int fd = at ? openat(dfd[dir_of[i]], base[i].c_str(), O_RDONLY) : open(paths[i].c_str(), O_RDONLY);
                         if (fd < 0) {
                             ++err;
@@ -104,9 +123,15 @@ int main(int argc, char** argv) {
                 errors.fetch_add(err);
             });
         for (auto& t : th) t.join();
+        if (P > 1 && lo != 0) _exit(errors.load() ? 1 : 0);  // a child: its part is done
+        for (const pid_t k : kids) {
+            int st = 0;
+            waitpid(k, &st, 0);
+            if (!WIFEXITED(st) || WEXITSTATUS(st)) errors.fetch_add(1);
+        }
         const double dt = now() - t0;
-        printf("{\"mode\": \"%s\", \"threads\": %d, \"files\": %zu, \"bytes\": %llu, \"errors\": %llu, \"s\": %.4f}\n",
-               mode.c_str(), T, n, (unsigned long long)bytes.load(), (unsigned long long)errors.load(), dt);
+        printf("{\"mode\": \"%s\", \"procs\": %d, \"threads\": %d, \"files\": %zu, \"bytes\": %llu, \"errors\": %llu, \"s\": %.4f}\n",
+               mode.c_str(), P, T, n, (unsigned long long)bytes.load(), (unsigned long long)errors.load(), dt);
         fflush(stdout);
     }
     return 0;
