@@ -7,6 +7,9 @@ a whole read (open + fstat + pread + close) 0.27-0.29 s in one process, 0.155-0.
 (tools/open_probe.cpp with PROCS=P, profiles/r02e_open_procs.json). One context's engine is one
 process, so it sits on the one-process floor; this pool runs P engines (one `oxh_ctx` each, all on
 the same GPU) in P spawned worker processes and gives each a contiguous share of the list.
+Measured on C3 warm (tools/bench_e2e.py, profiles/r02e_e2e_c3_procs.json): one engine 0.30-0.32 s,
+2 processes x 8 readers 0.21 s, 4 x 4 0.22 s -- the GPU side is then at its PCIe floor (9.87 GB of
+pinned H2D at 55 GB/s = 0.18 s), so 2 is the default.
 
 The list crosses the process boundary once, as NUL-terminated paths packed in one shared-memory
 arena plus an offsets table (`pack_paths`); each worker points its own char* table into its mapping
@@ -41,14 +44,9 @@ def pack_paths(paths: Sequence) -> tuple[np.ndarray, np.ndarray]:
 
 
 def _attach(name: str) -> shared_memory.SharedMemory:
-    shm = shared_memory.SharedMemory(name=name)
-    try:  # Python < 3.13 registers attached segments with the child's tracker, which would unlink them
-        from multiprocessing import resource_tracker
-
-        resource_tracker.unregister(shm._name, "shared_memory")  # type: ignore[attr-defined]
-    except Exception:
-        pass
-    return shm
+    # spawned workers share the parent's resource tracker: their (re-)registration of the name is the
+    # parent's own entry, which the parent's unlink in close() removes
+    return shared_memory.SharedMemory(name=name)
 
 
 def _worker(conn, device: int, staging_bytes: int, mode: str, threads: int) -> None:
@@ -115,7 +113,7 @@ class ShardedFileHasher:
     reader threads. `mode="cpu"` runs the oracle's restated reference loop in the workers instead
     (tools/ only: a comparison at the same process count)."""
 
-    def __init__(self, procs: int = 4, device: int = 0, threads: Optional[int] = None, staging_bytes: int = 0,
+    def __init__(self, procs: int = 2, device: int = 0, threads: Optional[int] = None, staging_bytes: int = 0,
                  mode: str = "gpu"):
         if procs < 1:
             raise _capi.OxenError("procs must be >= 1", _capi.OXH_ERR_INVALID)
