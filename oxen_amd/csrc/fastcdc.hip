@@ -77,16 +77,24 @@ struct CdcParams {
     uint32_t speccap;  // speculative chunk starts stored per section
 };
 
+// One recorded candidate group: its entry (group index in the unit << 47 | the full-window hash
+// before its first byte mod 2^47; bit 47 and up never reach a masked bit once the walk shifts it, so
+// 47 bits suffice) and its 16 bytes (the walk resolves exact flags from these), in one 32-byte record:
+// F1's two stores and the walk's two loads of a candidate touch one cache line, not one in each of
+// two arrays.
+struct alignas(16) CandRec {
+    uint64_t e;
+    uint64_t pad;
+    uint4 b;
+};
+
 struct CdcFiles {
     const uint8_t* arena;
     const uint64_t* foff;      // [n] arena offset of each file
     const uint64_t* flen;      // [n]
     const uint64_t* sec_base;  // [n+1] first global section of each file
     const uint32_t* sec_file;  // [n_sec] file of each section
-    uint64_t* cand_e;          // [n_sec * 64 * cap] candidate groups per unit, in order: group index in the unit
-                               // << 47 | the full-window hash before its first byte mod 2^47 (bit 47 and up
-                               // never reach a masked bit once the walk shifts it, so 47 bits suffice)
-    uint4* cand_b;             // [n_sec * 64 * cap] the group's 16 bytes (the walk resolves flags from these)
+    CandRec* cand;             // [n_sec * 64 * cap] candidate groups per unit, in position order
     uint32_t* cand_cnt;        // [n_sec * 64] true count per unit (> cap: list truncated, dense fallback)
     uint64_t* cand_occ;        // [n_sec] bit u: unit u of the section has a non-empty list
     uint32_t* spec;            // [n_sec * speccap] speculative starts, relative to section start
@@ -206,8 +214,7 @@ __global__ __launch_bounds__(64 * WAVES) void cdc_scan_kernel(CdcFiles f, CdcPar
         return *(const uint64_t*)(tab + a);
     };
     const uint64_t ubase = sec * 64 + (uint64_t)lane;  // global unit index
-    uint64_t* __restrict__ out_e = f.cand_e + ubase * prm.cap;
-    uint4* __restrict__ out_b = f.cand_b + ubase * prm.cap;
+    CandRec* __restrict__ out_c = f.cand + ubase * prm.cap;
     uint32_t count = 0;  // per lane
 
     // warm-up over the 48 bytes before the unit (lane 0 at a file start: none, the hash starts at 0)
@@ -309,10 +316,12 @@ __global__ __launch_bounds__(64 * WAVES) void cdc_scan_kernel(CdcFiles f, CdcPar
                 if (__builtin_amdgcn_ballot_w64(anyz == 0)) {
                     const uint32_t g = rb + 16 * (uint32_t)(i >> 2);  // the group, section-relative
                     if (anyz == 0 && g < sec_len) {
+#ifndef OXH_F1_NOSTORE  // diagnostic builds only: the cost of the candidate stores (output invalid)
                         if (count < prm.cap) {
-                            out_e[count] = ((uint64_t)((g - us) >> 4) << kEntryShift) | ((SH ? (hb >> 16) : hb) & kEntryHash);
-                            out_b[count] = make_uint4(wv[i - 3], wv[i - 2], wv[i - 1], wv[i]);
+                            out_c[count].e = ((uint64_t)((g - us) >> 4) << kEntryShift) | ((SH ? (hb >> 16) : hb) & kEntryHash);
+                            out_c[count].b = make_uint4(wv[i - 3], wv[i - 2], wv[i - 1], wv[i]);
                         }
+#endif
                         ++count;
                     }
                 }
@@ -426,19 +435,18 @@ __device__ uint64_t first_cand(const CdcFiles& f, const CdcParams& prm, uint64_t
         }
         const uint64_t sec_start = (cur.sec - u0) * prm.unit;  // the unit's start, file-relative
         if (sec_start >= hi) return hi;
-        const uint64_t* es = f.cand_e + cur.sec * prm.cap;
-        const uint4* bs = f.cand_b + cur.sec * prm.cap;
+        const CandRec* cs = f.cand + cur.sec * prm.cap;
         // an entry and its 16 bytes are loaded together (the bytes before the entry says whether they
         // are needed), and the first pair together with the count (speculatively: slots past the
         // count are scratch, read but never used)
         const uint32_t cnt = f.cand_cnt[cur.sec];
-        uint64_t e_nx = cur.idx < prm.cap ? es[cur.idx] : 0;
-        uint4 b_nx = cur.idx < prm.cap ? bs[cur.idx] : make_uint4(0, 0, 0, 0);
+        uint64_t e_nx = cur.idx < prm.cap ? cs[cur.idx].e : 0;
+        uint4 b_nx = cur.idx < prm.cap ? cs[cur.idx].b : make_uint4(0, 0, 0, 0);
         const uint32_t stored = cnt < prm.cap ? cnt : prm.cap;
         for (bool first = true; cur.idx < stored; first = false) {
             if (!first) {
-                e_nx = es[cur.idx];
-                b_nx = bs[cur.idx];
+                e_nx = cs[cur.idx].e;
+                b_nx = cs[cur.idx].b;
             }
             const uint64_t e = e_nx;
             const uint4 bv = b_nx;
@@ -465,7 +473,7 @@ __device__ uint64_t first_cand(const CdcFiles& f, const CdcParams& prm, uint64_t
         const uint64_t sec_end = sec_start + prm.unit;
         if (cnt > prm.cap) {
             // overflowed list: positions after the last stored group were not recorded
-            const uint64_t after = stored ? sec_start + (es[stored - 1] >> kEntryShift) * 16 + 16 : sec_start;
+            const uint64_t after = stored ? sec_start + (cs[stored - 1].e >> kEntryShift) * 16 + 16 : sec_start;
             const uint64_t a = lo > after ? lo : after;
             const uint64_t b = hi < sec_end ? hi : sec_end;
             if (a < b) {
@@ -927,15 +935,14 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     Scratch sc(st);
     uint64_t *d_foff, *d_flen, *d_sec_base, *d_first, *d_exit, *d_out_base;
     uint32_t *d_sec_file, *d_cand_cnt, *d_spec, *d_spec_cnt, *d_status, *d_k0, *d_count, *d_fix;
-    uint64_t *d_cand_e, *d_cand_occ;
-    uint4* d_cand_b;
+    uint64_t* d_cand_occ;
+    oxh::CandRec* d_cand;
     sc.want(&d_foff, n);
     sc.want(&d_flen, n);
     sc.want(&d_sec_base, n + 1);
     sc.want(&d_first, n + 1);
     sc.want(&d_sec_file, n_sec);
-    sc.want(&d_cand_e, n_sec * 64 * prm.cap);
-    sc.want(&d_cand_b, n_sec * 64 * prm.cap);
+    sc.want(&d_cand, n_sec * 64 * prm.cap);
     sc.want(&d_cand_cnt, n_sec * 64);
     sc.want(&d_cand_occ, n_sec);
     sc.want(&d_spec, n_sec * prm.speccap);
@@ -958,7 +965,7 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     }
 
     const double t_alloc = since();
-    oxh::CdcFiles f{(const uint8_t*)d_arena, d_foff, d_flen, d_sec_base, d_sec_file, d_cand_e, d_cand_b, d_cand_cnt, d_cand_occ, d_spec, d_spec_cnt};
+    oxh::CdcFiles f{(const uint8_t*)d_arena, d_foff, d_flen, d_sec_base, d_sec_file, d_cand, d_cand_cnt, d_cand_occ, d_spec, d_spec_cnt};
     oxh::CdcStitch sti{d_status, d_k0, d_count, d_exit, d_fix, d_out_base};
     if (n_sec) {
         // F1: one wave per section (kScanWaves per workgroup, 160 KiB of LDS); SH when the bits both
