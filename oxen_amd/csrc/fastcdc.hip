@@ -82,9 +82,12 @@ struct CdcParams {
 // 47 bits suffice) and its 16 bytes (the walk resolves exact flags from these), in one 32-byte record:
 // F1's two stores and the walk's two loads of a candidate touch one cache line, not one in each of
 // two arrays.
+// The first record of a unit's list also carries the unit's true candidate count in `n` (> cap: the
+// list was truncated and the walk scans the rest of the unit's bytes), so a walk entering a unit
+// gets the count and the first candidate from one line.
 struct alignas(16) CandRec {
     uint64_t e;
-    uint64_t pad;
+    uint64_t n;  // record 0 of a unit: the unit's count; unused in the others
     uint4 b;
 };
 
@@ -95,7 +98,6 @@ struct CdcFiles {
     const uint64_t* sec_base;  // [n+1] first global section of each file
     const uint32_t* sec_file;  // [n_sec] file of each section
     CandRec* cand;             // [n_sec * 64 * cap] candidate groups per unit, in position order
-    uint32_t* cand_cnt;        // [n_sec * 64] true count per unit (> cap: list truncated, dense fallback)
     uint64_t* cand_occ;        // [n_sec] bit u: unit u of the section has a non-empty list
     uint32_t* spec;            // [n_sec * speccap] speculative starts, relative to section start
     uint32_t* spec_cnt;        // [n_sec]
@@ -332,7 +334,7 @@ __global__ __launch_bounds__(64 * WAVES) void cdc_scan_kernel(CdcFiles f, CdcPar
             __builtin_amdgcn_sched_barrier(0);
         }
     }
-    f.cand_cnt[ubase] = count;
+    out_c[0].n = count;
     const uint64_t occ = __builtin_amdgcn_ballot_w64(count != 0);
     if (lane == 0) f.cand_occ[sec] = occ;
 }
@@ -439,7 +441,7 @@ __device__ uint64_t first_cand(const CdcFiles& f, const CdcParams& prm, uint64_t
         // an entry and its 16 bytes are loaded together (the bytes before the entry says whether they
         // are needed), and the first pair together with the count (speculatively: slots past the
         // count are scratch, read but never used)
-        const uint32_t cnt = f.cand_cnt[cur.sec];
+        const uint32_t cnt = (uint32_t)cs[0].n;
         uint64_t e_nx = cur.idx < prm.cap ? cs[cur.idx].e : 0;
         uint4 b_nx = cur.idx < prm.cap ? cs[cur.idx].b : make_uint4(0, 0, 0, 0);
         const uint32_t stored = cnt < prm.cap ? cnt : prm.cap;
@@ -934,7 +936,7 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     auto since = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(); };
     Scratch sc(st);
     uint64_t *d_foff, *d_flen, *d_sec_base, *d_first, *d_exit, *d_out_base;
-    uint32_t *d_sec_file, *d_cand_cnt, *d_spec, *d_spec_cnt, *d_status, *d_k0, *d_count, *d_fix;
+    uint32_t *d_sec_file, *d_spec, *d_spec_cnt, *d_status, *d_k0, *d_count, *d_fix;
     uint64_t* d_cand_occ;
     oxh::CandRec* d_cand;
     sc.want(&d_foff, n);
@@ -943,7 +945,6 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     sc.want(&d_first, n + 1);
     sc.want(&d_sec_file, n_sec);
     sc.want(&d_cand, n_sec * 64 * prm.cap);
-    sc.want(&d_cand_cnt, n_sec * 64);
     sc.want(&d_cand_occ, n_sec);
     sc.want(&d_spec, n_sec * prm.speccap);
     sc.want(&d_spec_cnt, n_sec);
@@ -965,7 +966,7 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     }
 
     const double t_alloc = since();
-    oxh::CdcFiles f{(const uint8_t*)d_arena, d_foff, d_flen, d_sec_base, d_sec_file, d_cand, d_cand_cnt, d_cand_occ, d_spec, d_spec_cnt};
+    oxh::CdcFiles f{(const uint8_t*)d_arena, d_foff, d_flen, d_sec_base, d_sec_file, d_cand, d_cand_occ, d_spec, d_spec_cnt};
     oxh::CdcStitch sti{d_status, d_k0, d_count, d_exit, d_fix, d_out_base};
     if (n_sec) {
         // F1: one wave per section (kScanWaves per workgroup, 160 KiB of LDS); SH when the bits both
