@@ -98,11 +98,16 @@ def _worker(conn, device: int, staging_bytes: int, mode: str, threads: int) -> N
                 O.oxo_hash_files(pp, k, o_p, s_p, t_p, threads or 1)
                 rc, err = 0, ""
             del base, offs, out, sizes, status
+            if has_meta and mode == "gpu":
+                del meta
             conn.send(("done", rc, err))
         except Exception as e:  # reported to the caller, which raises
             conn.send(("done", -1, repr(e)))
     for s in attached.values():
-        s.close()
+        try:
+            s.close()
+        except BufferError:  # a view from a failed call still holds it; the process is exiting
+            pass
     if mode == "gpu":
         ctx.close()
 
