@@ -5,6 +5,9 @@
 One step = one batched K1 launch hashing every buffer of the rank's shard, already resident in HBM
 (plus, for N > 1, the single all-gather of the 16-B digest table over RCCL). Workload (weak
 scaling, per GPU): BASELINE.json configs[1] -- 100 000 x 64 KiB splitmix64 blobs (6.1 GiB).
+N > 1: one process per GPU. Under torch.distributed.run (WORLD_SIZE set) this process is one rank
+and WORLD_SIZE must equal --gpus; without a launcher, `--gpus N` starts the N ranks itself before
+anything touches the GPU and exits with the worst rank's status.
 Prints ONE JSON line on rank 0 (the driver's contract), including:
   roofline      achieved HBM read GB/s of the K1 kernel (algorithmic bytes = buffer lengths) vs the
                 8 TB/s MI355X peak; `traffic` = PMC-measured HBM bytes per launch when a matching
@@ -33,11 +36,70 @@ WORKLOADS = {
     # name: (items per GPU, bytes per item, BASELINE config)
     "c2": (100_000, 65_536, "100 000 x 64 KiB random blobs, device-resident, 1 MI355X (BASELINE configs[1])"),
     "c4": (125_000, 262_144, "1 000 000 x 256 KiB blobs / 8 GPUs = 125 000 x 256 KiB per GPU (BASELINE configs[3])"),
+    # launcher / multi-rank mechanics in tests only; never a bench line
+    "t": (2_048, 65_536, "test size: 2 048 x 64 KiB (rank-launch mechanics)"),
 }
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def usable_cpus() -> int:
+    """CPUs this process may use: the affinity mask capped by the cgroup-v2 quota (cpu.max), as the
+    library's engine counts them; os.cpu_count() sees the whole machine on the GPU box."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max" and int(period) > 0:
+            n = min(n, max(1, -(-int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes of this script (one per GPU,
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, as torch.distributed.run sets
+    them) before this process touches the GPU, wait for all, and return the worst exit code. The
+    first rank to fail takes the others down (a dead rank would leave the rest in a barrier)."""
+    import subprocess
+
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GROUP_RANK="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    worst = 0
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            rc = procs[r].poll()
+            if rc is None:
+                continue
+            live.discard(r)
+            if rc != 0:
+                log(f"[bench] rank {r} exited with {rc}; stopping the other ranks")
+                worst = worst or rc
+                for q in live:
+                    procs[q].terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+        if p.returncode != 0 and worst == 0:
+            worst = p.returncode
+    return worst if worst >= 0 else 128 - worst
 
 
 def cpu_baseline(da, gpu_digests: np.ndarray, seed: int, budget_s: float = 10.0) -> dict:
@@ -48,7 +110,7 @@ def cpu_baseline(da, gpu_digests: np.ndarray, seed: int, budget_s: float = 10.0)
     from oxen_amd.workloads import splitmix_bytes
 
     oracle.build()
-    threads = min(16, os.cpu_count() or 1)
+    threads = usable_cpus()
     item_len = int(da.lens_host[0])
     nsample = min(da.n, max(threads, (1 << 30) // max(item_len, 1)))  # 1 GiB: beyond the host L3
     idx = np.linspace(0, da.n - 1, nsample).astype(np.int64)
@@ -137,6 +199,20 @@ def load_traffic(workload: str):
     return best
 
 
+def load_profile(workload: str):
+    """The newest rocprofv3 kernel-trace summary of the K1 kernel for this workload
+    (profiles/*_profile_<workload>.json, written by tools/prof_summary.py from the stats CSV)."""
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_profile_{workload}.json"))):
+        try:
+            d = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        if d.get("avg_ms"):
+            best = dict(d, source=os.path.relpath(p, ROOT))
+    return best
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -152,6 +228,15 @@ def main() -> None:
                     help="take the N>1 path (process group, pipelined RCCL gather) even at WORLD_SIZE=1: "
                          "rehearses the multi-GPU step on a one-GPU box under torch.distributed.run")
     args = ap.parse_args()
+    if args.gpus < 1:
+        log("[bench] --gpus must be >= 1")
+        sys.exit(2)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))  # this process never touches the GPU
+    if env_world is not None and int(env_world) != args.gpus:
+        log(f"[bench] WORLD_SIZE={env_world} but --gpus {args.gpus}: launch one rank per GPU, N = --gpus")
+        sys.exit(2)
 
     import torch
     import torch.distributed as dist
@@ -160,6 +245,10 @@ def main() -> None:
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = max(1, torch.cuda.device_count())
+    if world > ndev and args.backend == "nccl":
+        log(f"[bench] {world} ranks but {ndev} visible GPU(s): RCCL needs one GPU per rank "
+            "(--backend gloo rehearses N > 1 on fewer GPUs)")
+        sys.exit(2)
     dev = torch.device(f"cuda:{local_rank % ndev}")
     torch.cuda.set_device(dev)
     multi = world > 1 or args.dist  # the distributed step (barriers, gather, max over ranks)
@@ -232,19 +321,32 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize()
     gpu_s = ev0.elapsed_time(ev1) / 1e3
-    # per-launch kernel time, from HIP events on the launch stream (no collective in this window)
+    # per-launch kernel time, from HIP events on the launch stream (no collective in this window):
+    # (a) each launch alone between its own two events, the GPU idle before it -- what a profiler's
+    # per-dispatch duration measures, and the figure the roofline uses; (b) back to back, where one
+    # launch's last waves overlap the next one's first (a throughput figure, reported beside it)
+    kreps = max(5, args.steps)
+    iso = []
+    for _ in range(kreps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        da.hash(out)
+        e1.record()
+        torch.cuda.synchronize()
+        iso.append(e0.elapsed_time(e1) / 1e3)
+    kernel_s = float(np.median(iso))
     kev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     kev[0].record()
-    kreps = max(5, args.steps)
     for _ in range(kreps):
         da.hash(out)
     kev[1].record()
     torch.cuda.synchronize()
-    kernel_s = kev[0].elapsed_time(kev[1]) / 1e3 / kreps
+    kernel_b2b_s = kev[0].elapsed_time(kev[1]) / 1e3 / kreps
 
     elapsed = max(wall, gpu_s)
     log(f"[bench] rank {rank}: wall {wall * 1e3:.3f} ms, events {gpu_s * 1e3:.3f} ms, enqueue {t_enq * 1e3:.3f} ms, "
-        f"kernel {kernel_s * 1e3:.4f} ms x {args.steps} = {kernel_s * args.steps * 1e3:.3f} ms")
+        f"kernel {kernel_s * 1e3:.4f} ms alone (median of {kreps}), {kernel_b2b_s * 1e3:.4f} ms back to back; "
+        f"x {args.steps} = {kernel_b2b_s * args.steps * 1e3:.3f} ms")
     t = torch.tensor([elapsed, kernel_s], dtype=torch.float64, device=dev)
     if multi:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -274,9 +376,16 @@ def main() -> None:
                     "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": (tr["hbm_bytes_per_launch"] if tr else None),
                     "kernel": "xxh3_wave_kernel (K1)", "kernel_ms": round(kernel_s * 1e3, 4),
+                    "kernel_ms_how": f"HIP events around each launch alone on the launch stream, median of {kreps}",
+                    "kernel_ms_back_to_back": round(kernel_b2b_s * 1e3, 4),
                     "algorithmic_bytes_per_launch": bytes_per_rank}
         if tr:
             roofline["traffic_source"] = tr.get("source")
+        prof = load_profile(args.workload)
+        if prof:  # the rocprofv3 kernel-trace average of this same command, committed under profiles/
+            roofline["profile"] = {"avg_ms": prof["avg_ms"], "calls": prof["calls"], "command": prof["command"],
+                                   "source": prof["source"],
+                                   "frac": round(bytes_per_rank / (prof["avg_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
         cpu = None
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(da, digests, seed, args.cpu_budget)

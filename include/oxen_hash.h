@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define OXH_ABI_VERSION 1
+#define OXH_ABI_VERSION 2
 
 /* status codes (also used per item in status[]) */
 #define OXH_OK 0
@@ -167,6 +167,30 @@ int oxh_add_files(oxh_ctx* ctx, const char* const* paths, uint64_t n, const char
  * is removed unless dry_run; a failed removal is an error. */
 int oxh_clean_corrupted_versions(oxh_ctx* ctx, const char* versions_root, int dry_run, uint64_t* result);
 
+/* ---------------------------------------------------------------- reader-process pool
+ * oxh_hash_files / oxh_hash_files_meta over a list split across `procs` helper PROCESSES. The warm
+ * page-cache floor of reading many small files is open()+close() themselves, and it is per process
+ * (200 000 opens: 0.28 s in one process at any thread count, 0.16 s in two, 0.13 s in four;
+ * DESIGN.md §5), so one context's engine -- one process -- sits on it. The pool starts helper
+ * processes (posix_spawn of `oxh_hash_helper` from this library's directory, $OXH_HELPER overrides),
+ * each with its own context on devices[p % ndevices] and `threads` reader threads (<= 0: the
+ * process's CPU quota / procs, at most 16); ndevices = 0 means device 0. With devices {0..7} every
+ * GPU of a node is fed its own contiguous share over its own PCIe link. Shares are
+ * balanced by bytes when meta_sizes is given. Paths and outputs cross the process boundary through
+ * one shared-memory region; calls on one pool serialise. Helpers exit on oxh_pool_destroy, or when
+ * the creating process exits. A helper that dies makes the call, and every later call, fail with
+ * OXH_ERR_HIP. Creation fails with the first helper's error (e.g. OXH_ERR_NODEVICE without a GPU).
+ * Replaces the reference's fan-out of 64-file batches over num_cpus*2 tasks of one process
+ * (core/v_latest/add.rs:422-425) with a fan-out over processes and devices. */
+typedef struct oxh_pool oxh_pool;
+int oxh_pool_create(const int* devices, int ndevices, int procs, int threads, uint64_t staging_bytes, oxh_pool** out);
+/* oxh_hash_files (meta_sizes == NULL) or oxh_hash_files_meta semantics, per-file status[] included. */
+int oxh_pool_hash_files(oxh_pool* pool, const char* const* paths, const uint64_t* meta_sizes, uint64_t n,
+                        uint64_t* out, uint64_t* sizes, int32_t* status);
+/* procs = number of helpers; pids (may be NULL) receives their process ids. */
+int oxh_pool_size(oxh_pool* pool, int* procs, int* pids);
+int oxh_pool_destroy(oxh_pool* pool);
+
 /* Text-metadata fusion (K1T): the same digests as oxh_hash_files plus, per file, the counts liboxen's
  * text metadata reads in a second full pass (repositories/metadata/text.rs:11-20 ->
  * util/fs.rs:217-263): counts[2i] = num_lines (1 + number of b'\n'), counts[2i+1] = num_chars
@@ -186,18 +210,32 @@ int oxh_hash_files_text_utf8(oxh_ctx* ctx, const char* const* paths, uint64_t n,
  * (util/fs.rs:1580-1619) x n, behind LocalRepository::is_modified_from_node_with_metadata
  * (model/repository/local_repository.rs:601-615). Per item, from the caller's walk: sizes[i] =
  * metadata.len(), node_bytes[i] = node.num_bytes(), mtime_matched[i] = mtime_matches(...) (the
- * caller's tolerance rule), node_hashes[2i..2i+1] = node.hash() (lo, hi).
- *   sizes[i] != node_bytes[i]  -> modified[i] = 1, file not read;
- *   else mtime_matched[i]      -> modified[i] = 0, file not read;
- *   else modified[i] = (get_hash_given_metadata(path) != node.hash()); every such file is hashed in
- *        one engine request (oxh_hash_files_meta semantics, read to EOF).
- * The reference's metadata-hash comparison between the last two steps is a shortcut whose verdict
- * the content comparison repeats (metadata is extracted from the content) and is not taken.
- * status[i] = OXH_OK, or the read error of a file that had to be hashed (modified[i] = 0 then; the
- * reference returns that error). status and n_hashed (the count of files read) may be NULL. */
+ * caller's tolerance rule), node_hashes[2i..2i+1] = node.hash() (lo, hi);
+ * node_meta_present[i] / node_meta_hashes[2i..2i+1] = node.metadata_hash() (Some / its value; both
+ * NULL: None for every item); file_meta_kind[i] (OXH_META_*; NULL: OXH_META_NONE for every item) says
+ * how the working file's maybe_get_metadata_hash(get_file_metadata(path, data_type)) (fs.rs:1601-1607)
+ * is obtained, with file_meta_hashes[2i..2i+1] its value for OXH_META_GIVEN. In the reference's order:
+ *   sizes[i] != node_bytes[i]  -> modified[i] = 1, file not read                      (fs.rs:1590-1592)
+ *   else mtime_matched[i]      -> modified[i] = 0, file not read                      (fs.rs:1595-1597)
+ *   else OXH_META_ERROR        -> status[i] = OXH_ERR_META (the reference's `?`), file not read
+ *   else node and file metadata hashes both Some and different -> modified[i] = 1     (fs.rs:1609-1614)
+ *        (OXH_META_GIVEN: decided before any read; OXH_META_TEXT: MetadataText {num_lines, num_chars}
+ *        is counted on the hashing read itself (K1T, repositories/metadata/text.rs:11-20) and its
+ *        serde_json `{"text":{"num_lines":L,"num_chars":C}}` hashed on the device)
+ *   else modified[i] = (get_hash_given_metadata(path) != node.hash())                (fs.rs:1616-1618)
+ * Every file that has to be read is read once, all of them in one engine request (oxh_hash_files_meta
+ * semantics, read to EOF). status[i] = OXH_OK, OXH_ERR_META as above, or the read error of a file
+ * that had to be read (modified[i] = 0 then; the reference returns that error). status and n_hashed
+ * (the count of files read) may be NULL. */
+#define OXH_ERR_META 6      /* the caller's metadata extraction failed (per item, oxh_files_modified) */
+#define OXH_META_NONE 0     /* the file's metadata hash is None (no metadata for its data type) */
+#define OXH_META_GIVEN 1    /* the caller computed it: file_meta_hashes[2i..2i+1] */
+#define OXH_META_TEXT 2     /* data type Text: counted on the hashing read and hashed on the device */
+#define OXH_META_ERROR 3    /* the caller's extraction returned an error */
 int oxh_files_modified(oxh_ctx* ctx, const char* const* paths, const uint64_t* sizes, const uint64_t* node_bytes,
-                       const uint8_t* mtime_matched, const uint64_t* node_hashes, uint64_t n, uint8_t* modified,
-                       int32_t* status, uint64_t* n_hashed);
+                       const uint8_t* mtime_matched, const uint64_t* node_hashes, const uint8_t* node_meta_present,
+                       const uint64_t* node_meta_hashes, const uint8_t* file_meta_kind, const uint64_t* file_meta_hashes,
+                       uint64_t n, uint8_t* modified, int32_t* status, uint64_t* n_hashed);
 /* Device-resident is_utf8 sniff: d_flags[i] (int32) for item i of the arena (first 4 KiB). */
 int oxh_utf8_prefix_device(const void* d_arena, const uint64_t* d_offsets, const uint64_t* d_lens, uint64_t n,
                            int32_t* d_flags, void* stream);

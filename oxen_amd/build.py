@@ -13,9 +13,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "liboxen_hash.so")
-SOURCES = [os.path.join(CSRC, "xxh3_kernels.hip"), os.path.join(CSRC, "oxen_hash_capi.hip"), os.path.join(CSRC, "fastcdc.hip")]
+SOURCES = [os.path.join(CSRC, "xxh3_kernels.hip"), os.path.join(CSRC, "oxen_hash_capi.hip"), os.path.join(CSRC, "fastcdc.hip"),
+           os.path.join(CSRC, "reader_pool.cpp")]
 DEPS = SOURCES + [os.path.join(CSRC, "xxh3_device.hpp"), os.path.join(CSRC, "fastcdc_gear.h"), os.path.join(CSRC, "pool.hpp"), os.path.join(CSRC, "scratch.hpp"),
-                  os.path.join(ROOT, "include", "oxen_hash.h")]
+                  os.path.join(CSRC, "reader_pool.hpp"), os.path.join(ROOT, "include", "oxen_hash.h")]
+HELPER_SRC = os.path.join(CSRC, "hash_helper.cpp")
+HELPER = os.path.join(HERE, "oxh_hash_helper")  # the reader-pool helper process (oxh_pool_*)
 ARCH = "gfx950"
 
 
@@ -54,6 +57,9 @@ def build_host(force: bool = False, verbose: bool = False) -> str:
     (tests/native/test_hasher.cpp, commit_tree_cli.cpp). All link against liboxen_hash.so."""
     hdr = os.path.join(ROOT, "include", "oxen_hash.h")
     steps = [
+        (HELPER, [HELPER_SRC, os.path.join(CSRC, "reader_pool.hpp"), hdr, LIB],
+         ["g++", "-std=c++17", "-O2", "-Wall", "-o", HELPER + ".tmp", HELPER_SRC,
+          f"-L{HERE}", "-l:liboxen_hash.so", "-Wl,-rpath,$ORIGIN"]),
         (HOST_LIB, [HOST_SRC, HOST_HDR, COMMIT_SRC, COMMIT_HDR, hdr, LIB],
          ["g++", "-std=c++17", "-O2", "-Wall", "-shared", "-fPIC", "-o", HOST_LIB + ".tmp", HOST_SRC, COMMIT_SRC,
           f"-L{HERE}", "-l:liboxen_hash.so", "-Wl,-rpath,$ORIGIN"]),

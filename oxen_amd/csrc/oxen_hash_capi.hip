@@ -220,6 +220,7 @@ int default_threads() {
 namespace oxh {
 // for the other translation units of the library (fastcdc.hip)
 int set_error(int code, const std::string& msg) { return fail(code, msg); }
+int cpu_quota() { return usable_cpus(); }
 }  // namespace oxh
 
 // ---------------------------------------------------------------- context
@@ -909,7 +910,7 @@ int oxh_xxh3_128_large_batch_device(const void* const* d_bufs, const uint64_t* l
 
 // ---------------------------------------------------------------- streaming XXH3 (Xxh3)
 // xxhash-rust's Xxh3::new / update / digest128 (hasher.rs:9,73-76,157-173, 183-244), with the device
-// doing the hashing: bytes collect in a pinned buffer of S + 1025 bytes (S = OXH_STREAM_PIECE_MIB,
+// doing the hashing: bytes collect in a pinned buffer (grown on demand) of up to S + 1025 bytes (S = OXH_STREAM_PIECE_MIB,
 // default 16 MiB, whole 1 KiB blocks); each time it fills, its first S bytes go to the device as one
 // K1L piece (block sums chip-wide, then the chain resumed from the stream's 8 accumulators, which stay
 // in device memory) and the last 1025 bytes move to the front. XXH3 scrambles every block but the
@@ -919,12 +920,15 @@ int oxh_xxh3_128_large_batch_device(const void* const* d_bufs, const uint64_t* l
 struct oxh_xxh3_stream {
     int device = 0;
     uint64_t piece = 0;           // S
-    uint8_t* h_pend = nullptr;    // pinned, S + 1025
+    uint8_t* h_pend = nullptr;    // pinned, grown on demand up to S + 1025
+    uint64_t h_cap = 0;
     uint64_t fill = 0, total = 0, pieces = 0;
-    uint8_t* d_mem = nullptr;     // [piece 0 | piece 1 | sums 0 | sums 1 | state 8 | out 2]
+    uint8_t* d_mem = nullptr;     // [piece 0 | piece 1 | sums 0 | sums 1 | state 8 | out 2], from the first piece on
     uint8_t* d_piece[2] = {};
     uint64_t* d_sums[2] = {};
     uint64_t *d_state = nullptr, *d_out = nullptr;
+    uint8_t* d_one = nullptr;     // a stream that never reached a piece: its bytes + out, grown on demand
+    uint64_t d_one_cap = 0;
     hipStream_t st = nullptr;
     hipEvent_t ev_copied = nullptr, ev_free[2] = {};
     bool used[2] = {};
@@ -932,8 +936,27 @@ struct oxh_xxh3_stream {
 
 namespace {
 
+// the stream and its events are created on first device use: a short-lived Xxh3 over a small blob
+// (HashingReader / AtomicFile over one received file) pays for neither until its digest
+int stream_queue(oxh_xxh3_stream* s) {
+    if (s->st) return OXH_OK;
+    if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) {
+        s->st = nullptr;
+        (void)hipGetLastError();
+        return fail(OXH_ERR_NOMEM, "stream queue");
+    }
+    return OXH_OK;
+}
+
 int stream_device(oxh_xxh3_stream* s) {
     if (s->d_mem) return OXH_OK;
+    if (int rc = stream_queue(s)) return rc;
+    if (hipEventCreateWithFlags(&s->ev_copied, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&s->ev_free[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&s->ev_free[1], hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(OXH_ERR_NOMEM, "stream events");
+    }
     const uint64_t pb = align_up(s->piece + 1025) + 256, sb = ((s->piece >> 10) + 1) * 64;
     if (hipMalloc(&s->d_mem, 2 * pb + 2 * sb + 256) != hipSuccess) {
         s->d_mem = nullptr;
@@ -946,6 +969,23 @@ int stream_device(oxh_xxh3_stream* s) {
     s->d_sums[1] = reinterpret_cast<uint64_t*>(s->d_mem + 2 * pb + sb);
     s->d_state = reinterpret_cast<uint64_t*>(s->d_mem + 2 * pb + 2 * sb);
     s->d_out = s->d_state + 8;
+    return OXH_OK;
+}
+
+// room for `need` pending bytes (pinned; grown x4 from 64 KiB, capped at S + 1025)
+int stream_reserve(oxh_xxh3_stream* s, uint64_t need) {
+    if (need <= s->h_cap) return OXH_OK;
+    const uint64_t full = s->piece + 1025;
+    const uint64_t cap = std::min(full, std::max({need, 4 * s->h_cap, (uint64_t)64 << 10}));
+    uint8_t* h = nullptr;
+    if (hipHostMalloc(&h, cap, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(OXH_ERR_NOMEM, "stream pending buffer");
+    }
+    if (s->fill) memcpy(h, s->h_pend, s->fill);
+    if (s->h_pend) (void)hipHostFree(s->h_pend);
+    s->h_pend = h;
+    s->h_cap = cap;
     return OXH_OK;
 }
 
@@ -993,32 +1033,24 @@ int stream_flush(oxh_xxh3_stream* s) {
 int oxh_xxh3_stream_create(oxh_ctx* ctx, oxh_xxh3_stream** out) {
     if (!ctx || !out) return fail(OXH_ERR_INVALID, "bad stream arguments");
     *out = nullptr;
-    HIP_TRY(hipSetDevice(ctx->device));
     oxh_xxh3_stream* s = new oxh_xxh3_stream();
     s->device = ctx->device;
     const char* e = getenv("OXH_STREAM_PIECE_MIB");
     const uint64_t kib = e && strtoull(e, nullptr, 10) ? strtoull(e, nullptr, 10) << 10 : 16ull << 10;
     s->piece = kib << 10;  // whole 1 KiB blocks
-    if (hipHostMalloc(&s->h_pend, s->piece + 1025, hipHostMallocDefault) != hipSuccess ||
-        hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&s->ev_copied, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&s->ev_free[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&s->ev_free[1], hipEventDisableTiming) != hipSuccess) {
-        (void)hipGetLastError();
-        oxh_xxh3_stream_destroy(s);
-        return fail(OXH_ERR_NOMEM, "stream buffers");
-    }
-    *out = s;
+    *out = s;              // nothing is allocated until bytes arrive
     return OXH_OK;
 }
 
 int oxh_xxh3_stream_update(oxh_xxh3_stream* s, const void* data, uint64_t len) {
     if (!s || (len && !data)) return fail(OXH_ERR_INVALID, "bad stream update");
+    if (!len) return OXH_OK;
     HIP_TRY(hipSetDevice(s->device));
     const uint8_t* p = (const uint8_t*)data;
     const uint64_t cap = s->piece + 1025;
     while (len) {
         const uint64_t take = std::min(len, cap - s->fill);
+        if (int rc = stream_reserve(s, s->fill + take)) return rc;
         memcpy(s->h_pend + s->fill, p, take);
         s->fill += take;
         s->total += take;
@@ -1033,20 +1065,36 @@ int oxh_xxh3_stream_update(oxh_xxh3_stream* s, const void* data, uint64_t len) {
 int oxh_xxh3_stream_digest(oxh_xxh3_stream* s, uint64_t* out2) {
     if (!s || !out2) return fail(OXH_ERR_INVALID, "bad stream digest");
     HIP_TRY(hipSetDevice(s->device));
-    if (int rc = stream_device(s)) return rc;
-    int b = 0;
-    if (int rc = stream_take_piece(s, b)) return rc;
-    if (s->fill) HIP_TRY(hipMemcpyAsync(s->d_piece[b], s->h_pend, s->fill, hipMemcpyHostToDevice, s->st));
+    if (int rc = stream_queue(s)) return rc;
+    uint64_t* d_out = nullptr;
     if (s->pieces == 0) {  // the whole stream is pending: a one-shot digest (K1, or K1L above 1 MiB)
-        const uint8_t* d = s->d_piece[b];
-        if (int rc = large_batch_device(&d, &s->fill, 1, s->d_out, s->st)) return rc;
-    } else if (int rc = stream_chain(s, b, s->fill, false)) {  // fill >= 1025: the final piece
-        return rc;
+        const uint64_t need = align_up(s->fill + 1) + 256;
+        if (need > s->d_one_cap) {
+            if (s->d_one) (void)hipFree(s->d_one);
+            s->d_one = nullptr, s->d_one_cap = 0;
+            const uint64_t cap = std::max<uint64_t>(need, 64 << 10);
+            if (hipMalloc(&s->d_one, cap) != hipSuccess) {
+                s->d_one = nullptr;
+                (void)hipGetLastError();
+                return fail(OXH_ERR_NOMEM, "stream device buffer");
+            }
+            s->d_one_cap = cap;
+        }
+        d_out = reinterpret_cast<uint64_t*>(s->d_one + s->d_one_cap - 256);
+        if (s->fill) HIP_TRY(hipMemcpyAsync(s->d_one, s->h_pend, s->fill, hipMemcpyHostToDevice, s->st));
+        const uint8_t* d = s->d_one;
+        if (int rc = large_batch_device(&d, &s->fill, 1, d_out, s->st)) return rc;
+    } else {  // fill >= 1025: the final piece
+        int b = 0;
+        if (int rc = stream_take_piece(s, b)) return rc;
+        HIP_TRY(hipMemcpyAsync(s->d_piece[b], s->h_pend, s->fill, hipMemcpyHostToDevice, s->st));
+        if (int rc = stream_chain(s, b, s->fill, false)) return rc;
+        HIP_TRY(hipEventRecord(s->ev_free[b], s->st));
+        s->used[b] = true;
+        d_out = s->d_out;
     }
-    HIP_TRY(hipEventRecord(s->ev_free[b], s->st));
-    s->used[b] = true;
     uint64_t h[2];
-    HIP_TRY(hipMemcpyAsync(h, s->d_out, 16, hipMemcpyDeviceToHost, s->st));
+    HIP_TRY(hipMemcpyAsync(h, d_out, 16, hipMemcpyDeviceToHost, s->st));
     HIP_TRY(hipStreamSynchronize(s->st));
     out2[0] = h[0];
     out2[1] = h[1];
@@ -1065,6 +1113,7 @@ int oxh_xxh3_stream_destroy(oxh_xxh3_stream* s) {
     (void)hipSetDevice(s->device);
     if (s->st) (void)hipStreamSynchronize(s->st);
     if (s->d_mem) (void)hipFree(s->d_mem);
+    if (s->d_one) (void)hipFree(s->d_one);
     if (s->h_pend) (void)hipHostFree(s->h_pend);
     if (s->ev_copied) (void)hipEventDestroy(s->ev_copied);
     for (hipEvent_t e : s->ev_free)
@@ -1868,32 +1917,84 @@ int oxh_hash_files_text_utf8(oxh_ctx* c, const char* const* paths, uint64_t n, u
 }
 
 // util::fs::classify_modified_from_node_with_metadata (util/fs.rs:1580-1619) x n: the size and mtime
-// verdicts are decided on the host from what the caller's walk holds; only the items that reach the
-// content-hash comparison are read, all of them in ONE engine request (oxh_hash_files_meta semantics).
+// verdicts and a caller-computed metadata-hash verdict are decided on the host from what the caller's
+// walk holds; every item that still needs its file read is read ONCE, all of them in ONE engine request
+// (oxh_hash_files_meta semantics), with the text counts of K1T when an item's metadata is MetadataText.
 int oxh_files_modified(oxh_ctx* c, const char* const* paths, const uint64_t* sizes, const uint64_t* node_bytes,
-                       const uint8_t* mtime_matched, const uint64_t* node_hashes, uint64_t n, uint8_t* modified,
-                       int32_t* status, uint64_t* n_hashed) {
+                       const uint8_t* mtime_matched, const uint64_t* node_hashes, const uint8_t* node_meta_present,
+                       const uint64_t* node_meta_hashes, const uint8_t* file_meta_kind, const uint64_t* file_meta_hashes,
+                       uint64_t n, uint8_t* modified, int32_t* status, uint64_t* n_hashed) {
     if (!c || (n && (!paths || !sizes || !node_bytes || !mtime_matched || !node_hashes || !modified)))
         return fail(OXH_ERR_INVALID, "bad arguments");
+    if ((node_meta_present == nullptr) != (node_meta_hashes == nullptr))
+        return fail(OXH_ERR_INVALID, "node_meta_present and node_meta_hashes go together");
     std::vector<uint64_t> idx;
+    bool any_text = false;
     for (uint64_t i = 0; i < n; ++i) {
-        modified[i] = sizes[i] != node_bytes[i] ? 1 : 0;  // fs.rs:1589-1592: no hashing needed
+        const int kind = file_meta_kind ? file_meta_kind[i] : OXH_META_NONE;
+        if (kind > OXH_META_ERROR) return fail(OXH_ERR_INVALID, "file_meta_kind out of range");
+        if (kind == OXH_META_GIVEN && !file_meta_hashes) return fail(OXH_ERR_INVALID, "file_meta_hashes is NULL");
+    }
+    for (uint64_t i = 0; i < n; ++i) {
+        modified[i] = sizes[i] != node_bytes[i] ? 1 : 0;  // fs.rs:1590-1592: no hashing needed
         if (status) status[i] = OXH_OK;
-        if (!modified[i] && !mtime_matched[i]) idx.push_back(i);  // fs.rs:1595-1597: a matched mtime is trusted
+        if (modified[i] || mtime_matched[i]) continue;     // fs.rs:1595-1597: a matched mtime is trusted
+        const int kind = file_meta_kind ? file_meta_kind[i] : OXH_META_NONE;
+        const bool node_has = node_meta_present && node_meta_present[i];
+        if (kind == OXH_META_ERROR) {  // fs.rs:1605-1606: the extraction's `?`
+            if (status) status[i] = OXH_ERR_META;
+            continue;
+        }
+        if (kind == OXH_META_GIVEN && node_has &&
+            (file_meta_hashes[2 * i] != node_meta_hashes[2 * i] || file_meta_hashes[2 * i + 1] != node_meta_hashes[2 * i + 1])) {
+            modified[i] = 1;  // fs.rs:1609-1614, before any read
+            continue;
+        }
+        any_text |= kind == OXH_META_TEXT;
+        idx.push_back(i);
     }
     if (n_hashed) *n_hashed = idx.size();
     if (idx.empty()) return OXH_OK;
     const uint64_t m = idx.size();
     std::vector<const char*> p(m);
-    std::vector<uint64_t> ms(m), out(2 * m);
+    std::vector<uint64_t> ms(m), out(2 * m), cnt(any_text ? 2 * m : 0);
     std::vector<int32_t> st(m, OXH_OK);
     for (uint64_t k = 0; k < m; ++k) p[k] = paths[idx[k]], ms[k] = sizes[idx[k]];
-    const int rc = hash_files_impl(c, p.data(), m, out.data(), nullptr, st.data(), nullptr, nullptr, nullptr, ms.data());
+    int rc = hash_files_impl(c, p.data(), m, out.data(), nullptr, st.data(), any_text ? cnt.data() : nullptr, nullptr,
+                             nullptr, ms.data());
     if (rc) return rc;
+    // MetadataText of the text items whose node has a metadata hash: serde_json of GenericMetadata
+    // (model/metadata/generic_metadata.rs, untagged; MetadataText's field order) hashed in one batch
+    std::vector<uint64_t> tk, toff, tlen;
+    std::string json;
+    for (uint64_t k = 0; k < m; ++k) {
+        const uint64_t i = idx[k];
+        if (st[k] != OXH_OK || !file_meta_kind || file_meta_kind[i] != OXH_META_TEXT) continue;
+        if (!(node_meta_present && node_meta_present[i])) continue;  // None on the node side: no comparison
+        char buf[96];
+        const int len = snprintf(buf, sizeof buf, "{\"text\":{\"num_lines\":%llu,\"num_chars\":%llu}}",
+                                 (unsigned long long)cnt[2 * k], (unsigned long long)cnt[2 * k + 1]);
+        tk.push_back(k), toff.push_back(json.size()), tlen.push_back((uint64_t)len);
+        json.append(buf, (size_t)len);
+    }
+    std::vector<uint64_t> mh(2 * tk.size());
+    if (!tk.empty()) {
+        rc = oxh_hash_streams(c, (const uint8_t*)json.data(), toff.data(), tlen.data(), tk.size(), mh.data());
+        if (rc) return rc;
+    }
+    std::vector<uint8_t> meta_differs(m, 0);
+    for (size_t j = 0; j < tk.size(); ++j) {
+        const uint64_t i = idx[tk[j]];
+        meta_differs[tk[j]] = mh[2 * j] != node_meta_hashes[2 * i] || mh[2 * j + 1] != node_meta_hashes[2 * i + 1];
+    }
     for (uint64_t k = 0; k < m; ++k) {
         const uint64_t i = idx[k];
         if (st[k] != OXH_OK) {  // the reference returns the read error for this path
             if (status) status[i] = st[k];
+            continue;
+        }
+        if (meta_differs[k]) {  // fs.rs:1609-1614
+            modified[i] = 1;
             continue;
         }
         // fs.rs:1616-1618: node.hash() against get_hash_given_metadata(path, metadata)

@@ -132,18 +132,36 @@ def hash_files_given_metadata_128bit(paths: Sequence[str], meta_sizes: Sequence[
     return _u128_list(out, status), [int(s) for s in sizes], [int(s) for s in status]
 
 
+def _split_u128(values) -> np.ndarray:
+    return np.array([(int(h) & 0xFFFFFFFFFFFFFFFF, int(h) >> 64) for h in values], dtype=np.uint64).reshape(-1, 2)
+
+
+TEXT = "text"  # files_modified's file_metadata marker for data type Text (MetadataText counted on the read)
+
+
 def files_modified(paths: Sequence[str], sizes: Sequence[int], node_bytes: Sequence[int],
                    mtime_matched: Sequence[bool], node_hashes: Sequence[int],
-                   ctx: Optional[_capi.Context] = None):
+                   ctx: Optional[_capi.Context] = None, node_metadata_hashes: Optional[Sequence[Optional[int]]] = None,
+                   file_metadata: Optional[Sequence] = None):
     """`classify_modified_from_node_with_metadata` (util/fs.rs:1580-1619) over many working-tree files
     (oxh_files_modified): the modified check `oxen status` runs per tracked file
     (core/v_latest/status.rs:710,734). sizes = the walk's metadata.len(), node_bytes / node_hashes =
-    the committed FileNode's num_bytes / hash (u128), mtime_matched = the caller's mtime verdict.
-    Returns (modified, status, n_hashed): only files with an equal size and a drifted mtime are read,
-    all in one GPU pass; status[i] != 0 is that file's read error (the reference returns it)."""
+    the committed FileNode's num_bytes / hash (u128), mtime_matched = the caller's mtime verdict,
+    node_metadata_hashes[i] = node.metadata_hash() (None or u128; omitted: all None).
+    file_metadata[i] is the working file's side of fs.rs:1600-1607 (omitted: all None):
+      None            no metadata for its data type (maybe_get_metadata_hash -> None)
+      hasher.TEXT     data type Text: MetadataText is counted on the hashing read itself (K1T)
+      int             the metadata hash the caller already extracted
+      dict / object   the GenericMetadata itself (its serde_json is hashed on the device)
+      Exception       the caller's extraction failed (status[i] = OXH_ERR_META, as the reference's `?`)
+    Returns (modified, status, n_hashed): only files with an equal size and a drifted mtime whose
+    metadata hash does not already differ are read, all in one GPU pass; status[i] != 0 is that
+    file's error (the reference returns it)."""
     ctx = ctx or default_context()
     n = len(paths)
     if not (len(sizes) == len(node_bytes) == len(mtime_matched) == len(node_hashes) == n):
+        raise _capi.OxenError("files_modified: argument lengths differ", _capi.OXH_ERR_INVALID)
+    if (node_metadata_hashes is not None and len(node_metadata_hashes) != n) or (file_metadata is not None and len(file_metadata) != n):
         raise _capi.OxenError("files_modified: argument lengths differ", _capi.OXH_ERR_INVALID)
     if n == 0:
         return [], [], 0
@@ -151,22 +169,53 @@ def files_modified(paths: Sequence[str], sizes: Sequence[int], node_bytes: Seque
     sz = np.ascontiguousarray(sizes, dtype=np.uint64)
     nb = np.ascontiguousarray(node_bytes, dtype=np.uint64)
     mm = np.ascontiguousarray([1 if m else 0 for m in mtime_matched], dtype=np.uint8)
-    nh = np.array([(int(h) & 0xFFFFFFFFFFFFFFFF, int(h) >> 64) for h in node_hashes], dtype=np.uint64).reshape(n, 2)
+    nh = _split_u128(node_hashes)
+    nmp = nmh = fk = fh = None
+    if node_metadata_hashes is not None:
+        nmp = np.array([0 if h is None else 1 for h in node_metadata_hashes], dtype=np.uint8)
+        nmh = _split_u128([0 if h is None else h for h in node_metadata_hashes])
+    if file_metadata is not None:
+        fk = np.zeros(n, dtype=np.uint8)
+        fhv = [0] * n
+        objs = []
+        for i, f in enumerate(file_metadata):
+            if f is None:
+                continue
+            if isinstance(f, BaseException):
+                fk[i] = _capi.OXH_META_ERROR
+            elif isinstance(f, str) and f == TEXT:
+                fk[i] = _capi.OXH_META_TEXT
+            elif isinstance(f, (int, np.integer)) and not isinstance(f, bool):
+                fk[i], fhv[i] = _capi.OXH_META_GIVEN, int(f)
+            else:
+                fk[i] = _capi.OXH_META_GIVEN
+                objs.append(i)
+        if objs:  # get_metadata_hash of every GenericMetadata object, one batched GPU pass
+            for i, h in zip(objs, hash_streams_128bit([metadata_json(file_metadata[i]).encode("utf-8") for i in objs], ctx)):
+                fhv[i] = h
+        fh = _split_u128(fhv)
     modified = np.zeros(n, dtype=np.uint8)
     status = np.zeros(n, dtype=np.int32)
     hashed = (ctypes.c_uint64 * 1)()
+    ptr = lambda a: None if a is None else a.ctypes.data  # noqa: E731
     _capi.check(_capi.lib().oxh_files_modified(ctx.handle, arr, sz.ctypes.data_as(_capi._u64p),
                                                nb.ctypes.data_as(_capi._u64p), mm.ctypes.data,
-                                               nh.ctypes.data_as(_capi._u64p), n, modified.ctypes.data,
+                                               nh.ctypes.data_as(_capi._u64p), ptr(nmp), ptr(nmh), ptr(fk), ptr(fh),
+                                               n, modified.ctypes.data,
                                                status.ctypes.data_as(_capi._i32p), hashed), "oxh_files_modified")
     return [bool(m) for m in modified], [int(s) for s in status], int(hashed[0])
 
 
 def classify_modified_from_node_with_metadata(path, node_num_bytes: int, node_hash: int,
-                                              metadata: os.stat_result, mtime_matched: bool) -> bool:
-    """util/fs.rs:1580-1619 for one file (the batched form is files_modified); a read error raises
-    OxenError like the reference's `?` on get_hash_given_metadata."""
-    modified, status, _ = files_modified([path], [metadata.st_size], [node_num_bytes], [mtime_matched], [node_hash])
+                                              metadata: os.stat_result, mtime_matched: bool,
+                                              node_metadata_hash: Optional[int] = None, file_metadata=None) -> bool:
+    """util/fs.rs:1580-1619 for one file (the batched form is files_modified); an extraction or read
+    error raises OxenError like the reference's `?`."""
+    modified, status, _ = files_modified([path], [metadata.st_size], [node_num_bytes], [mtime_matched], [node_hash],
+                                         node_metadata_hashes=[node_metadata_hash], file_metadata=[file_metadata])
+    if status[0] == _capi.OXH_ERR_META:
+        err = file_metadata
+        raise OxenError(str(err) if str(err) else "could not compute file metadata", _capi.OXH_ERR_META)
     if status[0] != 0:
         raise OxenError("Could not read file for hashing", _capi.OXH_ERR_IO)
     return modified[0]
@@ -438,9 +487,9 @@ class HashingWriter:
     def write(self, b: bytes) -> int:
         n = self.inner.write(b)
         if n is None:
-            n = len(b)
-        if n > 0:
-            self.hasher.update(memoryview(b)[:n])
+            n = memoryview(b).nbytes
+        if n > 0:  # n counts bytes: slice the byte view, not the elements of e.g. array('H')
+            self.hasher.update(memoryview(b).cast("B")[:n])
         return n
 
     def flush(self) -> None:

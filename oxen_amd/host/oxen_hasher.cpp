@@ -216,26 +216,36 @@ std::vector<Modified> classify_modified_batch(const std::vector<TrackedFile>& fi
     ctx = ctx ? ctx : hasher::default_context();
     const size_t n = files.size();
     std::vector<const char*> cp(n);
-    std::vector<uint64_t> sizes(n), node_bytes(n), node_hashes(2 * n);
-    std::vector<uint8_t> mtime(n), modified(n);
+    std::vector<uint64_t> sizes(n), node_bytes(n), node_hashes(2 * n), nmh(2 * n), fmh(2 * n);
+    std::vector<uint8_t> mtime(n), modified(n), nmp(n), fk(n);
     std::vector<int32_t> status(n);
     for (size_t i = 0; i < n; ++i) {
-        cp[i] = files[i].path.c_str();
-        sizes[i] = files[i].size;
-        node_bytes[i] = files[i].node_num_bytes;
-        node_hashes[2 * i] = (uint64_t)files[i].node_hash;
-        node_hashes[2 * i + 1] = (uint64_t)(files[i].node_hash >> 64);
-        mtime[i] = files[i].mtime_matched ? 1 : 0;
+        const TrackedFile& f = files[i];
+        cp[i] = f.path.c_str();
+        sizes[i] = f.size;
+        node_bytes[i] = f.node_num_bytes;
+        node_hashes[2 * i] = (uint64_t)f.node_hash;
+        node_hashes[2 * i + 1] = (uint64_t)(f.node_hash >> 64);
+        mtime[i] = f.mtime_matched ? 1 : 0;
+        nmp[i] = f.node_metadata_hash.has_value();
+        const u128 h = f.node_metadata_hash.value_or(0);
+        nmh[2 * i] = (uint64_t)h, nmh[2 * i + 1] = (uint64_t)(h >> 64);
+        fk[i] = f.file_metadata.kind;
+        fmh[2 * i] = (uint64_t)f.file_metadata.hash, fmh[2 * i + 1] = (uint64_t)(f.file_metadata.hash >> 64);
     }
     uint64_t hashed = 0;
-    check(oxh_files_modified(ctx, cp.data(), sizes.data(), node_bytes.data(), mtime.data(), node_hashes.data(), n,
-                             modified.data(), status.data(), &hashed),
+    check(oxh_files_modified(ctx, cp.data(), sizes.data(), node_bytes.data(), mtime.data(), node_hashes.data(), nmp.data(),
+                             nmh.data(), fk.data(), fmh.data(), n, modified.data(), status.data(), &hashed),
           "oxh_files_modified");
     if (n_hashed) *n_hashed = hashed;
     std::vector<Modified> r(n);
     for (size_t i = 0; i < n; ++i) {
         r[i].modified = modified[i] != 0;
-        if (status[i] != OXH_OK) {
+        r[i].code = status[i];
+        if (status[i] == OXH_ERR_META) {
+            r[i].ok = false;
+            r[i].error = files[i].file_metadata.error.empty() ? "could not compute file metadata" : files[i].file_metadata.error;
+        } else if (status[i] != OXH_OK) {
             r[i].ok = false;
             r[i].error = "Could not read file for hashing";  // hasher.rs:136-139
         }
@@ -244,10 +254,11 @@ std::vector<Modified> classify_modified_batch(const std::vector<TrackedFile>& fi
 }
 
 bool classify_modified_from_node_with_metadata(const std::string& path, uint64_t node_num_bytes, u128 node_hash,
-                                               const struct stat& metadata, bool mtime_matched) {
-    const std::vector<Modified> r =
-        classify_modified_batch({TrackedFile{path, (uint64_t)metadata.st_size, node_num_bytes, node_hash, mtime_matched}});
-    if (!r[0].ok) throw OxenError::basic_str(r[0].error, OXH_ERR_IO);
+                                               const struct stat& metadata, bool mtime_matched,
+                                               std::optional<u128> node_metadata_hash, const FileMetadataHash& file_metadata) {
+    TrackedFile t{path, (uint64_t)metadata.st_size, node_num_bytes, node_hash, mtime_matched, node_metadata_hash, file_metadata};
+    const std::vector<Modified> r = classify_modified_batch({t});
+    if (!r[0].ok) throw OxenError::basic_str(r[0].error, r[0].code);
     return r[0].modified;
 }
 

@@ -18,8 +18,7 @@
 #include <string_view>
 #include <vector>
 
-struct oxh_ctx;
-struct oxh_xxh3_stream;
+#include "../../include/oxen_hash.h"
 
 namespace liboxen {
 
@@ -160,25 +159,43 @@ namespace util::fs {
 // One tracked working-tree file as `oxen status`'s walk holds it (core/v_latest/status.rs:690-745):
 // metadata.len(), the committed FileNode's num_bytes and hash, and the caller's mtime verdict
 // (LocalRepository::mtime_matches, model/repository/local_repository.rs:601-615).
+// The working file's side of the metadata-hash comparison (util/fs.rs:1600-1607):
+// maybe_get_metadata_hash(get_file_metadata(path, data_type)).
+struct FileMetadataHash {
+    enum Kind : uint8_t {
+        None = OXH_META_NONE,    // no metadata for the file's data type
+        Given = OXH_META_GIVEN,  // the caller extracted it: `hash`
+        Text = OXH_META_TEXT,    // data type Text: MetadataText counted on the hashing read (K1T)
+        Error = OXH_META_ERROR,  // the caller's extraction failed: `error`
+    } kind = None;
+    u128 hash = 0;
+    std::string error;
+};
 struct TrackedFile {
     std::string path;
     uint64_t size = 0;
     uint64_t node_num_bytes = 0;
     u128 node_hash = 0;
     bool mtime_matched = false;
+    std::optional<u128> node_metadata_hash;  // node.metadata_hash()
+    FileMetadataHash file_metadata;
 };
 struct Modified {
-    bool ok = true;         // false: the file had to be hashed and could not be read
+    bool ok = true;         // false: metadata extraction failed, or the file had to be read and could not be
     bool modified = false;
+    int code = OXH_OK;
     std::string error;
 };
 // classify_modified_from_node_with_metadata (util/fs.rs:1580-1619) x n through oxh_files_modified:
-// only files of an unchanged size with a drifted mtime are read, all in one GPU request.
+// size, mtime and a caller-given metadata hash decide first; the files that remain are read once,
+// all in one GPU request (text files' MetadataText counted on that read).
 std::vector<Modified> classify_modified_batch(const std::vector<TrackedFile>& files, oxh_ctx* ctx = nullptr,
                                               uint64_t* n_hashed = nullptr);
-// One file; a read error throws OxenError, as the reference's `?` does.
+// One file; an extraction or read error throws OxenError, as the reference's `?` does.
 bool classify_modified_from_node_with_metadata(const std::string& path, uint64_t node_num_bytes, u128 node_hash,
-                                               const struct stat& metadata, bool mtime_matched);
+                                               const struct stat& metadata, bool mtime_matched,
+                                               std::optional<u128> node_metadata_hash = std::nullopt,
+                                               const FileMetadataHash& file_metadata = FileMetadataHash());
 
 // util/fs/atomic_file.rs: AtomicFile with an expected hash -- verify-before-publish. Bytes go to an
 // AtomicTempFile sibling `<target>.oxentmp.<random>` (:54-159) while a GPU Xxh3 stream (oxh_xxh3_stream)

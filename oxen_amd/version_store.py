@@ -106,8 +106,8 @@ class AtomicFile:
     def stream(self, reader) -> None:
         """stream / stream_async: `reader.read(n)` (b"" at EOF) in STREAMING_BUF_SIZE pieces."""
         tmp = _TempFile(self.target)
+        h = hasher.Xxh3(self.ctx) if self.expected is not None else None
         try:
-            h = hasher.Xxh3(self.ctx) if self.expected is not None else None
             while True:
                 chunk = reader.read(STREAMING_BUF_SIZE)
                 if not chunk:
@@ -117,11 +117,12 @@ class AtomicFile:
                 tmp.write_all(chunk)
             if h is not None:
                 actual = h.digest128()
-                h.close()
                 if actual != self.expected:
                     raise HashMismatchError(self.target, self.expected, actual)
             tmp.commit()
         finally:
+            if h is not None:
+                h.close()  # the device stream is released now, not at garbage collection
             tmp.discard()
 
     def write(self, data: bytes) -> None:

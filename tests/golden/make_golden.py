@@ -97,7 +97,9 @@ def main() -> None:
                     continue
                 rel = os.path.relpath(p, dt_src)
                 data = open(p, "rb").read()
-                copied = len(data) <= 65536
+                # data fixtures only: the text of a reference source file or script is never copied
+                # (its digest stays; tests read the original from /root/reference when present)
+                copied = len(data) <= 65536 and not fn.endswith((".py", ".sh", ".rs", ".js", ".ts"))
                 if copied:
                     q = os.path.join(dt_dst, rel)
                     os.makedirs(os.path.dirname(q), exist_ok=True)

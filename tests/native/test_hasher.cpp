@@ -243,6 +243,29 @@ static void modified_check(const std::string& golden) {
     CHECK(stat(hello.c_str(), &sb) == 0 && !fs::classify_modified_from_node_with_metadata(hello, 5, h, sb, false));
     CHECK(throws_oxen([&] { fs::classify_modified_from_node_with_metadata(golden + "/no/such/file", (uint64_t)sb.st_size, h, sb, false); },
                       "Could not read file for hashing"));
+
+    // the metadata-hash step (fs.rs:1599-1614): hello.txt is MetadataText {1 line, 5 chars}
+    const u128 mh = liboxen::util::hasher::get_metadata_hash(std::string("{\"text\":{\"num_lines\":1,\"num_chars\":5}}"));
+    fs::FileMetadataHash text, given_stale, err;
+    text.kind = fs::FileMetadataHash::Text;
+    given_stale.kind = fs::FileMetadataHash::Given, given_stale.hash = mh + 1;
+    err.kind = fs::FileMetadataHash::Error, err.error = "no extractor";
+    std::vector<fs::TrackedFile> m = {
+        {hello, 5, 5, h, false, mh, text},            // counted on the read: equal -> content: clean
+        {hello, 5, 5, h, false, mh + 7, text},        // stale node metadata hash, same content: modified
+        {hello, 5, 5, h, false, std::nullopt, text},  // node has none: no comparison, clean
+        {hello, 5, 5, h, false, mh, given_stale},     // caller-given differs: modified, not read
+        {hello, 5, 5, h, false, mh, err},             // extraction error: returned, not read
+    };
+    const std::vector<fs::Modified> q = fs::classify_modified_batch(m, nullptr, &hashed);
+    CHECK(hashed == 3);
+    CHECK(q[0].ok && !q[0].modified);
+    CHECK(q[1].ok && q[1].modified);
+    CHECK(q[2].ok && !q[2].modified);
+    CHECK(q[3].ok && q[3].modified);
+    CHECK(!q[4].ok && q[4].code == OXH_ERR_META && q[4].error == "no extractor");
+    CHECK(fs::classify_modified_from_node_with_metadata(hello, 5, h, sb, false, mh + 7, text));
+    CHECK(throws_oxen([&] { fs::classify_modified_from_node_with_metadata(hello, 5, h, sb, false, mh, err); }, "no extractor"));
 }
 
 static std::vector<std::string> list_dir(const std::string& d) {

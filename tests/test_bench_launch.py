@@ -1,0 +1,102 @@
+"""bench.py's multi-GPU launch (one process per GPU: `--gpus N` starts the N ranks itself when no
+launcher set WORLD_SIZE) and the RCCL leg of the N > 1 step (shard.PipelinedGather on "nccl")."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _run(args, env=None, timeout=300):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, BENCH] + args, env=e, capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_rejects_bad_gpu_counts():
+    r = _run(["--gpus", "0"])
+    assert r.returncode == 2
+    r = _run(["--gpus", "2"], env={"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "WORLD_SIZE=3 but --gpus 2" in r.stderr
+
+
+def test_bench_launches_ranks_and_propagates_failure():
+    """Without a GPU (or with fewer GPUs than ranks) every spawned rank refuses to put two RCCL ranks
+    on one device; the launcher exits non-zero instead of reporting a one-GPU number."""
+    import torch
+
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("enough GPUs for a real 2-rank run")
+    r = _run(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--workload", "t"])
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert r.stderr.count("RCCL needs one GPU per rank") == 2
+    assert not r.stdout.strip()
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_gloo_one_gpu(cuda):
+    """`bench.py --gpus 2` spawns two ranks itself (gloo rehearsal on the one GPU of the test box):
+    the JSON line reports n_gpus 2 and rank 0 checked both ranks' digests against the oracle."""
+    r = _run(["--gpus", "2", "--backend", "gloo", "--workload", "t", "--steps", "3", "--warmup", "1",
+              "--no-cpu-baseline"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, r.stdout
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 3 and d["config"]["items_per_gpu"] == 2048
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.gpu
+def test_pipelined_gather_rccl_in_process(cuda, oracle_lib):
+    """The RCCL leg of C4 in the GPU suite: an in-process "nccl" group of world size 1, bench.py's
+    pipelined step (K1 into one of two digest tables while the previous table's all-gather runs on
+    RCCL's stream) for several steps; every gathered table equals the local K1 digests, which equal
+    the oracle on a sample."""
+    import torch
+    import torch.distributed as dist
+
+    from oxen_amd.device import DeviceArena, to_numpy_u64
+    from oxen_amd.shard import PipelinedGather
+
+    dist.init_process_group("nccl", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{_free_port()}",
+                            device_id=cuda)
+    try:
+        rng = np.random.default_rng(11)
+        lens = rng.integers(0, 300_000, 3000).astype(np.uint64)
+        da = DeviceArena.splitmix(lens, seed=19, device=cuda)
+        ref = torch.empty((len(lens), 2), dtype=torch.int64, device=cuda)
+        da.hash(ref)
+        pipe = PipelinedGather(len(lens), 1, cuda)
+        fulls = []
+        for _ in range(6):
+            b, local = pipe.next_local()
+            local.zero_()
+            da.hash(local)
+            fulls.append(pipe.gather(b))
+        pipe.drain()
+        torch.cuda.synchronize()
+        want = to_numpy_u64(ref).reshape(-1, 2)
+        for f in fulls[-2:]:  # the two tables still holding their last step's gather
+            assert np.array_equal(to_numpy_u64(f).reshape(-1, 2), want)
+        host = da.arena.cpu().numpy()
+        idx = rng.choice(len(lens), 200, replace=False)
+        got = oracle_lib.batch(host, da.offsets_host[idx], da.lens_host[idx])
+        assert np.array_equal(got, want[idx])
+    finally:
+        dist.destroy_process_group()

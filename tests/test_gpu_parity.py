@@ -820,6 +820,83 @@ def test_files_modified_status_check(oracle_lib, tmp_path, cuda):
     assert modified[-3] is True  # the oversize file with one changed byte
 
 
+def _text_meta_hash(oracle_lib, data: bytes) -> int:
+    """maybe_get_metadata_hash(MetadataText) restated: count_lines (util/fs.rs:217-263, with_chars,
+    no trailing-line removal) -> serde_json -> XXH3-128 (hasher.rs:95-100), on the oracle."""
+    lines = 1 + data.count(b"\n")
+    chars = sum(1 for b in data if (b & 0xC0) != 0x80)
+    return oracle_lib.xxh3_128_int(('{"text":{"num_lines":%d,"num_chars":%d}}' % (lines, chars)).encode())
+
+
+def test_files_modified_metadata_hash_step(oracle_lib, tmp_path, cuda):
+    """The metadata-hash step of classify_modified_from_node_with_metadata (util/fs.rs:1599-1614):
+    with the size equal and the mtime drifted, node.metadata_hash() and the working file's
+    maybe_get_metadata_hash are compared BEFORE the content hash -- both Some and different gives
+    modified even when the content is unchanged; an extraction error is returned. Every combination
+    of node side (None / the right hash / a stale hash) and file side (None, caller-given equal or
+    different, Text counted on the read, extraction error) against fs.rs restated over the oracle."""
+    from oxen_amd import _capi, hasher
+
+    rng = np.random.default_rng(23)
+    texts = [b"", b"one line", b"a\nb\nc\n", "naïve café ✓\n".encode() * 40, b"x" * 70_000 + b"\n"]
+    blobs = texts + [rng.integers(0, 256, int(n), dtype=np.uint8).tobytes() for n in (1, 777, 65_536)]
+    paths = []
+    for k, b in enumerate(blobs):
+        p = tmp_path / f"m{k}.dat"
+        p.write_bytes(b)
+        paths.append(str(p))
+    rows = []  # (path index, node meta, file meta, content edited)
+    for k, b in enumerate(blobs):
+        right = _text_meta_hash(oracle_lib, b)
+        for node_meta in (None, right, right ^ (1 << 100)):
+            for file_meta in (None, right, right ^ 5, hasher.TEXT, RuntimeError("bad metadata")):
+                rows.append((k, node_meta, file_meta))
+    # same-size content edits of two files (the node hashes stay the committed ones)
+    committed = [oracle_lib.xxh3_128_int(b) for b in blobs]
+    for k in (3, 6):
+        b = bytearray(blobs[k])
+        b[len(b) // 2] ^= 0x01
+        open(paths[k], "wb").write(bytes(b))
+    now = [open(p, "rb").read() for p in paths]
+
+    def want_of(k, node_meta, file_meta):
+        if isinstance(file_meta, Exception):
+            return False, _capi.OXH_ERR_META
+        if file_meta is hasher.TEXT:
+            file_meta = _text_meta_hash(oracle_lib, now[k])
+        if node_meta is not None and file_meta is not None and node_meta != file_meta:
+            return True, 0
+        return oracle_lib.xxh3_128_int(now[k]) != committed[k], 0
+
+    idx = [r[0] for r in rows]
+    want = [want_of(*r) for r in rows]
+    with _capi.Context(0, staging_bytes=1 << 20) as c:
+        modified, status, n_hashed = hasher.files_modified(
+            [paths[k] for k in idx], [len(now[k]) for k in idx], [len(blobs[k]) for k in idx], [False] * len(rows),
+            [committed[k] for k in idx], c, node_metadata_hashes=[r[1] for r in rows], file_metadata=[r[2] for r in rows])
+        assert modified == [w[0] for w in want]
+        assert status == [w[1] for w in want]
+        # read: everything but extraction errors and caller-given metadata that already differs
+        assert n_hashed == sum(1 for r in rows if not isinstance(r[2], Exception)
+                               and not (isinstance(r[2], int) and r[1] is not None and r[1] != r[2]))
+        # unchanged content, stale node metadata hash -> modified (the case the content check alone misses)
+        k = 0
+        st = os.stat(paths[k])
+        assert hasher.classify_modified_from_node_with_metadata(paths[k], len(blobs[k]), committed[k], st, False,
+                                                                node_metadata_hash=123, file_metadata=hasher.TEXT)
+        assert not hasher.classify_modified_from_node_with_metadata(paths[k], len(blobs[k]), committed[k], st, False,
+                                                                    node_metadata_hash=None, file_metadata=hasher.TEXT)
+        with pytest.raises(_capi.OxenError) as e:
+            hasher.classify_modified_from_node_with_metadata(paths[k], len(blobs[k]), committed[k], st, False,
+                                                             file_metadata=ValueError("no extractor"))
+        assert e.value.code == _capi.OXH_ERR_META and "no extractor" in str(e.value)
+        # a GenericMetadata object on the file side is hashed as serde_json, like get_metadata_hash
+        meta = {"text": {"num_lines": 1, "num_chars": 0}}
+        assert not hasher.classify_modified_from_node_with_metadata(paths[0], 0, committed[0], os.stat(paths[0]), False,
+                                                                    node_metadata_hash=_text_meta_hash(oracle_lib, b""),
+                                                                    file_metadata=meta)
+
+
 @pytest.mark.parametrize("mode", ["short", "packed", "auto"])
 def test_k1_many_ragged_items(cuda, oracle_lib, mode):
     """Many ragged, byte-packed items (FastCDC-chunk-like, with short-path items mixed in): the

@@ -66,6 +66,44 @@ def test_sync_writer_hashes_only_accepted_bytes(cuda, oracle_lib):  # hasher.rs:
     assert w.write(b"0123456789") == 4
     assert inner.written == b"0123" and w.digest128() == oracle_lib.xxh3_128_int(b"0123")
 
+    # a non-byte buffer: the count is bytes, and exactly those bytes are hashed
+    import array
+
+    class ByteShortWriter(ShortWriter):
+        def write(self, b):
+            raw = memoryview(b).cast("B")
+            self.written += bytes(raw[:6])
+            return min(6, raw.nbytes)
+
+    inner = ByteShortWriter()
+    w = hasher.HashingWriter(inner)
+    a = array.array("H", [1, 2, 3, 4, 5])
+    assert w.write(a) == 6
+    assert w.digest128() == oracle_lib.xxh3_128_int(a.tobytes()[:6]) and inner.written == a.tobytes()[:6]
+    w = hasher.HashingWriter(io.BytesIO())
+    w.write(a)  # BytesIO returns the byte count
+    assert w.digest128() == oracle_lib.xxh3_128_int(a.tobytes())
+
+
+def test_many_short_lived_streams(cuda, oracle_lib):
+    """Xxh3 streams are cheap until bytes arrive (pending buffer grown on demand, device memory for a
+    one-shot digest only): many tiny streams, an empty one, and one that crosses into pieces."""
+    from oxen_amd import hasher
+
+    for k in range(300):
+        h = hasher.Xxh3()
+        data = bytes([k % 251]) * (k * 7)
+        h.update(data)
+        assert h.digest128() == oracle_lib.xxh3_128_int(data)
+        h.close()
+    h = hasher.Xxh3()
+    assert h.digest128() == oracle_lib.xxh3_128_int(b"")
+    data = bytes(range(256)) * (70 * 1024)  # 17.5 MiB: one 16 MiB piece, then the final one
+    for i in range(0, len(data), 100_000):
+        h.update(data[i:i + 100_000])
+    assert h.digest128() == oracle_lib.xxh3_128_int(data)
+    h.close()
+
 
 @pytest.mark.parametrize("piece_mib", ["1", None], ids=["1MiB-pieces", "16MiB-pieces"])
 def test_stream_pieces_ragged_updates_and_mid_stream_digests(cuda, oracle_lib, monkeypatch, piece_mib):

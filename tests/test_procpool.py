@@ -1,7 +1,8 @@
-"""oxen_amd.procpool.ShardedFileHasher: the file list split over worker processes (packed paths in
-shared memory, per-worker char* tables, outputs written in place). The pool mechanics are checked on
-CPU with the oracle's restated reference loop in the workers; the GPU test runs the real engines."""
+"""The C ABI's reader-process pool (oxh_pool_*, oxen_amd/csrc/reader_pool.cpp + oxh_hash_helper) and its
+Python mirror oxen_amd.procpool.ShardedFileHasher: the file list split over helper processes, each
+with its own context (device p % ndevices), paths and outputs in one shared region."""
 import os
+import signal
 
 import numpy as np
 import pytest
@@ -29,30 +30,78 @@ def test_pack_paths_roundtrip():
     assert [b[o:b.index(b"\0", o)].decode() for o in offs.tolist()] == ps
 
 
-def test_pool_mechanics_with_the_cpu_loop(tmp_path, oracle_lib):
+def test_pool_helper_is_built(built_lib):
+    from oxen_amd import build
+
+    assert os.access(build.HELPER, os.X_OK)
+
+
+def test_pool_fails_loudly_without_a_gpu(built_lib):
+    """On a host without a gfx950 device every helper reports OXH_ERR_NODEVICE and creation fails with
+    it (no CPU fallback); the helpers are reaped."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    from oxen_amd import _capi
     from oxen_amd.procpool import ShardedFileHasher
 
-    paths = _tree(tmp_path)
-    want_out, want_sizes, want_st = oracle_lib.hash_files(paths, threads=2)
-    meta = [os.path.getsize(p) if os.path.exists(p) else 0 for p in paths]
-    with ShardedFileHasher(procs=3, threads=2, mode="cpu") as pool:
-        for m in (None, meta):
-            out, sizes, st = pool.hash_files(paths, m)
-            assert np.array_equal(out[:-1], want_out[:-1]) and st[-1] != 0 and (st[:-1] == 0).all()
-            assert np.array_equal(sizes[:-1], want_sizes[:-1])
-        out, sizes, st = pool.hash_files(paths[:2])  # fewer files than workers
-        assert np.array_equal(out, want_out[:2])
+    with pytest.raises(_capi.OxenError) as e:
+        ShardedFileHasher(procs=2)
+    assert e.value.code == _capi.OXH_ERR_NODEVICE, str(e.value)
+
+
+def test_pool_rejects_bad_arguments(built_lib, monkeypatch):
+    from oxen_amd import _capi
+    from oxen_amd.procpool import ShardedFileHasher
+
+    with pytest.raises(_capi.OxenError):
+        ShardedFileHasher(procs=0)
+    monkeypatch.setenv("OXH_HELPER", "/nonexistent/oxh_hash_helper")
+    with pytest.raises(_capi.OxenError) as e:
+        ShardedFileHasher(procs=1)
+    assert "helper not found" in str(e.value)
 
 
 @pytest.mark.gpu
-def test_sharded_gpu_engines_match_oracle(cuda, tmp_path, oracle_lib):
+@pytest.mark.parametrize("procs,devices", [(2, (0,)), (3, (0, 0))])
+def test_sharded_gpu_engines_match_oracle(cuda, tmp_path, oracle_lib, procs, devices):
     from oxen_amd.procpool import ShardedFileHasher
 
     paths = _tree(tmp_path, 2000)
-    want_out, _, _ = oracle_lib.hash_files(paths, threads=4)
+    want_out, want_sizes, _ = oracle_lib.hash_files(paths, threads=4)
     meta = [os.path.getsize(p) if os.path.exists(p) else 0 for p in paths]
-    with ShardedFileHasher(procs=2, threads=4, staging_bytes=8 << 20) as pool:
+    with ShardedFileHasher(procs=procs, devices=devices, threads=4, staging_bytes=8 << 20) as pool:
+        pids = pool.pids()
+        assert len(set(pids)) == procs and os.getpid() not in pids
         for m in (None, meta):
             out, sizes, st = pool.hash_files(paths, m)
             assert (st[:-1] == 0).all() and st[-1] != 0
             assert np.array_equal(out[:-1], want_out[:-1]) and (out[-1] == 0).all()
+            assert np.array_equal(sizes[:-1], want_sizes[:-1])
+        out, _, st = pool.hash_files(paths[:1])  # fewer files than helpers
+        assert np.array_equal(out, want_out[:1]) and st[0] == 0
+        out, _, _ = pool.hash_files(paths * 3)  # the shared region grows (helpers re-map it)
+        assert np.array_equal(out[:-1][: len(paths) - 1], want_out[:-1])
+        assert np.array_equal(out[2 * len(paths):2 * len(paths) + len(paths) - 1], want_out[:-1])
+        assert pool.hash_files([])[0].shape == (0, 2)
+
+
+@pytest.mark.gpu
+def test_pool_helper_death_breaks_the_pool(cuda, tmp_path):
+    """A helper that dies fails the call and every later one (no stale replies, no partial outputs)."""
+    from oxen_amd import _capi
+    from oxen_amd.procpool import ShardedFileHasher
+
+    paths = _tree(tmp_path, 50)
+    pool = ShardedFileHasher(procs=2, threads=2, staging_bytes=8 << 20)
+    try:
+        pool.hash_files(paths)
+        os.kill(pool.pids()[1], signal.SIGKILL)
+        with pytest.raises(_capi.OxenError):
+            pool.hash_files(paths)
+        with pytest.raises(_capi.OxenError) as e:
+            pool.hash_files(paths)
+        assert "unusable" in str(e.value)
+    finally:
+        pool.close()

@@ -44,6 +44,8 @@ def sharded(a, paths, meta, nbytes, cpu_call, drop_cache):
     rounds + one cold run each; digests checked against the one-process CPU loop."""
     import numpy as np
 
+    from cpu_procpool import CpuShardedLoop
+
     from oxen_amd.procpool import ShardedFileHasher, pack_paths
 
     res = {}
@@ -51,7 +53,7 @@ def sharded(a, paths, meta, nbytes, cpu_call, drop_cache):
     blob, offs = pack_paths(paths)  # packed once, outside the timing (as c_paths is)
     for P in [int(x) for x in a.procs.split(",") if x]:
         th = max(1, a.threads // P)
-        pools = {"gpu": ShardedFileHasher(procs=P, threads=th), "cpu": ShardedFileHasher(procs=P, threads=th, mode="cpu")}
+        pools = {"gpu": ShardedFileHasher(procs=P, threads=th), "cpu": CpuShardedLoop(procs=P, threads=th)}
         try:
             ts = {"gpu": [], "cpu": []}
             ok = True
