@@ -28,6 +28,7 @@
 #include <condition_variable>
 #include <functional>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <random>
 #include <set>
@@ -622,44 +623,70 @@ struct LargeResult {
     int status = OXH_OK;  // this item's status: OXH_OK, OXH_ERR_IO or OXH_ERR_NOMEM
 };
 
-// Hash one large item of L bytes from `src` (see above). Returns a run-level error code only for
-// HIP failures; the item's own outcome (I/O error, allocation failure) is res.status.
-int large_item(oxh_ctx* c, uint64_t L, LargeSource& src, bool want_counts, bool want_utf8, ItemSink* sink, uint64_t id,
-               LargeResult& res) {
+// One large item of a large_items() batch: its source and what the caller wants, then the outcome.
+struct LargeJob {
+    uint64_t L = 0;
+    LargeSource* src = nullptr;
+    bool want_counts = false, want_utf8 = false;
+    ItemSink* sink = nullptr;
+    uint64_t id = 0;
+    LargeResult res;
+};
+
+// Files up to this many at a time share one large-item pipeline (OXH_BIG_FILES overrides; device
+// memory: 2 piece buffers of OXH_BIG_PIECE_MIB + 1 KiB per file).
+int big_files_at_once() {
+    const char* e = getenv("OXH_BIG_FILES");
+    const int v = e && atoi(e) > 0 ? atoi(e) : 4;
+    return std::min(v, (int)oxh::kChainJobs);
+}
+
+// Hash n (<= kChainJobs) large items side by side (see above). Round r moves piece r of every item
+// that has one to the device (the copies are PCIe-bound and serial on the copy stream), launches its
+// block sums chip-wide, and then ONE chain launch continues every item's serial chain over its piece
+// (the chains are latency-bound: 16 files' chains cost about what one does). The chains of round r
+// run on the device while the host moves round r+1's pieces, so the chain time hides behind the
+// copies of the next round instead of adding up file after file. Returns a run-level error code only
+// for HIP failures; each item's own outcome (I/O error, allocation failure) is its res.status.
+int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
+    if (n <= 0) return OXH_OK;
+    if (n > (int)oxh::kChainJobs) return fail(OXH_ERR_INVALID, "too many large items in one batch");
     const uint64_t P = std::max<uint64_t>(
         1, getenv("OXH_BIG_PIECE_MIB") ? strtoull(getenv("OXH_BIG_PIECE_MIB"), nullptr, 10) : 1024) << 20;
-    // pieces 0 .. k-1 hold P bytes each; the last one L - k*P bytes, in [1025, P + 1024]
-    const uint64_t k = L > P + 1024 ? (L - 1025) / P : 0;
     const uint64_t cap = P + 1024;  // bytes per piece buffer
     const uint64_t slot = align_up(cap) + 256;
-    // an allocation that fails is this item's failure (OXH_ERR_NOMEM), not the engine run's: the
+    constexpr uint64_t kRes = 256;  // per item: [digest 2 | counts 2 | desc off, len | utf8 | state 8]
+    // an allocation that fails is these items' failure (OXH_ERR_NOMEM), not the engine run's: the
     // other requests in the live pipeline carry on
     auto nomem = [&]() {
         (void)hipGetLastError();
-        res.status = OXH_ERR_NOMEM;
+        for (int q = 0; q < n; ++q) jobs[q].res.status = OXH_ERR_NOMEM;
         return OXH_OK;
     };
-    if (c->d_big_size < 2 * slot + 4096) {
+    const uint64_t need = (uint64_t)n * (2 * slot + kRes) + 4096;
+    if (c->d_big_size < need) {
         if (c->d_big) {
             HIP_TRY(hipDeviceSynchronize());
             (void)hipFree(c->d_big);
             c->d_big = nullptr;
             c->d_big_size = 0;
         }
-        if (hipMalloc(&c->d_big, 2 * slot + 4096) != hipSuccess) {
+        if (hipMalloc(&c->d_big, need) != hipSuccess) {
             c->d_big = nullptr;
             return nomem();
         }
-        c->d_big_size = 2 * slot + 4096;
+        c->d_big_size = need;
     }
-    uint8_t* dbuf[2] = {c->d_big, c->d_big + slot};
-    // results area: [digest 2 | counts 2 | desc off, len | utf8 | state 8]
-    uint64_t* d_res = reinterpret_cast<uint64_t*>(c->d_big + 2 * slot);
+    auto dbuf = [&](int q, int b) { return c->d_big + ((uint64_t)q * 2 + b) * slot; };
+    uint8_t* d_res_all = c->d_big + (uint64_t)n * 2 * slot;
+    auto d_res = [&](int q) { return reinterpret_cast<uint64_t*>(d_res_all + (uint64_t)q * kRes); };
     struct Res {
         uint64_t out[2], cnt[2], off, len;
         int32_t utf8, pad;
-    } h{};
-    h.len = L;
+    };
+    static_assert(sizeof(Res) + 64 <= kRes, "results area");
+    std::vector<uint8_t> h_res((size_t)n * kRes, 0);
+    for (int q = 0; q < n; ++q) reinterpret_cast<Res*>(h_res.data() + (size_t)q * kRes)->len = jobs[q].L;
     for (int b = 0; b < 2; ++b) {
         if (!c->h_bounce[b] && hipHostMalloc(&c->h_bounce[b], kBounce, hipHostMallocDefault) != hipSuccess) {
             c->h_bounce[b] = nullptr;
@@ -669,102 +696,139 @@ int large_item(oxh_ctx* c, uint64_t L, LargeSource& src, bool want_counts, bool 
         if (!c->ev_piece_free[b]) HIP_TRY(hipEventCreateWithFlags(&c->ev_piece_free[b], hipEventDisableTiming));
     }
     uint64_t* sums = nullptr;
-    oxh::ScratchLease lease(c->stream);  // block sums of the two pieces in flight
+    oxh::ScratchLease lease(c->stream);  // block sums of the two rounds in flight
     const uint64_t sums_per = (cap >> 10) * 8;
-    if (lease.get(2 * sums_per * 8, (void**)&sums) != hipSuccess) return nomem();
-    HIP_TRY(hipMemcpyAsync(d_res, &h, sizeof h, hipMemcpyHostToDevice, c->stream));
+    if (lease.get(2 * sums_per * 8 * (uint64_t)n, (void**)&sums) != hipSuccess) return nomem();
+    HIP_TRY(hipMemcpyAsync(d_res_all, h_res.data(), h_res.size(), hipMemcpyHostToDevice, c->stream));
 
-    std::string sink_tmp;
-    int sfd = -1;
-    std::atomic<bool> sink_ok{true};
-    if (sink) {
-        sfd = sink->open_stream(id, sink_tmp);
-        if (sfd < 0) sink_ok.store(false);
+    struct State {
+        uint64_t k = 0;  // pieces 0 .. k-1 hold P bytes each; the last one L - k*P bytes, in [1025, P + 1024]
+        std::string sink_tmp;
+        int sfd = -1;
+        std::atomic<bool> sink_ok{true};
+        bool io_ok = true;
+    };
+    std::vector<State> st(n);
+    uint64_t rounds = 0;
+    for (int q = 0; q < n; ++q) {
+        const uint64_t L = jobs[q].L;
+        st[q].k = L > P + 1024 ? (L - 1025) / P : 0;
+        rounds = std::max(rounds, st[q].k + 1);
+        if (jobs[q].sink) {
+            st[q].sfd = jobs[q].sink->open_stream(jobs[q].id, st[q].sink_tmp);
+            if (st[q].sfd < 0) st[q].sink_ok.store(false);
+        }
     }
     int rc = OXH_OK;
-    bool io_ok = true, piece_used[2] = {false, false};
-    // piece [off, off + plen) -> device buffer d on the copy stream; false on an I/O error
-    auto copy_piece = [&](uint64_t off, uint64_t plen, uint8_t* d) -> bool {
-        if (!sink && src.direct(c, off, plen, d)) return true;  // a sink must see the bytes on the host
-        for (uint64_t o = 0, q = 0; o < plen; o += kBounce, ++q) {  // bounce-buffer path
-            const int bb = (int)(q & 1);
+    // piece [off, off + plen) of item q -> device buffer d on the copy stream; false on an I/O error
+    auto copy_piece = [&](int q, uint64_t off, uint64_t plen, uint8_t* d) -> bool {
+        LargeSource& src = *jobs[q].src;
+        State& S = st[q];
+        if (!jobs[q].sink && src.direct(c, off, plen, d)) return true;  // a sink must see the bytes on the host
+        for (uint64_t o = 0, part = 0; o < plen; o += kBounce, ++part) {  // bounce-buffer path
+            const int bb = (int)(part & 1);
             if (c->bounce_used[bb] && hipEventSynchronize(c->ev_bounce[bb]) != hipSuccess) return false;
-            const uint64_t n = std::min(kBounce, plen - o);
-            src.will_need(off + o + n, 2 * kBounce);  // two bounce pieces ahead while the pool reads this one
-            const int parts = (int)((n + kBigRead - 1) / kBigRead);
+            const uint64_t m = std::min(kBounce, plen - o);
+            src.will_need(off + o + m, 2 * kBounce);  // two bounce pieces ahead while the pool reads this one
+            const int parts = (int)((m + kBigRead - 1) / kBigRead);
             std::atomic<bool> bad{false};
             c->pool->parallel_for(parts, [&](int t) {
-                const uint64_t lo = (uint64_t)t * kBigRead, hi = std::min(n, lo + kBigRead);
+                const uint64_t lo = (uint64_t)t * kBigRead, hi = std::min(m, lo + kBigRead);
                 if (!src.read(off + o + lo, hi - lo, c->h_bounce[bb] + lo)) {
                     bad.store(true);
                     return;
                 }
-                if (sfd >= 0 && sink_ok.load(std::memory_order_relaxed))  // the same bytes to the temp blob
+                if (S.sfd >= 0 && S.sink_ok.load(std::memory_order_relaxed))  // the same bytes to the temp blob
                     for (uint64_t put = lo; put < hi;) {
-                        const ssize_t x = pwrite(sfd, c->h_bounce[bb] + put, hi - put, (off_t)(off + o + put));
+                        const ssize_t x = pwrite(S.sfd, c->h_bounce[bb] + put, hi - put, (off_t)(off + o + put));
                         if (x <= 0) {
-                            sink_ok.store(false);
+                            S.sink_ok.store(false);
                             break;
                         }
                         put += (uint64_t)x;
                     }
             });
             if (bad.load()) return false;
-            if (hipMemcpyAsync(d + o, c->h_bounce[bb], n, hipMemcpyHostToDevice, c->copy_stream) != hipSuccess ||
+            if (hipMemcpyAsync(d + o, c->h_bounce[bb], m, hipMemcpyHostToDevice, c->copy_stream) != hipSuccess ||
                 hipEventRecord(c->ev_bounce[bb], c->copy_stream) != hipSuccess)
                 return false;
             c->bounce_used[bb] = true;
         }
         return hipStreamSynchronize(c->copy_stream) == hipSuccess;
     };
-    for (uint64_t j = 0; j <= k && io_ok && rc == OXH_OK; ++j) {
-        const int b = (int)(j & 1);
-        const uint64_t off = j * P, plen = j < k ? P : L - off;
-        // the chain of piece j-2 (which read dbuf[b] and its block sums) is done
-        if (piece_used[b] && hipEventSynchronize(c->ev_piece_free[b]) != hipSuccess) {
+    bool round_used[2] = {false, false};
+    for (uint64_t r = 0; r < rounds && rc == OXH_OK; ++r) {
+        const int b = (int)(r & 1);
+        // the chains of round r-2 (which read buffers b and their block sums) are done
+        if (round_used[b] && hipEventSynchronize(c->ev_piece_free[b]) != hipSuccess) {
             rc = fail(OXH_ERR_HIP, "large-item piece wait");
             break;
         }
-        if (!copy_piece(off, plen, dbuf[b])) {
-            io_ok = false;
-            break;
-        }
-        piece_used[b] = true;
-        uint64_t* s_b = sums + (uint64_t)b * sums_per;
-        const bool last = j == k;
-        const uint64_t nb = last ? (plen - 1) >> 10 : plen >> 10;
-        const uint64_t nwaves = (nb + 3) / 4, blocks = (nwaves + 3) / 4;
-        hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, c->stream, dbuf[b], nb, s_b);
-        if (want_counts)
-            hipLaunchKernelGGL(oxh::text_count_kernel, dim3(2048), dim3(256), 0, c->stream, dbuf[b], plen,
-                               (unsigned long long*)(d_res + 2));
-        if (j == 0 && want_utf8)
-            hipLaunchKernelGGL(oxh::utf8_prefix_kernel, dim3(1), dim3(64), 0, c->stream, dbuf[b], d_res + 4, d_res + 5,
-                               (uint64_t)1, (int32_t*)(d_res + 6));
         oxh::ChainBatch batch;
-        batch.job[0] = {dbuf[b], plen, s_b, d_res, L, d_res + 7, (j > 0 ? oxh::kChainResume : 0u) | (last ? 0u : oxh::kChainPartial)};
-        hipLaunchKernelGGL(oxh::xxh3_chain_kernel, dim3(1), dim3(64), kChainLdsPad, c->stream, batch);
+        int nj = 0;
+        for (int q = 0; q < n; ++q) {
+            State& S = st[q];
+            if (!S.io_ok || r > S.k) continue;
+            const uint64_t off = r * P, plen = r < S.k ? P : jobs[q].L - off;
+            uint8_t* d = dbuf(q, b);
+            if (!copy_piece(q, off, plen, d)) {
+                S.io_ok = false;  // its earlier chains finish harmlessly; the item is reported as unreadable
+                continue;
+            }
+            uint64_t* s_q = sums + ((uint64_t)b * n + q) * sums_per;
+            const bool last = r == S.k;
+            const uint64_t nb = last ? (plen - 1) >> 10 : plen >> 10;
+            const uint64_t nwaves = (nb + 3) / 4, blocks = (nwaves + 3) / 4;
+            hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, c->stream, d, nb, s_q);
+            if (jobs[q].want_counts)
+                hipLaunchKernelGGL(oxh::text_count_kernel, dim3(2048), dim3(256), 0, c->stream, d, plen,
+                                   (unsigned long long*)(d_res(q) + 2));
+            if (r == 0 && jobs[q].want_utf8)
+                hipLaunchKernelGGL(oxh::utf8_prefix_kernel, dim3(1), dim3(64), 0, c->stream, d, d_res(q) + 4, d_res(q) + 5,
+                                   (uint64_t)1, (int32_t*)(d_res(q) + 6));
+            batch.job[nj++] = {d, plen, s_q, d_res(q), jobs[q].L, d_res(q) + 7,
+                               (r > 0 ? oxh::kChainResume : 0u) | (last ? 0u : oxh::kChainPartial)};
+        }
+        if (nj) hipLaunchKernelGGL(oxh::xxh3_chain_kernel, dim3(nj), dim3(64), kChainLdsPad, c->stream, batch);
         if (hipGetLastError() != hipSuccess || hipEventRecord(c->ev_piece_free[b], c->stream) != hipSuccess)
             rc = fail(OXH_ERR_HIP, "large-item piece launch");
+        round_used[b] = true;
     }
-    if (rc == OXH_OK && hipMemcpyAsync(&h, d_res, sizeof h, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+    if (rc == OXH_OK && hipMemcpyAsync(h_res.data(), d_res_all, h_res.size(), hipMemcpyDeviceToHost, c->stream) != hipSuccess)
         rc = fail(OXH_ERR_HIP, "large-item results D2H");
     if (hipStreamSynchronize(c->stream) != hipSuccess && rc == OXH_OK) rc = fail(OXH_ERR_HIP, "large-item sync");
-    if (sink) {  // publish (or drop) the temp blob now that the digest is known
-        sink->close_stream(id, sfd, sink_tmp, rc == OXH_OK && io_ok && sink_ok.load(), h.out[0], h.out[1]);
-        sink->commit();
+    std::vector<ItemSink*> sinks;
+    for (int q = 0; q < n; ++q) {
+        const Res& h = *reinterpret_cast<const Res*>(h_res.data() + (size_t)q * kRes);
+        if (jobs[q].sink) {  // publish (or drop) the temp blob now that the digest is known
+            jobs[q].sink->close_stream(jobs[q].id, st[q].sfd, st[q].sink_tmp,
+                                       rc == OXH_OK && st[q].io_ok && st[q].sink_ok.load(), h.out[0], h.out[1]);
+            if (std::find(sinks.begin(), sinks.end(), jobs[q].sink) == sinks.end()) sinks.push_back(jobs[q].sink);
+        }
+        LargeResult& res = jobs[q].res;
+        if (rc) continue;
+        if (!st[q].io_ok) {
+            res.status = OXH_ERR_IO;
+            continue;
+        }
+        res.out[0] = h.out[0];
+        res.out[1] = h.out[1];
+        res.cnt[0] = 1 + h.cnt[0];
+        res.cnt[1] = jobs[q].L - h.cnt[1];
+        res.utf8 = h.utf8;
     }
-    if (rc) return rc;
-    if (!io_ok) {
-        res.status = OXH_ERR_IO;
-        return OXH_OK;
-    }
-    res.out[0] = h.out[0];
-    res.out[1] = h.out[1];
-    res.cnt[0] = 1 + h.cnt[0];
-    res.cnt[1] = L - h.cnt[1];
-    res.utf8 = h.utf8;
-    return OXH_OK;
+    for (ItemSink* k : sinks) k->commit();
+    return rc;
+}
+
+// One large item (host buffers of oxh_hash_buffers / _streams, and the single-file case).
+int large_item(oxh_ctx* c, uint64_t L, LargeSource& src, bool want_counts, bool want_utf8, ItemSink* sink, uint64_t id,
+               LargeResult& res) {
+    LargeJob j;
+    j.L = L, j.src = &src, j.want_counts = want_counts, j.want_utf8 = want_utf8, j.sink = sink, j.id = id;
+    const int rc = large_items(c, &j, 1);
+    res = j.res;
+    return rc;
 }
 
 }  // namespace
@@ -1566,21 +1630,35 @@ void drain_files(FileStream& fs, int s, const SlotRun& p) {
     }
 }
 
-// A file of the engine larger than a staging slot.
-int big_file(FileStream& fs, FileRequest* r, uint64_t i) {
-    const uint64_t L = r->lens[i];
-    LargeResult res;
-    {
-        FileSource src(r->paths[i], L, r->sink == nullptr);
-        if (src.fd < 0) {
-            res.status = OXH_ERR_IO;
-        } else if (int rc = large_item(fs.c, L, src, r->counts != nullptr, r->utf8 != nullptr, r->sink, i, res)) {
-            return rc;
+// Files of the engine larger than a staging slot, up to big_files_at_once() side by side.
+int big_files(FileStream& fs, const std::vector<std::pair<FileRequest*, uint64_t>>& items) {
+    const int n = (int)items.size();
+    std::vector<std::unique_ptr<FileSource>> srcs(n);
+    std::vector<LargeJob> jobs;
+    std::vector<int> who;  // jobs[k] is items[who[k]]
+    for (int q = 0; q < n; ++q) {
+        FileRequest* r = items[q].first;
+        const uint64_t i = items[q].second;
+        srcs[q].reset(new FileSource(r->paths[i], r->lens[i], r->sink == nullptr));
+        if (srcs[q]->fd < 0) {
+            r->st[i] = OXH_ERR_IO;
+            continue;
         }
+        LargeJob j;
+        j.L = r->lens[i], j.src = srcs[q].get(), j.want_counts = r->counts != nullptr, j.want_utf8 = r->utf8 != nullptr;
+        j.sink = r->sink, j.id = i;
+        jobs.push_back(j);
+        who.push_back(q);
     }
-    if (res.status != OXH_OK) {
-        r->st[i] = res.status;
-    } else {
+    if (int rc = large_items(fs.c, jobs.data(), (int)jobs.size())) return rc;
+    for (size_t k = 0; k < jobs.size(); ++k) {
+        FileRequest* r = items[who[k]].first;
+        const uint64_t i = items[who[k]].second;
+        const LargeResult& res = jobs[k].res;
+        if (res.status != OXH_OK) {
+            r->st[i] = res.status;
+            continue;
+        }
         r->out[2 * i] = res.out[0];
         r->out[2 * i + 1] = res.out[1];
         if (r->counts) {
@@ -1589,12 +1667,12 @@ int big_file(FileStream& fs, FileRequest* r, uint64_t i) {
         }
         if (r->utf8) r->utf8[i] = res.utf8;
     }
-    account(fs, r, 1);
+    for (int q = 0; q < n; ++q) account(fs, items[q].first, 1);
     return OXH_OK;
 }
 
-// A file larger than a staging slot, with or without a sink: streamed in pieces (big_file).
-int oversize_file(FileStream& fs, FileRequest* r, uint64_t i) { return big_file(fs, r, i); }
+// A file larger than a staging slot, with or without a sink: streamed in pieces (big_files).
+int oversize_file(FileStream& fs, FileRequest* r, uint64_t i) { return big_files(fs, {{r, i}}); }
 
 // A file whose size changed between the stat (or the caller's metadata) and the read: stat and read
 // it afresh (the reference reads whatever the file holds, hasher.rs:126-148). It fits a staging
@@ -1692,6 +1770,7 @@ void run_stream(oxh_ctx* c) {
     int s = 0, nbusy = 0;  // s: the slot being filled; the nbusy slots before it are submitted
     static const double wait_limit = getenv("OXH_WAIT_LIMIT_S") ? atof(getenv("OXH_WAIT_LIMIT_S")) : 60.0;
     double last_progress = Trace::now();
+    double big_wait_since = 0;  // when the oldest waiting large file was first seen
     while (rc == OXH_OK) {
         // 1. drain submitted slots whose digests are back, oldest first, and free them
         bool progressed = false;
@@ -1721,16 +1800,26 @@ void run_stream(oxh_ctx* c) {
             rc = refresh_file(fs, it.first, it.second);
             continue;
         }
-        if (fs.n_oversize.load(std::memory_order_acquire)) {
-            std::pair<FileRequest*, uint64_t> it;
-            {
-                std::lock_guard<std::mutex> g(fs.omu);
-                it = fs.oversize.back();
-                fs.oversize.pop_back();
+        if (const uint64_t no = fs.n_oversize.load(std::memory_order_acquire)) {
+            // several large files share one piece pipeline (their chains overlap the next pieces'
+            // copies): while readers are still claiming files, give more of them a moment to arrive
+            const double now = Trace::now();
+            if (big_wait_since == 0) big_wait_since = now;
+            const bool readers_done = fs.idle.load(std::memory_order_acquire) == fs.nreaders;
+            if ((int)no >= big_files_at_once() || readers_done || now - big_wait_since > 0.002) {
+                std::vector<std::pair<FileRequest*, uint64_t>> items;
+                {
+                    std::lock_guard<std::mutex> g(fs.omu);
+                    while (!fs.oversize.empty() && (int)items.size() < big_files_at_once()) {
+                        items.push_back(fs.oversize.back());
+                        fs.oversize.pop_back();
+                    }
+                }
+                fs.n_oversize.fetch_sub(items.size());
+                big_wait_since = 0;
+                rc = big_files(fs, items);
+                continue;
             }
-            fs.n_oversize.fetch_sub(1);
-            rc = oversize_file(fs, it.first, it.second);
-            continue;
         }
         // 3. the slot being filled: seal it early (flush) when it holds enough bytes or every reader
         //    is idle and the next slot is free; submit it once sealed and its writers are done

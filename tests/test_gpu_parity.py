@@ -724,6 +724,47 @@ def test_big_file_streamed_pieces(oracle_lib, tmp_path, cuda, monkeypatch, piece
         assert d == want and all(s == 0 for s in st) and all(stored)
 
 
+@pytest.mark.parametrize("at_once", ["1", "3", "32"])
+def test_big_files_side_by_side(oracle_lib, tmp_path, cuda, monkeypatch, at_once):
+    """Several files above a staging slot share one piece pipeline (OXH_BIG_FILES at a time): piece r of
+    every file goes to the device, then one chain launch continues every file's chain. Files of
+    different piece counts (1 .. 5 pieces, last pieces of 1 025 B .. P + 1 024 B), mixed with small
+    files, in one call and through the fused add; digests, text counts and is_utf8 vs the oracle."""
+    from oxen_amd import _capi, hasher
+    from oxen_amd.workloads import splitmix_bytes
+
+    monkeypatch.setenv("OXH_BIG_PIECE_MIB", "8")
+    monkeypatch.setenv("OXH_BIG_FILES", at_once)
+    P = 8 << 20
+    big = [5 << 20, 2 * P + 1025, P + 1024, P + 1025, 4 * P + 12_345, 3 * P, (5 << 20) + 1, 2 * P - 7]
+    rng = np.random.default_rng(int(at_once))
+    sizes = []
+    for b in big:
+        sizes += [int(x) for x in rng.integers(0, 100_000, 7)] + [b]
+    blobs = [splitmix_bytes(700 + k, 0, s).tobytes() for k, s in enumerate(sizes)]
+    blobs[1] = ("héllo\nwörld\n" * 1000).encode()  # a text-ish one
+    paths = []
+    for k, b in enumerate(blobs):
+        p = tmp_path / f"f{k}.bin"
+        p.write_bytes(b)
+        paths.append(str(p))
+    want = [oracle_lib.xxh3_128_int(b) for b in blobs]
+    arrs = [np.frombuffer(b, dtype=np.uint8) for b in blobs]
+    want_counts = [(1 + int(np.count_nonzero(a == 10)), len(a) - int(np.count_nonzero((a & 0xC0) == 0x80))) for a in arrs]
+    want_utf8 = [oracle_lib.is_utf8_prefix(b[:4096]) for b in blobs]
+    with _capi.Context(0, staging_bytes=4 << 20) as c:
+        d, sz, st = hasher.hash_files_128bit(paths, c)
+        assert st == [0] * len(paths) and sz == [len(b) for b in blobs] and d == want
+        d, sz, st, meta, u8 = hasher.hash_files_text_utf8_128bit(paths, c)
+        assert d == want and u8 == want_utf8
+        assert [(m["text"]["num_lines"], m["text"]["num_chars"]) for m in meta] == want_counts
+        root = str(tmp_path / "store")
+        d, sz, st, stored = hasher.add_files(paths, root, c)
+        assert d == want and all(s == 0 for s in st) and all(stored)
+        for k in range(7, len(paths), 8):  # every big blob published with the file's bytes
+            assert open(hasher.version_path(root, want[k]), "rb").read() == blobs[k]
+
+
 def test_hash_files_given_metadata(oracle_lib, tmp_path, cuda):
     """oxh_hash_files_meta (get_hash_given_metadata with the walk's sizes, hasher.rs:56-65): no
     fstat per file; sizes that are stale (file grew, shrank, emptied), a directory, a missing path and
