@@ -546,9 +546,10 @@ constexpr uint64_t kBounce = 64ull << 20, kBigRead = 4ull << 20;
 // Where a large item's bytes come from.
 struct LargeSource {
     virtual ~LargeSource() = default;
-    // Copy [off, off + n) straight to device memory `d` (no bounce buffer) if this source can; true
-    // once the copy has completed.
-    virtual bool direct(oxh_ctx*, uint64_t, uint64_t, uint8_t*) { return false; }
+    // Pin [off, off + n) in place for an asynchronous H2D copy (no bounce buffer) if this source can:
+    // the host pointer to copy from, or nullptr. unpin() once the copy has completed.
+    virtual const uint8_t* pin(uint64_t, uint64_t) { return nullptr; }
+    virtual void unpin(const uint8_t*) {}
     // [off, off + n) will be read soon.
     virtual void will_need(uint64_t, uint64_t) {}
     // Read [off, off + n) into dst; called from several threads for disjoint ranges. false = I/O error.
@@ -585,16 +586,16 @@ struct FileSource final : LargeSource {
         for (unsigned char v : resident) in += v & 1;
         return in * 10 >= npg * 9;
     }
-    bool direct(oxh_ctx* c, uint64_t off, uint64_t n, uint8_t* d) override {
+    const uint8_t* pin(uint64_t off, uint64_t n) override {
         if (!map || !mostly_resident(off, n) || hipHostRegister(map + off, n, hipHostRegisterReadOnly) != hipSuccess) {
             (void)hipGetLastError();
-            return false;
+            return nullptr;
         }
-        const bool ok = hipMemcpyAsync(d, map + off, n, hipMemcpyHostToDevice, c->copy_stream) == hipSuccess &&
-                        hipStreamSynchronize(c->copy_stream) == hipSuccess;
-        (void)hipHostUnregister(map + off);
+        return map + off;
+    }
+    void unpin(const uint8_t* p) override {
+        (void)hipHostUnregister((void*)p);
         (void)hipGetLastError();
-        return ok;
     }
     void will_need(uint64_t off, uint64_t n) override { (void)posix_fadvise(fd, (off_t)off, (off_t)n, POSIX_FADV_WILLNEED); }
     bool read(uint64_t off, uint64_t n, uint8_t* dst) override {
@@ -724,7 +725,6 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
     auto copy_piece = [&](int q, uint64_t off, uint64_t plen, uint8_t* d) -> bool {
         LargeSource& src = *jobs[q].src;
         State& S = st[q];
-        if (!jobs[q].sink && src.direct(c, off, plen, d)) return true;  // a sink must see the bytes on the host
         for (uint64_t o = 0, part = 0; o < plen; o += kBounce, ++part) {  // bounce-buffer path
             const int bb = (int)(part & 1);
             if (c->bounce_used[bb] && hipEventSynchronize(c->ev_bounce[bb]) != hipSuccess) return false;
@@ -756,9 +756,43 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
         }
         return hipStreamSynchronize(c->copy_stream) == hipSuccess;
     };
+    // With OXH_BIG_DIRECT=1, pieces whose pages are in the page cache are pinned in place and copied
+    // asynchronously; the next round's pieces are pinned while this round's copies run, and a round's
+    // pins are released once its copies are done.
+    std::vector<hipEvent_t> ev_copy(n, nullptr);
+    for (int q = 0; q < n; ++q)
+        if (hipEventCreateWithFlags(&ev_copy[q], hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            for (hipEvent_t e : ev_copy)
+                if (e) (void)hipEventDestroy(e);
+            return fail(OXH_ERR_HIP, "large-item events");
+        }
+    std::vector<const uint8_t*> pinned(n, nullptr), next_pin(n, nullptr);
+    std::vector<std::pair<int, const uint8_t*>> to_unpin;  // (item, pinned range) of copies in flight
+    auto piece_len = [&](int q, uint64_t r) { return r < st[q].k ? P : jobs[q].L - r * P; };
+    // Pinning page-cache pages in place (OXH_BIG_DIRECT=1) measured 10-27 ms per GiB to register and
+    // ~10 ms per GiB to release on the MI355X boxes (r03, OXH_TRACE), more than the 16 pool threads take
+    // to copy the same bytes into the pinned bounce buffers; the bounce path is the default.
+    const bool may_pin = getenv("OXH_BIG_DIRECT") && atoi(getenv("OXH_BIG_DIRECT")) != 0;
+    auto pin_round = [&](uint64_t r, std::vector<const uint8_t*>& into) {
+        if (!may_pin) return;
+        for (int q = 0; q < n; ++q) {
+            if (into[q]) jobs[q].src->unpin(into[q]);
+            into[q] = (!jobs[q].sink && st[q].io_ok && r <= st[q].k) ? jobs[q].src->pin(r * P, piece_len(q, r)) : nullptr;
+        }
+    };
+    Trace tr;  // OXH_TRACE=1: where a batch's host time goes
+    double t_pin = 0, t_wait = 0, t_unpin = 0, t_bounce = 0;
+    const double t_start = Trace::now();
+    {
+        const double t0 = Trace::now();
+        pin_round(0, next_pin);
+        t_pin += Trace::now() - t0;
+    }
     bool round_used[2] = {false, false};
     for (uint64_t r = 0; r < rounds && rc == OXH_OK; ++r) {
         const int b = (int)(r & 1);
+        pinned.swap(next_pin);
         // the chains of round r-2 (which read buffers b and their block sums) are done
         if (round_used[b] && hipEventSynchronize(c->ev_piece_free[b]) != hipSuccess) {
             rc = fail(OXH_ERR_HIP, "large-item piece wait");
@@ -768,12 +802,37 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
         int nj = 0;
         for (int q = 0; q < n; ++q) {
             State& S = st[q];
-            if (!S.io_ok || r > S.k) continue;
-            const uint64_t off = r * P, plen = r < S.k ? P : jobs[q].L - off;
-            uint8_t* d = dbuf(q, b);
-            if (!copy_piece(q, off, plen, d)) {
-                S.io_ok = false;  // its earlier chains finish harmlessly; the item is reported as unreadable
+            if (!S.io_ok || r > S.k) {
+                if (pinned[q]) jobs[q].src->unpin(pinned[q]);  // pinned ahead, before the item failed
+                pinned[q] = nullptr;
                 continue;
+            }
+            const uint64_t off = r * P, plen = piece_len(q, r);
+            uint8_t* d = dbuf(q, b);
+            if (pinned[q]) {  // copy-free: the DMA engine reads the page cache (a sink must see host bytes)
+                if (hipMemcpyAsync(d, pinned[q], plen, hipMemcpyHostToDevice, c->copy_stream) != hipSuccess ||
+                    hipEventRecord(ev_copy[q], c->copy_stream) != hipSuccess) {
+                    rc = fail(OXH_ERR_HIP, "large-item piece copy");
+                    break;
+                }
+                to_unpin.push_back({q, pinned[q]});
+                pinned[q] = nullptr;
+            } else {
+                const double t0 = Trace::now();
+                const bool copied = copy_piece(q, off, plen, d);
+                t_bounce += Trace::now() - t0;
+                if (!copied) {
+                    S.io_ok = false;  // its earlier chains finish harmlessly; the item is reported as unreadable
+                    continue;
+                }
+                if (hipEventRecord(ev_copy[q], c->copy_stream) != hipSuccess) {
+                    rc = fail(OXH_ERR_HIP, "large-item piece event");
+                    break;
+                }
+            }
+            if (hipStreamWaitEvent(c->stream, ev_copy[q], 0) != hipSuccess) {
+                rc = fail(OXH_ERR_HIP, "large-item piece wait");
+                break;
             }
             uint64_t* s_q = sums + ((uint64_t)b * n + q) * sums_per;
             const bool last = r == S.k;
@@ -789,14 +848,40 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
             batch.job[nj++] = {d, plen, s_q, d_res(q), jobs[q].L, d_res(q) + 7,
                                (r > 0 ? oxh::kChainResume : 0u) | (last ? 0u : oxh::kChainPartial)};
         }
+        if (rc) break;
         if (nj) hipLaunchKernelGGL(oxh::xxh3_chain_kernel, dim3(nj), dim3(64), kChainLdsPad, c->stream, batch);
         if (hipGetLastError() != hipSuccess || hipEventRecord(c->ev_piece_free[b], c->stream) != hipSuccess)
             rc = fail(OXH_ERR_HIP, "large-item piece launch");
         round_used[b] = true;
+        double t0 = Trace::now();
+        if (r + 1 < rounds) pin_round(r + 1, next_pin);  // while this round's copies run
+        t_pin += Trace::now() - t0;
+        if (!to_unpin.empty()) {
+            t0 = Trace::now();
+            if (hipStreamSynchronize(c->copy_stream) != hipSuccess && rc == OXH_OK) rc = fail(OXH_ERR_HIP, "large-item copy");
+            t_wait += Trace::now() - t0;
+            t0 = Trace::now();
+            for (const auto& u : to_unpin) jobs[u.first].src->unpin(u.second);
+            t_unpin += Trace::now() - t0;
+            to_unpin.clear();
+        }
     }
+    // a failure mid-way: release what is still pinned
+    if (hipStreamSynchronize(c->copy_stream) != hipSuccess && rc == OXH_OK) rc = fail(OXH_ERR_HIP, "large-item copy");
+    for (int q = 0; q < n; ++q) {
+        if (pinned[q]) jobs[q].src->unpin(pinned[q]);
+        if (next_pin[q]) jobs[q].src->unpin(next_pin[q]);
+    }
+    for (const auto& u : to_unpin) jobs[u.first].src->unpin(u.second);
     if (rc == OXH_OK && hipMemcpyAsync(h_res.data(), d_res_all, h_res.size(), hipMemcpyDeviceToHost, c->stream) != hipSuccess)
         rc = fail(OXH_ERR_HIP, "large-item results D2H");
+    const double t_tail0 = Trace::now();
     if (hipStreamSynchronize(c->stream) != hipSuccess && rc == OXH_OK) rc = fail(OXH_ERR_HIP, "large-item sync");
+    if (tr.on)
+        fprintf(stderr, "[oxh] large_items n=%d rounds=%llu piece=%llu MiB: total %.1f ms, pin %.1f, copy wait %.1f, unpin %.1f, "
+                "bounce %.1f, chain tail %.1f\n", n, (unsigned long long)rounds, (unsigned long long)(P >> 20),
+                1e3 * (Trace::now() - t_start), 1e3 * t_pin, 1e3 * t_wait, 1e3 * t_unpin, 1e3 * t_bounce,
+                1e3 * (Trace::now() - t_tail0));
     std::vector<ItemSink*> sinks;
     for (int q = 0; q < n; ++q) {
         const Res& h = *reinterpret_cast<const Res*>(h_res.data() + (size_t)q * kRes);
@@ -818,6 +903,7 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
         res.utf8 = h.utf8;
     }
     for (ItemSink* k : sinks) k->commit();
+    for (hipEvent_t e : ev_copy) (void)hipEventDestroy(e);
     return rc;
 }
 

@@ -1,6 +1,13 @@
 """Block-level dedup chunkers on the GPU.
 
-Mirrors experiments/block-level-dedup/src/chunker/fastcdchunker.rs (`FastCDChunker`): the file is
+Fixed-size chunkers (experiments/block-level-dedup/src/chunker/fixedsize.rs, `FixedSizeChunker`, and
+fixedsize_multithreaded.rs, `FixedSizeMultiChunker`): a file is cut into chunk_size pieces (the last
+one shorter), each piece is named by the decimal xxh3_128 of its bytes and written to output_dir
+unless a chunk of that name exists; metadata.bin lists the names (bincode). Here the file is read in
+segments of whole chunks, each segment goes to the device once and `oxh_chunk_digests_device` hashes
+all its chunks in one launch; the chunk files are written by `concurrency` host threads.
+
+FastCDC (fastcdchunker.rs, `FastCDChunker`): the file is
 chunked with FastCDC v2020 (min 4096, avg = chunk_size, max = 2 * chunk_size, :55-57, :83-88) and
 every chunk is written to `output_dir/<decimal xxh3_128 of the chunk>` (:96-107); the chunk names go
 to `metadata.bin` as bincode 1.x of `ChunkMetadata {original_file_name: String, original_file_size:
@@ -40,25 +47,79 @@ def encode_metadata(original_file_name: str, original_file_size: int, chunks: li
     return b"".join(out)
 
 
-def decode_metadata(buf: bytes) -> tuple[str, int, list[str]]:
-    pos = 0
+class _Bincode:
+    """A reader over bincode 1.x default encoding (fixint, little-endian, u64 lengths)."""
 
-    def take(n):
-        nonlocal pos
-        if pos + n > len(buf):
+    def __init__(self, buf: bytes):
+        self.buf, self.pos = buf, 0
+
+    def take(self, n: int) -> bytes:
+        if self.pos + n > len(self.buf):
             raise _capi.OxenError("Bincode error: unexpected end of metadata", _capi.OXH_ERR_IO)
-        v = buf[pos:pos + n]
-        pos += n
+        v = self.buf[self.pos:self.pos + n]
+        self.pos += n
         return v
 
-    def string():
-        (n,) = struct.unpack("<Q", take(8))
-        return take(n).decode("utf-8")
+    def u64(self) -> int:
+        return struct.unpack("<Q", self.take(8))[0]
 
-    name = string()
-    (size,) = struct.unpack("<Q", take(8))
-    (count,) = struct.unpack("<Q", take(8))
-    return name, size, [string() for _ in range(count)]
+    def u8(self) -> int:
+        return self.take(1)[0]
+
+    def string(self) -> str:
+        return self.take(self.u64()).decode("utf-8")
+
+    def strings(self) -> list[str]:
+        return [self.string() for _ in range(self.u64())]
+
+
+def decode_metadata(buf: bytes) -> tuple[str, int, list[str]]:
+    r = _Bincode(buf)
+    name = r.string()
+    size = r.u64()
+    return name, size, r.strings()
+
+
+def _strings(items: list[str]) -> bytes:
+    return struct.pack("<Q", len(items)) + b"".join(_bincode_string(c) for c in items)
+
+
+def encode_fixed_metadata(original_file_name: str, original_file_size: int, chunk_size: int, chunks: list[str]) -> bytes:
+    """fixedsize_multithreaded.rs:14-20 ChunkMetadata {original_file_name, original_file_size: u64,
+    chunk_size: usize, chunks: Vec<String>} in bincode 1.x."""
+    return (_bincode_string(original_file_name) + struct.pack("<QQ", original_file_size, chunk_size) + _strings(chunks))
+
+
+def decode_fixed_metadata(buf: bytes) -> tuple[str, int, int, list[str]]:
+    r = _Bincode(buf)
+    name = r.string()
+    size, chunk = r.u64(), r.u64()
+    return name, size, chunk, r.strings()
+
+
+def encode_archive_metadata(chunk_size: int, entries: list[dict]) -> bytes:
+    """fixedsize.rs:22-35 ArchiveMetadata {chunk_size: usize, entries: Vec<ArchiveEntry {path: PathBuf,
+    is_dir: bool, chunks: Option<Vec<String>>, size: Option<u64>}>} in bincode 1.x (Option = u8 tag)."""
+    out = [struct.pack("<QQ", chunk_size, len(entries))]
+    for e in entries:
+        out.append(_bincode_string(e["path"]))
+        out.append(b"\x01" if e["is_dir"] else b"\x00")
+        out.append(b"\x00" if e["chunks"] is None else b"\x01" + _strings(e["chunks"]))
+        out.append(b"\x00" if e["size"] is None else b"\x01" + struct.pack("<Q", e["size"]))
+    return b"".join(out)
+
+
+def decode_archive_metadata(buf: bytes) -> tuple[int, list[dict]]:
+    r = _Bincode(buf)
+    chunk = r.u64()
+    entries = []
+    for _ in range(r.u64()):
+        path = r.string()
+        is_dir = r.u8() != 0
+        chunks = r.strings() if r.u8() else None
+        size = r.u64() if r.u8() else None
+        entries.append({"path": path, "is_dir": is_dir, "chunks": chunks, "size": size})
+    return chunk, entries
 
 
 class FastCDChunker:
@@ -114,6 +175,165 @@ class FastCDChunker:
 
     def get_chunk_hashes(self, input_dir: str) -> list[str]:
         return decode_metadata(open(os.path.join(input_dir, METADATA_FILE_NAME), "rb").read())[2]
+
+
+SEGMENT_BYTES = 1 << 30  # bytes of a file on the device at a time (whole chunks)
+
+
+class _FixedSizeBase:
+    """Shared by both fixed-size chunkers: a file -> its chunk names, chunks written as they are named."""
+
+    def __init__(self, chunk_size: int, concurrency: int = 1, device: Optional[str] = None):
+        if chunk_size == 0:
+            raise ValueError("Chunk size cannot be zero")
+        if concurrency == 0:
+            raise ValueError("Concurrency must be greater than zero")
+        self.chunk_size = int(chunk_size)
+        self.concurrency = int(concurrency)
+        self.device = device or "cuda"
+
+    def chunk_file(self, path: str, output_dir: str) -> list[str]:
+        """Decimal xxh3_128 names of the file's chunks; a chunk file is written unless one of that
+        name exists (fixedsize.rs:78-89, fixedsize_multithreaded.rs:95-105)."""
+        from concurrent.futures import ThreadPoolExecutor
+
+        from .device import chunk_digests_device
+
+        size = os.stat(path).st_size
+        seg = max(self.chunk_size, SEGMENT_BYTES // self.chunk_size * self.chunk_size)
+        names: list[str] = []
+        host = torch.empty(min(seg, max(size, 1)), dtype=torch.uint8).pin_memory()
+        dev = torch.empty(host.numel(), dtype=torch.uint8, device=self.device)
+        hv = host.numpy()
+        with open(path, "rb", buffering=0) as fh, ThreadPoolExecutor(self.concurrency) as ex:
+            off = 0
+            while off < size:
+                n = min(seg, size - off)
+                got = fh.readinto(memoryview(hv)[:n])
+                if got != n:
+                    raise _capi.OxenError(f"short read of {path!r}", _capi.OXH_ERR_IO)
+                dev[:n].copy_(host[:n], non_blocking=True)
+                dig = to_numpy_u64(chunk_digests_device(dev, self.chunk_size, n)).reshape(-1, 2)
+                seg_names = [chunk_name(lo, hi) for lo, hi in dig.tolist()]
+
+                def write(k, seg_names=seg_names, n=n):
+                    p = os.path.join(output_dir, seg_names[k])
+                    if not os.path.exists(p):
+                        lo = k * self.chunk_size
+                        with open(p, "wb") as out:
+                            out.write(hv[lo:min(n, lo + self.chunk_size)].tobytes())
+
+                list(ex.map(write, range(len(seg_names))))
+                names += seg_names
+                off += n
+        return names
+
+
+class FixedSizeChunker(_FixedSizeBase):
+    """fixedsize.rs:37-296 + the Chunker trait: packs a file or a whole directory tree (entries in
+    read_dir order, a directory's entry before its contents) into chunk files + ArchiveMetadata."""
+
+    def __init__(self, chunk_size: int, device: Optional[str] = None):
+        super().__init__(chunk_size, 1, device)
+
+    def name(self) -> str:
+        return "fixed-size-chunker"
+
+    def _file_entry(self, path: str, base: str, output_dir: str) -> dict:
+        chunks = self.chunk_file(path, output_dir)
+        return {"path": os.path.relpath(path, base), "is_dir": False, "chunks": chunks, "size": os.stat(path).st_size}
+
+    def _walk(self, cur: str, base: str, output_dir: str, entries: list) -> None:
+        with os.scandir(cur) as it:  # read_dir order (fixedsize.rs:116)
+            for e in it:
+                if e.is_dir():  # metadata() follows symlinks, as here
+                    entries.append({"path": os.path.relpath(e.path, base), "is_dir": True, "chunks": None, "size": None})
+                    self._walk(e.path, base, output_dir, entries)
+                elif e.is_file():
+                    entries.append(self._file_entry(e.path, base, output_dir))
+
+    def pack(self, input_path: str, output_dir: str) -> str:
+        os.makedirs(output_dir, exist_ok=True)
+        entries: list = []
+        if os.path.isfile(input_path):
+            base = os.path.dirname(os.path.abspath(input_path))
+            entries.append(self._file_entry(os.path.abspath(input_path), base, output_dir))
+        elif os.path.isdir(input_path):
+            entries.append({"path": ".", "is_dir": True, "chunks": None, "size": None})
+            self._walk(input_path, input_path, output_dir, entries)
+        else:
+            raise _capi.OxenError("Input path must be a file or a directory", _capi.OXH_ERR_INVALID)
+        with open(os.path.join(output_dir, METADATA_FILE_NAME), "wb") as f:
+            f.write(encode_archive_metadata(self.chunk_size, entries))
+        return output_dir
+
+    def unpack(self, chunk_dir: str, output_dir: str) -> str:
+        _, entries = decode_archive_metadata(open(os.path.join(chunk_dir, METADATA_FILE_NAME), "rb").read())
+        os.makedirs(output_dir, exist_ok=True)
+        for e in entries:
+            out = os.path.join(output_dir, e["path"])
+            if e["is_dir"]:
+                os.makedirs(out, exist_ok=True)
+                continue
+            os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
+            with open(out, "wb") as fh:
+                for c in e["chunks"] or []:
+                    p = os.path.join(chunk_dir, c)
+                    if not os.path.exists(p):
+                        raise FileNotFoundError(f"Chunk file not found during unpack: {p}")
+                    with open(p, "rb") as ch:
+                        fh.write(ch.read())
+        return output_dir
+
+    def get_chunk_hashes(self, input_dir: str) -> list[str]:
+        _, entries = decode_archive_metadata(open(os.path.join(input_dir, METADATA_FILE_NAME), "rb").read())
+        return [c for e in entries if not e["is_dir"] for c in (e["chunks"] or [])]
+
+
+class FixedSizeMultiChunker(_FixedSizeBase):
+    """fixedsize_multithreaded.rs:24-245 (the reference's rayon pool of `concurrency`): one file ->
+    chunk files + ChunkMetadata {original_file_name, original_file_size, chunk_size, chunks}."""
+
+    def name(self) -> str:
+        return "fixed-size-64k-multithreaded"
+
+    def pack(self, input_file: str, output_dir: str) -> str:
+        os.makedirs(output_dir, exist_ok=True)
+        try:
+            size = os.stat(input_file).st_size
+        except OSError as e:
+            raise FileNotFoundError(f"Failed to read input file metadata '{input_file}': {e}") from e
+        names = self.chunk_file(input_file, output_dir) if size else []
+        base = os.path.basename(os.path.normpath(input_file)) or "unknown_file"
+        with open(os.path.join(output_dir, METADATA_FILE_NAME), "wb") as f:
+            f.write(encode_fixed_metadata(base, size, self.chunk_size, names))
+        return output_dir
+
+    def unpack(self, chunk_dir: str, output_path: str) -> str:
+        _, _, _, chunks = decode_fixed_metadata(open(os.path.join(chunk_dir, METADATA_FILE_NAME), "rb").read())
+        with open(output_path, "wb") as out:
+            for c in chunks:
+                p = os.path.join(chunk_dir, c)
+                if not os.path.exists(p):
+                    raise FileNotFoundError(f"Chunk file not found during unpack: {p}")
+                with open(p, "rb") as fh:
+                    out.write(fh.read())
+        return output_path
+
+    def get_chunk_hashes(self, input_dir: str) -> list[str]:
+        return decode_fixed_metadata(open(os.path.join(input_dir, METADATA_FILE_NAME), "rb").read())[3]
+
+
+def get_chunker(algorithm: str, chunk_size: int):
+    """chunker.rs:60-124 get_chunker: "fixed-size", "fixed-size-multithreaded" (16 threads) and
+    "fastcdc" (the "copier" baseline copies files and hashes nothing: not on this path)."""
+    if algorithm == "fixed-size":
+        return FixedSizeChunker(chunk_size)
+    if algorithm == "fixed-size-multithreaded":
+        return FixedSizeMultiChunker(chunk_size, 16)
+    if algorithm == "fastcdc":
+        return FastCDChunker(chunk_size, 16)
+    raise _capi.OxenError(f"Chunker '{algorithm}' not found", _capi.OXH_ERR_INVALID)
 
 
 def fastcdc_gear() -> list[int]:
