@@ -35,6 +35,29 @@ def default_context() -> _capi.Context:
         return _ctx
 
 
+class _PathTable:
+    """A `const char* const*` table over NUL-terminated paths packed in one buffer (the pointer table
+    built with numpy: ~20x cheaper than a ctypes array of 200 000 c_char_p objects)."""
+
+    def __init__(self, paths: Sequence):
+        if all(isinstance(p, str) for p in paths):  # one encode of the joined list, NULs found by numpy
+            joined = os.fsencode("\0".join(paths) + "\0")
+        else:
+            joined = b"\0".join(p if isinstance(p, bytes) else os.fsencode(str(p)) for p in paths) + b"\0"
+        self.blob = np.frombuffer(joined, dtype=np.uint8)
+        ends = np.flatnonzero(self.blob == 0).astype(np.uint64) if len(paths) else np.zeros(0, dtype=np.uint64)
+        if len(ends) != len(paths):
+            raise OxenError("a path contains a NUL byte", _capi.OXH_ERR_INVALID)
+        offs = np.zeros(len(paths), dtype=np.uint64)
+        if len(paths) > 1:
+            offs[1:] = ends[:-1] + np.uint64(1)
+        self.ptrs = offs + np.uint64(self.blob.ctypes.data)
+
+    @property
+    def arg(self):
+        return self.ptrs.ctypes.data_as(ctypes.POINTER(ctypes.c_char_p))
+
+
 def _to_u128(lo: int, hi: int) -> int:
     return (int(hi) << 64) | int(lo)
 
@@ -98,7 +121,8 @@ def hash_files_128bit(paths: Sequence[str], ctx: Optional[_capi.Context] = None)
     n = len(paths)
     if n == 0:
         return [], [], []
-    arr = (ctypes.c_char_p * n)(*[os.fsencode(str(p)) for p in paths])
+    table = _PathTable(paths)
+    arr = table.arg
     out = np.zeros((n, 2), dtype=np.uint64)
     sizes = np.zeros(n, dtype=np.uint64)
     status = np.zeros(n, dtype=np.int32)
@@ -106,7 +130,7 @@ def hash_files_128bit(paths: Sequence[str], ctx: Optional[_capi.Context] = None)
                                            sizes.ctypes.data_as(_capi._u64p),
                                            status.ctypes.data_as(_capi._i32p)), "oxh_hash_files")
     digests = _u128_list(out, status)
-    return digests, [int(s) for s in sizes], [int(s) for s in status]
+    return digests, sizes.tolist(), status.tolist()
 
 
 
@@ -121,7 +145,8 @@ def hash_files_given_metadata_128bit(paths: Sequence[str], meta_sizes: Sequence[
         return [], [], []
     if len(meta_sizes) != n:
         raise _capi.OxenError("paths and meta_sizes differ in length", _capi.OXH_ERR_INVALID)
-    arr = (ctypes.c_char_p * n)(*[os.fsencode(str(p)) for p in paths])
+    table = _PathTable(paths)
+    arr = table.arg
     meta = np.ascontiguousarray(meta_sizes, dtype=np.uint64)
     out = np.zeros((n, 2), dtype=np.uint64)
     sizes = np.zeros(n, dtype=np.uint64)
@@ -129,7 +154,7 @@ def hash_files_given_metadata_128bit(paths: Sequence[str], meta_sizes: Sequence[
     _capi.check(_capi.lib().oxh_hash_files_meta(ctx.handle, arr, meta.ctypes.data_as(_capi._u64p), n,
                                                 out.ctypes.data_as(_capi._u64p), sizes.ctypes.data_as(_capi._u64p),
                                                 status.ctypes.data_as(_capi._i32p)), "oxh_hash_files_meta")
-    return _u128_list(out, status), [int(s) for s in sizes], [int(s) for s in status]
+    return _u128_list(out, status), sizes.tolist(), status.tolist()
 
 
 def _split_u128(values) -> np.ndarray:
@@ -165,7 +190,8 @@ def files_modified(paths: Sequence[str], sizes: Sequence[int], node_bytes: Seque
         raise _capi.OxenError("files_modified: argument lengths differ", _capi.OXH_ERR_INVALID)
     if n == 0:
         return [], [], 0
-    arr = (ctypes.c_char_p * n)(*[os.fsencode(str(p)) for p in paths])
+    table = _PathTable(paths)
+    arr = table.arg
     sz = np.ascontiguousarray(sizes, dtype=np.uint64)
     nb = np.ascontiguousarray(node_bytes, dtype=np.uint64)
     mm = np.ascontiguousarray([1 if m else 0 for m in mtime_matched], dtype=np.uint8)
@@ -228,7 +254,8 @@ def add_files(paths: Sequence[str], versions_root: str, ctx: Optional[_capi.Cont
     n = len(paths)
     if n == 0:
         return [], [], [], []
-    arr = (ctypes.c_char_p * n)(*[os.fsencode(str(p)) for p in paths])
+    table = _PathTable(paths)
+    arr = table.arg
     out = np.zeros((n, 2), dtype=np.uint64)
     sizes = np.zeros(n, dtype=np.uint64)
     status = np.zeros(n, dtype=np.int32)
@@ -238,7 +265,7 @@ def add_files(paths: Sequence[str], versions_root: str, ctx: Optional[_capi.Cont
                                           status.ctypes.data_as(_capi._i32p), stored.ctypes.data_as(_capi._i32p)),
                 "oxh_add_files")
     digests = _u128_list(out, status)
-    return digests, [int(s) for s in sizes], [int(s) for s in status], [bool(s) for s in stored]
+    return digests, sizes.tolist(), status.tolist(), [bool(s) for s in stored]
 
 
 def clean_corrupted_versions(versions_root: str, dry_run: bool = False, ctx: Optional[_capi.Context] = None) -> dict:
@@ -270,7 +297,8 @@ def hash_files_text_128bit(paths: Sequence[str], ctx: Optional[_capi.Context] = 
     n = len(paths)
     if n == 0:
         return [], [], [], []
-    arr = (ctypes.c_char_p * n)(*[os.fsencode(str(p)) for p in paths])
+    table = _PathTable(paths)
+    arr = table.arg
     out = np.zeros((n, 2), dtype=np.uint64)
     sizes = np.zeros(n, dtype=np.uint64)
     status = np.zeros(n, dtype=np.int32)
@@ -292,7 +320,8 @@ def hash_files_text_utf8_128bit(paths: Sequence[str], ctx: Optional[_capi.Contex
     n = len(paths)
     if n == 0:
         return [], [], [], [], []
-    arr = (ctypes.c_char_p * n)(*[os.fsencode(str(p)) for p in paths])
+    table = _PathTable(paths)
+    arr = table.arg
     out = np.zeros((n, 2), dtype=np.uint64)
     sizes = np.zeros(n, dtype=np.uint64)
     status = np.zeros(n, dtype=np.int32)
