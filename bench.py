@@ -387,7 +387,7 @@ def main() -> None:
                                    "source": prof["source"],
                                    "frac": round(bytes_per_rank / (prof["avg_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
         cpu = None
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU baseline is a rank-0, N = 1 figure
             cpu = cpu_baseline(da, digests, seed, args.cpu_budget)
         result = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,

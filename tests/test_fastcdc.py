@@ -249,3 +249,37 @@ def test_fastcdc_unit_list_overflow(cuda, oracle_lib, monkeypatch, cap):
     _check(cuda, oracle_lib, files, 64, 256, 1024)
     monkeypatch.setenv("OXH_CDC_SECTION_BYTES", "16384")
     _check(cuda, oracle_lib, files, 4096, 8192, 16384)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("avg", [8192, 65536])
+def test_fastcdc_gib_files_fully_checked(cuda, oracle_lib, avg):
+    """C5's shape scaled to 4 files of 1 GiB + ragged tails (device-generated splitmix data, files at
+    4 KiB-aligned starts as bench_fastcdc lays them out): every chunk boundary of every file and every
+    chunk digest against the C oracle -- the whole file, not a prefix."""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oxen_amd.device import fastcdc_device, fill_splitmix, to_numpy_u64
+
+    sizes = [(1 << 30) + 13, 1 << 30, (1 << 30) - 4097, (1 << 30) + 65_537]
+    pitch = ((max(sizes) + 4095) // 4096) * 4096
+    arena = torch.empty(pitch * len(sizes), dtype=torch.uint8, device=cuda)
+    fill_splitmix(arena, 4242)
+    offs = np.arange(len(sizes), dtype=np.uint64) * np.uint64(pitch)
+    lens = np.array(sizes, dtype=np.uint64)
+    c_off, c_len, dig, first = fastcdc_device(arena, offs, lens, 4096, avg, 2 * avg)
+    got_off, got_len = to_numpy_u64(c_off), to_numpy_u64(c_len)
+    got_dig = to_numpy_u64(dig).reshape(-1, 2)
+
+    def one(i):
+        host = arena[int(offs[i]):int(offs[i]) + sizes[i]].cpu().numpy()
+        want = F.chunks(host, 4096, avg, 2 * avg)
+        a, b = int(first[i]), int(first[i + 1])
+        ok = b - a == len(want) and np.array_equal(got_off[a:b] - offs[i], want[:, 0]) and np.array_equal(got_len[a:b], want[:, 1])
+        return bool(ok and np.array_equal(oracle_lib.batch(host, want[:, 0], want[:, 1], threads=4), got_dig[a:b]))
+
+    with ThreadPoolExecutor(4) as ex:
+        assert all(ex.map(one, range(len(sizes))))
+    del arena
+    torch.cuda.empty_cache()

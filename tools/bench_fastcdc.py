@@ -21,6 +21,38 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def check_all(arena, offs, size, c_off, c_len, dig, first, mn, av, mx, workers: int = 4) -> dict:
+    """Every file's chunk table (offsets, lengths) and every chunk digest against the C oracle, files
+    copied back one at a time per worker (host memory: workers x file size)."""
+    import time as _t
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import fastcdc as F
+    from oracle import oracle
+    from oxen_amd.device import to_numpy_u64
+
+    t0 = _t.perf_counter()
+    got_off = to_numpy_u64(c_off)
+    got_len = to_numpy_u64(c_len)
+    got_dig = to_numpy_u64(dig).reshape(-1, 2)
+
+    def one(i):
+        lo, hi = int(first[i]), int(first[i + 1])
+        o = int(offs[i])
+        host = arena[o:o + size].cpu().numpy()
+        want = F.chunks(host, mn, av, mx)  # the C oracle over the whole file (ctypes releases the GIL)
+        ok = len(want) == hi - lo
+        ok = ok and bool(np.array_equal(got_off[lo:hi] - np.uint64(o), want[:, 0]) and np.array_equal(got_len[lo:hi], want[:, 1]))
+        if ok:
+            ok = bool(np.array_equal(oracle.batch(host, want[:, 0], want[:, 1], threads=4), got_dig[lo:hi]))
+        return ok, hi - lo
+
+    with ThreadPoolExecutor(workers) as ex:
+        rs = list(ex.map(one, range(len(offs))))
+    return {"files_checked": len(rs), "chunks_checked": int(sum(r[1] for r in rs)),
+            "all_files_bit_exact": all(r[0] for r in rs), "check_s": round(_t.perf_counter() - t0, 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--files", type=int, default=16)
@@ -28,6 +60,8 @@ def main():
     ap.add_argument("--chunk", type=int, default=65536)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--check-mib", type=int, default=256)
+    ap.add_argument("--check-all", action="store_true",
+                    help="also check EVERY file's whole chunk table and every chunk digest against the C oracle")
     ap.add_argument("--variant", type=int, default=0, help="force a K1 variant (0 = the library's choice)")
     args = ap.parse_args()
 
@@ -80,6 +114,10 @@ def main():
     exact = bool(np.array_equal(got_off[:k], want[:k, 0]) and np.array_equal(got_len[:k], want[:k, 1]))
     wd = oracle.batch(host, want[:k, 0], want[:k, 1], threads=16)
     exact = exact and bool(np.array_equal(to_numpy_u64(dig[:k]).reshape(-1, 2), wd))
+    full = None
+    if args.check_all:
+        full = check_all(arena, offs, size, c_off, c_len, dig, first, mn, av, mx)
+        exact = exact and full["all_files_bit_exact"]
     res = {"workload": f"{args.files} x {args.gib:g} GiB splitmix blobs, FastCDC v2020 min/avg/max {mn}/{av}/{mx} "
                        f"+ XXH3-128 per chunk, device-resident",
            "bytes": total, "chunks": nchunks, "mean_chunk": total / max(nchunks, 1),
@@ -87,6 +125,8 @@ def main():
            "GiB_s": round(total / t / 2**30, 1), "GB_s": round(total / t / 1e9, 1),
            "prefix_checked_bytes": m, "prefix_chunks_bit_exact": exact, "reps_identical": same,
            "cpu_oracle_1core_GiB_s": round(m / cpu_s / 2**30, 3)}
+    if full:
+        res["check_all"] = full
     print(json.dumps(res), flush=True)
     if not (exact and same):
         sys.exit(1)
