@@ -111,6 +111,12 @@ std::string hash_buffer(const void* data, size_t len) { return format_hex(hash_b
 
 std::string hash_str(std::string_view s) { return hash_buffer(s.data(), s.size()); }
 
+namespace {
+// per-file outcomes of a hash_files-shaped call, with hasher.rs's error texts
+std::vector<FileHash> file_hashes(const std::vector<std::string>& paths, const std::vector<uint64_t>& out,
+                                  const std::vector<uint64_t>& sizes, const std::vector<int32_t>& status);
+}  // namespace
+
 std::vector<FileHash> hash_files(const std::vector<std::string>& paths, oxh_ctx* ctx) {
     ctx = ctx ? ctx : default_context();
     const size_t n = paths.size();
@@ -119,6 +125,35 @@ std::vector<FileHash> hash_files(const std::vector<std::string>& paths, oxh_ctx*
     std::vector<uint64_t> out(2 * n), sizes(n);
     std::vector<int32_t> status(n);
     check(oxh_hash_files(ctx, cp.data(), n, out.data(), sizes.data(), status.data()), "oxh_hash_files");
+    return file_hashes(paths, out, sizes, status);
+}
+
+ReaderPool::ReaderPool(int procs, const std::vector<int>& devices, int threads, uint64_t staging_bytes) {
+    check(oxh_pool_create(devices.data(), (int)devices.size(), procs, threads, staging_bytes, &p_), "oxh_pool_create");
+    procs_ = procs;
+}
+
+ReaderPool::~ReaderPool() {
+    if (p_) oxh_pool_destroy(p_);
+}
+
+std::vector<FileHash> ReaderPool::hash_files(const std::vector<std::string>& paths, const std::vector<uint64_t>& meta_sizes) {
+    const size_t n = paths.size();
+    if (!meta_sizes.empty() && meta_sizes.size() != n) throw OxenError::basic_str("paths and meta_sizes differ in length", OXH_ERR_INVALID);
+    std::vector<const char*> cp(n);
+    for (size_t i = 0; i < n; ++i) cp[i] = paths[i].c_str();
+    std::vector<uint64_t> out(2 * n), sizes(n);
+    std::vector<int32_t> status(n);
+    check(oxh_pool_hash_files(p_, cp.data(), meta_sizes.empty() ? nullptr : meta_sizes.data(), n, out.data(), sizes.data(),
+                              status.data()),
+          "oxh_pool_hash_files");
+    return file_hashes(paths, out, sizes, status);
+}
+
+namespace {
+std::vector<FileHash> file_hashes(const std::vector<std::string>& paths, const std::vector<uint64_t>& out,
+                                  const std::vector<uint64_t>& sizes, const std::vector<int32_t>& status) {
+    const size_t n = paths.size();
     std::vector<FileHash> r(n);
     for (size_t i = 0; i < n; ++i) {
         if (status[i] == OXH_OK) {
@@ -133,6 +168,7 @@ std::vector<FileHash> hash_files(const std::vector<std::string>& paths, oxh_ctx*
     }
     return r;
 }
+}  // namespace
 
 namespace {
 u128 hash_one_file(const std::string& path) {

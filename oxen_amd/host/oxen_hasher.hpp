@@ -91,6 +91,26 @@ struct FileHash {
     std::string error;
 };
 std::vector<FileHash> hash_files(const std::vector<std::string>& paths, oxh_ctx* ctx = nullptr);
+
+// The add loop's hash stage over helper processes (oxh_pool_*): the list split into contiguous
+// shares (by bytes when sizes are given), one helper process per share, helper p on
+// devices[p % devices.size()]. liboxen's fan-out of 64-file batches over tasks of one process
+// (add.rs:422-425) becomes a fan-out over processes and GPUs. Calls serialise; a helper that dies
+// makes this and every later call throw.
+class ReaderPool {
+   public:
+    explicit ReaderPool(int procs = 2, const std::vector<int>& devices = {0}, int threads = 0, uint64_t staging_bytes = 0);
+    ~ReaderPool();
+    ReaderPool(const ReaderPool&) = delete;
+    ReaderPool& operator=(const ReaderPool&) = delete;
+    // get_hash_given_metadata over every path (meta_sizes: the walk's metadata.len(), or empty)
+    std::vector<FileHash> hash_files(const std::vector<std::string>& paths, const std::vector<uint64_t>& meta_sizes = {});
+    int procs() const { return procs_; }
+
+   private:
+    oxh_pool* p_ = nullptr;
+    int procs_ = 0;
+};
 std::vector<u128> hash_buffers_128bit(const std::vector<std::string_view>& buffers, oxh_ctx* ctx = nullptr);
 
 // xxhash-rust Xxh3 (new / update / digest128 / reset) on the GPU (oxh_xxh3_stream_*).

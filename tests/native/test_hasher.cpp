@@ -179,6 +179,40 @@ static void file_errors(const std::string& golden) {
     CHECK(r[2].error == "Could not read file for hashing");
 }
 
+// The reader-process pool (oxh_pool_*) through liboxen::util::hasher::ReaderPool: the same outcomes
+// as one context's hash_files, per file, with and without the walk's sizes, over 2 and 3 helpers.
+static void reader_pool(const std::string& golden) {
+    const std::string missing = golden + "/no-such-file";
+    std::vector<std::string> paths;
+    std::vector<uint64_t> sizes;
+    if (DIR* dp = opendir((golden + "/data_test/text").c_str())) {
+        while (dirent* e = readdir(dp))
+            if (e->d_name[0] != '.') paths.push_back(golden + "/data_test/text/" + e->d_name);
+        closedir(dp);
+    }
+    paths.push_back(missing);
+    paths.push_back(golden);  // a directory: cannot be read
+    for (const std::string& p : paths) {
+        struct stat sb {};
+        sizes.push_back(stat(p.c_str(), &sb) == 0 ? (uint64_t)sb.st_size : 0);
+    }
+    const auto want = hasher::hash_files(paths);
+    for (int procs : {2, 3}) {
+        hasher::ReaderPool pool(procs, {0});
+        CHECK(pool.procs() == procs);
+        for (int with_sizes = 0; with_sizes < 2; ++with_sizes) {
+            const auto got = pool.hash_files(paths, with_sizes ? sizes : std::vector<uint64_t>{});
+            bool same = got.size() == want.size();
+            for (size_t i = 0; same && i < got.size(); ++i)
+                same = got[i].ok == want[i].ok && got[i].hash == want[i].hash && got[i].error == want[i].error &&
+                       (!got[i].ok || got[i].size == want[i].size);
+            CHECK(same);
+        }
+        CHECK(pool.hash_files({}).empty());
+    }
+    CHECK(throws_oxen([&] { hasher::ReaderPool bad(0); }));
+}
+
 static void merkle_hash() {
     const MerkleHash h = MerkleHash::from_str("2da4b9c5a75caad3688558138047f8a");
     CHECK(h.to_string() == "2da4b9c5a75caad3688558138047f8a");
@@ -372,6 +406,7 @@ int main(int argc, char** argv) {
         hashing_writer_tests();
         known_answers(golden);
         file_errors(golden);
+        reader_pool(golden);
         merkle_hash();
         long_stream();
         modified_check(golden);

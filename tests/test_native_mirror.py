@@ -25,6 +25,7 @@ def test_mirror_builds_and_exports_the_hasher_api(native):
                  "liboxen::util::hasher::get_hash_given_metadata", "liboxen::util::hasher::get_combined_hash",
                  "liboxen::util::hasher::get_metadata_hash", "liboxen::util::hasher::Xxh3::digest128",
                  "liboxen::util::hasher::hash_files", "liboxen::MerkleHash::from_str",
+                 "liboxen::util::hasher::ReaderPool::hash_files",
                  "liboxen::util::fs::classify_modified_batch", "liboxen::util::fs::AtomicFile::stream",
                  "liboxen::storage::LocalVersionStore::store_version_from_reader",
                  "liboxen::storage::LocalVersionStore::store_versions"]:
