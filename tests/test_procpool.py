@@ -88,6 +88,26 @@ def test_sharded_gpu_engines_match_oracle(cuda, tmp_path, oracle_lib, procs, dev
 
 
 @pytest.mark.gpu
+def test_pool_concurrent_callers(cuda, tmp_path, oracle_lib):
+    """Several threads share one pool (liboxen's tokio tasks holding one process-wide pool): calls
+    serialise inside the library and each gets its own list's digests."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oxen_amd.procpool import ShardedFileHasher
+
+    paths = _tree(tmp_path, 600)[:-1]
+    want, _, _ = oracle_lib.hash_files(paths, threads=4)
+    lists = [list(range(k, len(paths), 5)) for k in range(5)]
+    with ShardedFileHasher(procs=2, threads=4, staging_bytes=8 << 20) as pool:
+        def call(idx):
+            out, _, st = pool.hash_files([paths[i] for i in idx])
+            return (st == 0).all() and np.array_equal(out, want[idx])
+
+        with ThreadPoolExecutor(5) as ex:
+            assert all(ex.map(call, lists * 3))
+
+
+@pytest.mark.gpu
 def test_pool_helper_death_breaks_the_pool(cuda, tmp_path):
     """A helper that dies fails the call and every later one (no stale replies, no partial outputs)."""
     from oxen_amd import _capi
