@@ -251,9 +251,10 @@ struct oxh_ctx {
     // and two pinned bounce buffers the file is read into in pieces
     uint8_t* d_big = nullptr;
     uint64_t d_big_size = 0;
-    uint8_t* h_bounce[2] = {};
-    hipEvent_t ev_bounce[2] = {};
-    bool bounce_used[2] = {};
+    uint8_t* h_bounce[4] = {};   // kNBounce pinned bounce buffers, used as a ring
+    hipEvent_t ev_bounce[4] = {};
+    bool bounce_used[4] = {};
+    uint64_t bounce_next = 0;    // the ring position (kept across pieces and files)
     hipEvent_t ev_piece_free[2] = {};
     void* live = nullptr;  // the engine's current run (a FileStream, for diagnostics), under qmu
     std::vector<struct FileRequest*> rq[NSLOT];  // per staged item: its request and index in it
@@ -542,6 +543,7 @@ int oversize_item(oxh_ctx* c, const uint8_t* src, uint64_t len, uint64_t* out2, 
 // add) every bounce part is also written to the sink's temp as it is read, and the temp is published
 // once the digest is known: the item never has to fit in host memory.
 constexpr uint64_t kBounce = 64ull << 20, kBigRead = 4ull << 20;
+constexpr int kNBounce = 4;  // bounce buffers in the ring: reads of the next parts run while earlier H2Ds drain
 
 // Where a large item's bytes come from.
 struct LargeSource {
@@ -688,14 +690,15 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
     static_assert(sizeof(Res) + 64 <= kRes, "results area");
     std::vector<uint8_t> h_res((size_t)n * kRes, 0);
     for (int q = 0; q < n; ++q) reinterpret_cast<Res*>(h_res.data() + (size_t)q * kRes)->len = jobs[q].L;
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < kNBounce; ++b) {
         if (!c->h_bounce[b] && hipHostMalloc(&c->h_bounce[b], kBounce, hipHostMallocDefault) != hipSuccess) {
             c->h_bounce[b] = nullptr;
             return nomem();
         }
         if (!c->ev_bounce[b]) HIP_TRY(hipEventCreateWithFlags(&c->ev_bounce[b], hipEventDisableTiming));
-        if (!c->ev_piece_free[b]) HIP_TRY(hipEventCreateWithFlags(&c->ev_piece_free[b], hipEventDisableTiming));
     }
+    for (int b = 0; b < 2; ++b)
+        if (!c->ev_piece_free[b]) HIP_TRY(hipEventCreateWithFlags(&c->ev_piece_free[b], hipEventDisableTiming));
     uint64_t* sums = nullptr;
     oxh::ScratchLease lease(c->stream);  // block sums of the two rounds in flight
     const uint64_t sums_per = (cap >> 10) * 8;
@@ -725,8 +728,8 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
     auto copy_piece = [&](int q, uint64_t off, uint64_t plen, uint8_t* d) -> bool {
         LargeSource& src = *jobs[q].src;
         State& S = st[q];
-        for (uint64_t o = 0, part = 0; o < plen; o += kBounce, ++part) {  // bounce-buffer path
-            const int bb = (int)(part & 1);
+        for (uint64_t o = 0; o < plen; o += kBounce) {  // bounce-buffer path
+            const int bb = (int)(c->bounce_next++ % kNBounce);
             if (c->bounce_used[bb] && hipEventSynchronize(c->ev_bounce[bb]) != hipSuccess) return false;
             const uint64_t m = std::min(kBounce, plen - o);
             src.will_need(off + o + m, 2 * kBounce);  // two bounce pieces ahead while the pool reads this one
@@ -754,7 +757,10 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
                 return false;
             c->bounce_used[bb] = true;
         }
-        return hipStreamSynchronize(c->copy_stream) == hipSuccess;
+        // no wait here: the piece's kernels wait for the copy stream through ev_copy, and a bounce
+        // buffer is refilled only after its own H2D (ev_bounce), so the next piece's reads overlap
+        // this piece's last copies
+        return true;
     };
     // With OXH_BIG_DIRECT=1, pieces whose pages are in the page cache are pinned in place and copied
     // asynchronously; the next round's pieces are pinned while this round's copies run, and a round's
@@ -1006,11 +1012,12 @@ int oxh_ctx_destroy(oxh_ctx* c) {
         if (c->ev_done[s]) (void)hipEventDestroy(c->ev_done[s]);
     }
     if (c->d_big) (void)hipFree(c->d_big);
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < kNBounce; ++b) {
         if (c->h_bounce[b]) (void)hipHostFree(c->h_bounce[b]);
         if (c->ev_bounce[b]) (void)hipEventDestroy(c->ev_bounce[b]);
-        if (c->ev_piece_free[b]) (void)hipEventDestroy(c->ev_piece_free[b]);
     }
+    for (int b = 0; b < 2; ++b)
+        if (c->ev_piece_free[b]) (void)hipEventDestroy(c->ev_piece_free[b]);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     delete c->pool;
