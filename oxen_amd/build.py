@@ -45,6 +45,8 @@ NATIVE_TEST_SRC = os.path.join(ROOT, "tests", "native", "test_hasher.cpp")
 NATIVE_TEST = os.path.join(ROOT, "tests", "native", "test_hasher")
 COMMIT_CLI_SRC = os.path.join(ROOT, "tests", "native", "commit_tree_cli.cpp")
 COMMIT_CLI = os.path.join(ROOT, "tests", "native", "commit_tree_cli")
+FAKE_HELPER_SRC = os.path.join(ROOT, "tests", "native", "fake_pool_helper.cpp")
+FAKE_HELPER = os.path.join(ROOT, "tests", "native", "fake_pool_helper")  # tests only: the pool without a GPU
 
 
 def _stale(target: str, deps: list[str]) -> bool:
@@ -66,6 +68,8 @@ def build_host(force: bool = False, verbose: bool = False) -> str:
         (NATIVE_TEST, [NATIVE_TEST_SRC, HOST_HDR, HOST_LIB],
          ["g++", "-std=c++17", "-O2", "-Wall", "-o", NATIVE_TEST + ".tmp", NATIVE_TEST_SRC,
           f"-L{HERE}", "-l:liboxen_hasher.so", "-l:liboxen_hash.so", "-Wl,-rpath,$ORIGIN/../../oxen_amd"]),
+        (FAKE_HELPER, [FAKE_HELPER_SRC, os.path.join(CSRC, "reader_pool.hpp")],
+         ["g++", "-std=c++17", "-O2", "-Wall", "-o", FAKE_HELPER + ".tmp", FAKE_HELPER_SRC]),
         (COMMIT_CLI, [COMMIT_CLI_SRC, COMMIT_HDR, HOST_HDR, HOST_LIB],
          ["g++", "-std=c++17", "-O2", "-Wall", "-o", COMMIT_CLI + ".tmp", COMMIT_CLI_SRC,
           f"-L{HERE}", "-l:liboxen_hasher.so", "-l:liboxen_hash.so", "-Wl,-rpath,$ORIGIN/../../oxen_amd"]),

@@ -51,6 +51,79 @@ def test_pool_fails_loudly_without_a_gpu(built_lib):
     assert e.value.code == _capi.OXH_ERR_NODEVICE, str(e.value)
 
 
+@pytest.fixture
+def fake_helper(built_lib, monkeypatch):
+    """The pool's mechanics on any host: OXH_HELPER points at tests/native/fake_pool_helper (the same
+    wire protocol, no GPU; its "digest" is (size, the file's index in the call))."""
+    from oxen_amd import build
+
+    build.build_host()
+    monkeypatch.setenv("OXH_HELPER", build.FAKE_HELPER)
+    return build.FAKE_HELPER
+
+
+def _fake_want(paths, meta):
+    sizes = [os.path.getsize(p) if os.path.isfile(p) else None for p in paths]
+    out = np.array([[s or 0, (i + (1 << 40 if meta else 0)) if s is not None else 0] for i, s in enumerate(sizes)],
+                   dtype=np.uint64).reshape(-1, 2)
+    return out, np.array([s or 0 for s in sizes], dtype=np.uint64), np.array([0 if s is not None else 3 for s in sizes], dtype=np.int32)
+
+
+@pytest.mark.parametrize("procs,devices", [(1, (0,)), (3, (0, 1)), (4, (2, 3, 5))])
+def test_pool_mechanics_with_a_fake_helper(fake_helper, tmp_path, procs, devices):
+    """Every item lands in its own slot whatever the split; meta sizes reach the helpers; the shared
+    region grows between calls (helpers re-map it); empty calls and fewer files than helpers."""
+    from oxen_amd.procpool import ShardedFileHasher
+
+    paths = _tree(tmp_path, 300)
+    meta = [os.path.getsize(p) if os.path.exists(p) else 0 for p in paths]
+    with ShardedFileHasher(procs=procs, devices=devices, threads=2) as pool:
+        assert len(set(pool.pids())) == procs
+        for m in (None, meta):
+            got = pool.hash_files(paths, m)
+            for g, w in zip(got, _fake_want(paths, m is not None)):
+                assert np.array_equal(g, w)
+        big = paths * 40  # ~12 000 paths: a larger region
+        got = pool.hash_files(big)
+        for g, w in zip(got, _fake_want(big, False)):
+            assert np.array_equal(g, w)
+        assert pool.hash_files(paths[:1])[0][0, 0] == os.path.getsize(paths[0])
+        assert pool.hash_files([])[0].shape == (0, 2)
+
+
+def test_pool_fake_helper_concurrency_and_death(fake_helper, tmp_path):
+    """Concurrent callers serialise and each gets its own answers; a killed helper fails the call
+    and every later one; a helper that fails at start-up fails creation with its status."""
+    import signal
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oxen_amd import _capi
+    from oxen_amd.procpool import ShardedFileHasher
+
+    paths = _tree(tmp_path, 200)
+    with ShardedFileHasher(procs=3, threads=2) as pool:
+        lists = [paths[k::4] for k in range(4)]
+
+        def call(ps):
+            got = pool.hash_files(ps)
+            return all(np.array_equal(g, w) for g, w in zip(got, _fake_want(ps, False)))
+
+        with ThreadPoolExecutor(4) as ex:
+            assert all(ex.map(call, lists * 5))
+        os.kill(pool.pids()[2], signal.SIGKILL)
+        with pytest.raises(_capi.OxenError):
+            pool.hash_files(paths)
+        with pytest.raises(_capi.OxenError, match="unusable"):
+            pool.hash_files(paths)
+    os.environ["OXH_FAKE_FAIL_DEVICE"] = "1"
+    try:
+        with pytest.raises(_capi.OxenError) as e:
+            ShardedFileHasher(procs=2, devices=(0, 1))
+        assert e.value.code == _capi.OXH_ERR_NODEVICE and "no device" in str(e.value)
+    finally:
+        del os.environ["OXH_FAKE_FAIL_DEVICE"]
+
+
 def test_pool_rejects_bad_arguments(built_lib, monkeypatch):
     from oxen_amd import _capi
     from oxen_amd.procpool import ShardedFileHasher
