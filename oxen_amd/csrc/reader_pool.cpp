@@ -115,7 +115,8 @@ void reap(oxh_pool* p, bool polite) {
         bool alive = false;
         for (auto& h : p->helpers)
             if (h.pid > 0) {
-                if (waitpid(h.pid, nullptr, WNOHANG) == h.pid) h.pid = -1;
+                const pid_t w = waitpid(h.pid, nullptr, WNOHANG);
+                if (w == h.pid || (w < 0 && errno == ECHILD)) h.pid = -1;  // ECHILD: SIGCHLD ignored, reaped already
                 else alive = true;
             }
         if (!alive) return;
@@ -124,7 +125,8 @@ void reap(oxh_pool* p, bool polite) {
     for (auto& h : p->helpers)
         if (h.pid > 0) {
             kill(h.pid, SIGKILL);
-            waitpid(h.pid, nullptr, 0);
+            while (waitpid(h.pid, nullptr, 0) < 0 && errno == EINTR) {
+            }
             h.pid = -1;
         }
 }

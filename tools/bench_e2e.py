@@ -53,7 +53,8 @@ def sharded(a, paths, meta, nbytes, cpu_call, drop_cache):
     blob, offs = pack_paths(paths)  # packed once, outside the timing (as c_paths is)
     for P in [int(x) for x in a.procs.split(",") if x]:
         th = max(1, a.threads // P)
-        pools = {"gpu": ShardedFileHasher(procs=P, threads=th), "cpu": CpuShardedLoop(procs=P, threads=th)}
+        pools = {"gpu": ShardedFileHasher(procs=P, threads=th, staging_bytes=a.pool_staging_mib << 20),
+                 "cpu": CpuShardedLoop(procs=P, threads=th)}
         try:
             ts = {"gpu": [], "cpu": []}
             ok = True
@@ -92,6 +93,7 @@ def main():
     ap.add_argument("--staging-mib", default="16,64,256", help="staging slot sizes to sweep (warm cache)")
     ap.add_argument("--procs", default="2,4", help="reader process counts for the sharded runs")
     ap.add_argument("--only-procs", action="store_true", help="skip the add / fsck / staging parts")
+    ap.add_argument("--pool-staging-mib", type=int, default=0, help="staging slot size of the pool's helpers (0 = default)")
     a = ap.parse_args()
 
     import numpy as np
