@@ -116,10 +116,11 @@ __device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t b, uint32_t c) {
     return r;
 }
 __device__ __forceinline__ uint32_t min_u32(uint32_t a, uint32_t b) { return a < b ? a : b; }
+// min of three: the backend forms v_min3_u32 from the nested umin. (An inline-asm v_min3 made the
+// compiler put an `s_nop 0` between every two asm blocks -- it cannot see their hazards -- one wasted
+// issue slot per 4 bytes in F1, ~5 % of its issue-bound loop.)
 __device__ __forceinline__ uint32_t min3_u32(uint32_t a, uint32_t b, uint32_t c) {
-    uint32_t r;
-    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
+    return __builtin_elementwise_min(__builtin_elementwise_min(a, b), c);
 }
 
 // 16 bytes at p[pos .. pos+16) of a file of length flen as four little-endian words (zeros past the
