@@ -209,7 +209,10 @@ def files_modified(paths: Sequence[str], sizes: Sequence[int], node_bytes: Seque
                 continue
             if isinstance(f, BaseException):
                 fk[i] = _capi.OXH_META_ERROR
-            elif isinstance(f, str) and f == TEXT:
+            elif isinstance(f, str):
+                if f != TEXT:
+                    raise _capi.OxenError(f"files_modified: file_metadata[{i}] is a string other than hasher.TEXT",
+                                          _capi.OXH_ERR_INVALID)
                 fk[i] = _capi.OXH_META_TEXT
             elif isinstance(f, (int, np.integer)) and not isinstance(f, bool):
                 fk[i], fhv[i] = _capi.OXH_META_GIVEN, int(f)
