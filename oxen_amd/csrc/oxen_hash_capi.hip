@@ -978,7 +978,7 @@ int oxh_ctx_create(int device, uint64_t staging_bytes, oxh_ctx** out) {
     const char* fl = getenv("OXH_FLUSH_MIB");
     c->flush_bytes = std::min<uint64_t>(c->stage_bytes, (fl ? (uint64_t)atoll(fl) : 16ull) << 20);
     c->pool = new oxh::Pool(default_threads());
-    c->rpool = new oxh::Pool(default_threads());
+    c->rpool = new oxh::Pool(default_threads(), /*private_fds=*/true);  // readers use only their own fds
     c->engine = std::thread(engine_main, c);
     *out = c;
     return OXH_OK;

@@ -1,5 +1,11 @@
 // oxen_amd/csrc/pool.hpp -- the runtime's blocking thread pool (file readers / copiers / writers).
 #pragma once
+#include <dirent.h>
+#include <sched.h>
+#include <stdlib.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <atomic>
 #include <condition_variable>
 #include <functional>
@@ -8,10 +14,40 @@
 #include <vector>
 
 namespace oxh {
+// A worker of a pool made with private_fds gets a file-descriptor table of its own: it calls
+// unshare(CLONE_FILES) and drops every descriptor the copy inherited (stdin/out/err stay), so the
+// files it opens and closes never take the table lock the rest of the process takes. On the MI355X
+// boxes that lock is the warm small-file floor of one process: 200 000 open + close pairs take
+// 0.28 s in one process whatever its thread count and 0.13-0.16 s in 2-4 processes
+// (profiles/r02e_open_procs.json); tools/open_probe.cpp UNSHARE=1 measures the same threads with
+// private tables. Only for workers that use nothing but the descriptors they open themselves (the
+// streaming readers). OXH_SHARED_FDS=1 turns it off.
+inline void make_fd_table_private() {
+    const char* e = getenv("OXH_SHARED_FDS");
+    if (e && atoi(e) != 0) return;
+    if (unshare(CLONE_FILES) != 0) return;  // keep sharing: correct, just slower
+#ifdef SYS_close_range
+    if (syscall(SYS_close_range, 3u, ~0u, 0u) == 0) return;
+#endif
+    if (DIR* d = opendir("/proc/thread-self/fd")) {  // older kernels: close the copies one by one
+        std::vector<int> fds;
+        while (dirent* de = readdir(d)) {
+            const int fd = atoi(de->d_name);
+            if (fd > 2 && fd != dirfd(d)) fds.push_back(fd);
+        }
+        closedir(d);
+        for (int fd : fds) close(fd);
+    }
+}
+
 class Pool {
    public:
-    explicit Pool(int n) {
-        for (int i = 0; i < n; ++i) th_.emplace_back([this] { run(); });
+    explicit Pool(int n, bool private_fds = false) {
+        for (int i = 0; i < n; ++i)
+            th_.emplace_back([this, private_fds] {
+                if (private_fds) make_fd_table_private();
+                run();
+            });
     }
     ~Pool() {
         {

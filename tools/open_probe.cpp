@@ -11,10 +11,14 @@
 //   dirfd_oc      openat(dirfd, basename) + close
 // PROCS=P in the environment splits the list into P contiguous parts read by P forked processes of
 // T/P threads each (separate file tables and address spaces): does the floor belong to one process?
+// UNSHARE=1: every reader thread first calls unshare(CLONE_FILES) -- its own file-descriptor table
+// (threads still share the address space), so its open/close no longer take the process-wide table
+// lock the other threads take.
 // Prints one JSON line per run.
 //   g++ -O2 -std=c++17 -pthread tools/open_probe.cpp -o tools/open_probe
 //   find DIR -type f | tools/open_probe 16 full dirfd nostat dirfd_nostat openclose dirfd_oc
 #include <fcntl.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <sys/stat.h>
@@ -83,6 +87,7 @@ int main(int argc, char** argv) {
         std::vector<std::thread> th;
         for (int t = 0; t < (P > 1 ? TP : T); ++t)
             th.emplace_back([&] {
+                if (getenv("UNSHARE") && atoi(getenv("UNSHARE"))) unshare(CLONE_FILES);
                 std::vector<char> buf(1 << 20);
                 uint64_t mine = 0, err = 0;
                 for (;;) {
@@ -130,8 +135,8 @@ int main(int argc, char** argv) {
             if (!WIFEXITED(st) || WEXITSTATUS(st)) errors.fetch_add(1);
         }
         const double dt = now() - t0;
-        printf("{\"mode\": \"%s\", \"procs\": %d, \"threads\": %d, \"files\": %zu, \"bytes\": %llu, \"errors\": %llu, \"s\": %.4f}\n",
-               mode.c_str(), P, T, n, (unsigned long long)bytes.load(), (unsigned long long)errors.load(), dt);
+        printf("{\"mode\": \"%s\", \"unshare\": %d, \"procs\": %d, \"threads\": %d, \"files\": %zu, \"bytes\": %llu, \"errors\": %llu, \"s\": %.4f}\n",
+               mode.c_str(), getenv("UNSHARE") ? atoi(getenv("UNSHARE")) : 0, P, T, n, (unsigned long long)bytes.load(), (unsigned long long)errors.load(), dt);
         fflush(stdout);
     }
     return 0;
