@@ -416,8 +416,9 @@ struct Trace {
 //  * open_stream() / close_stream(): a file larger than a staging slot, whose bytes pass through
 //    bounce buffers piece by piece: the engine writes each piece to the returned fd while the
 //    digest is still being computed, then hands over the digest (or ok = false);
-//  * commit(): everything put / closed so far is made durable and visible; the engine calls it
-//    before the items' callers are released.
+//  * commit(): everything put / closed so far is to be made durable and visible; the engine calls it
+//    once per drained slot. The sink may do that work asynchronously; its owner waits for it before
+//    reading outcomes.
 // Publish failures are the sink's own business (oxh_add_files turns them into per-item statuses).
 struct ItemSink {
     virtual ~ItemSink() = default;
@@ -1875,7 +1876,9 @@ void run_stream(oxh_ctx* c) {
                 rc = fail(OXH_ERR_HIP, std::string("slot event: ") + hipGetErrorString(q));
                 break;
             }
+            const double td = Trace::now();
             drain_files(fs, t, pend[t]);
+            tr.drain += Trace::now() - td;
             fs.slot[t].state.store(0, std::memory_order_release);
             --nbusy;
             progressed = true;
@@ -2000,9 +2003,9 @@ void run_stream(oxh_ctx* c) {
         readers.wait();
     }
     if (tr.on)
-        fprintf(stderr, "[oxh] run: requests=%zu files=%llu slots=%d total=%.3fs submit=%.3fs readers=%d rc=%d\n",
+        fprintf(stderr, "[oxh] run: requests=%zu files=%llu slots=%d total=%.3fs submit=%.3fs drain=%.3fs readers=%d rc=%d\n",
                 fs.reqs.size(), (unsigned long long)fs.files, tr.batches, Trace::now() - t_start, tr.submit,
-                fs.nreaders, rc);
+                tr.drain, fs.nreaders, rc);
 }
 
 // The context's engine thread: one run per burst of requests.
@@ -2226,18 +2229,44 @@ int make_temp(const std::string& dir, std::string& tmp) {
 // write a `data.oxentmp.<random>` sibling, make the data durable, rename it to
 // {root}/{hex[..2]}/{hex[2..]}/data (local.rs:66-75), make the rename durable; a blob already in the
 // store is not rewritten (local.rs:112). AtomicTempFile::commit fsyncs each file and its parent; here
-// one syncfs() per drained slot covers every temp of the slot before any of them is renamed, and a
-// second one covers the renames -- the same ordering, two barriers per slot instead of two per file.
+// one syncfs() covers every temp of a drained slot before any of them is renamed, and a second one
+// covers the renames -- the same ordering, two barriers per slot instead of two per file.
+// The barriers run on a committer thread: commit() hands the slot's temps over and returns, so the
+// engine reads, hashes and writes the next slots while the disk takes the last ones (a committer
+// that falls behind takes every queued slot under one pair of barriers). wait() returns once every
+// handed-over temp is published; oxh_add_files calls it before it reads the outcomes.
+// OXH_PUBLISH_INLINE=1 publishes inside commit() instead (the r02 form, for A/B).
+// OXH_PUBLISH_SYNC=fsync replaces the two syncfs barriers with the reference's own per-blob steps
+// (fsync the temp, rename, fsync its parent), run by the committer's threads: for filesystems where
+// syncfs is costly (one shared with other tenants' dirty data).
 // Identical content twice in one call is published once; every duplicate shares that publish's
 // outcome (finish()).
 class VersionPublisher final : public ItemSink {
    public:
-    VersionPublisher(oxh_ctx* c, std::string root, uint64_t n) : c_(c), root_(std::move(root)), owner_(n, kNone), result_(n, 0) {}
+    VersionPublisher(oxh_ctx* c, std::string root, uint64_t n)
+        : c_(c), root_(std::move(root)), owner_(n, kNone), result_(n, 0),
+          inline_(env_flag("OXH_PUBLISH_INLINE")),
+          fsync_each_(getenv("OXH_PUBLISH_SYNC") && !strcmp(getenv("OXH_PUBLISH_SYNC"), "fsync")) {}
     ~VersionPublisher() override {
+        {
+            std::lock_guard<std::mutex> g(cq_mu_);
+            quit_ = true;
+        }
+        cq_cv_.notify_all();
+        if (committer_.joinable()) committer_.join();  // publishes whatever is still queued first
+        if (trace_)
+            fprintf(stderr, "[oxh] publish: put=%.3fs (thread time) publish=%.3fs batches=%d wait=%.3fs inline=%d fsync=%d\n",
+                    put_s_.load() * 1e-9, publish_s_ * 1e-9, nbatches_, wait_s_ * 1e-9, (int)inline_, (int)fsync_each_);
+        delete rpool_;
         if (root_fd_ >= 0) close(root_fd_);
     }
 
     void put(uint64_t id, const uint8_t* bytes, uint64_t len, uint64_t lo, uint64_t hi) override {
+        const Clock t0(trace_);
+        put_impl(id, bytes, len, lo, hi);
+        put_s_.fetch_add(t0.ns(), std::memory_order_relaxed);
+    }
+    void put_impl(uint64_t id, const uint8_t* bytes, uint64_t len, uint64_t lo, uint64_t hi) {
         if (!claim(id, lo, hi)) return;
         std::string dir, path;
         target(lo, hi, dir, path);
@@ -2303,37 +2332,24 @@ class VersionPublisher final : public ItemSink {
             batch.swap(staged_);
         }
         if (batch.empty()) return;
-        // 1. the data of every temp is durable before any rename (AtomicTempFile::commit's sync_all,
-        //    atomic_file.rs:122); should syncfs fail, each temp is fsynced on its own
-        const bool synced = sync_fs();
-        auto each = [&](const std::function<void(Staged&)>& fn) {
-            if (batch.size() < 64) {
-                for (Staged& s : batch) fn(s);
-                return;
-            }
-            if (!c_->wpool) c_->wpool = new oxh::Pool(c_->pool->size());
-            const int ntasks = (int)std::min<size_t>(batch.size(), (size_t)c_->wpool->size() * 4);
-            c_->wpool->parallel_for(ntasks, [&](int t) {
-                for (size_t k = (size_t)t; k < batch.size(); k += (size_t)ntasks) fn(batch[k]);
-            });
-        };
-        each([&](Staged& s) {
-            bool ok = true;
-            if (!synced) {
-                const int fd = open(s.tmp.c_str(), O_RDONLY | O_CLOEXEC);
-                ok = fd >= 0 && fsync(fd) == 0;
-                if (fd >= 0) close(fd);
-            }
-            // 2. publish (atomic_file.rs:132-139): a failed rename removes the temp
-            if (ok && rename(s.tmp.c_str(), s.path.c_str()) == 0) {
-                result_[s.id] = kWritten;
-            } else {
-                unlink(s.tmp.c_str());
-                result_[s.id] = kFailed;
-            }
-        });
-        // 3. the renames themselves, best effort like the reference's parent fsync (:141-156)
-        (void)sync_fs();
+        if (inline_) {
+            publish(batch);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(cq_mu_);
+            cq_.push_back(std::move(batch));
+            if (!committer_.joinable()) committer_ = std::thread([this] { committer(); });
+        }
+        cq_cv_.notify_all();
+    }
+
+    // every temp handed to commit() so far is published (or failed)
+    void wait() {
+        const Clock t0(trace_);
+        std::unique_lock<std::mutex> g(cq_mu_);
+        cq_cv_.wait(g, [&] { return cq_.empty() && !publishing_; });
+        wait_s_ += t0.ns();
     }
 
     // Per-item outcome into the caller's arrays: a file whose content failed to publish (its own
@@ -2360,6 +2376,85 @@ class VersionPublisher final : public ItemSink {
         uint64_t id;
         std::string tmp, path;
     };
+    struct Clock {  // OXH_TRACE: wall time of a section, 0 when tracing is off
+        std::chrono::steady_clock::time_point t;
+        bool on;
+        explicit Clock(bool o) : on(o) {
+            if (on) t = std::chrono::steady_clock::now();
+        }
+        uint64_t ns() const {
+            return on ? (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t).count() : 0;
+        }
+    };
+    static bool env_flag(const char* name) {
+        const char* e = getenv(name);
+        return e && atoi(e) != 0;
+    }
+
+    void committer() {
+        std::unique_lock<std::mutex> g(cq_mu_);
+        for (;;) {
+            cq_cv_.wait(g, [&] { return quit_ || !cq_.empty(); });
+            if (cq_.empty()) return;  // quit, nothing left
+            std::vector<Staged> batch = std::move(cq_.front());
+            for (size_t k = 1; k < cq_.size(); ++k)
+                for (Staged& st : cq_[k]) batch.push_back(std::move(st));
+            cq_.clear();
+            publishing_ = true;
+            g.unlock();
+            publish(batch);
+            g.lock();
+            publishing_ = false;
+            cq_cv_.notify_all();
+        }
+    }
+
+    void publish(std::vector<Staged>& batch) {
+        const Clock t0(trace_);
+        publish_impl(batch);
+        publish_s_ += t0.ns();
+        ++nbatches_;
+    }
+    void publish_impl(std::vector<Staged>& batch) {
+        // 1. the data of every temp is durable before any rename (AtomicTempFile::commit's sync_all,
+        //    atomic_file.rs:122); should syncfs fail, each temp is fsynced on its own
+        const bool synced = !fsync_each_ && sync_fs();
+        auto each = [&](const std::function<void(Staged&)>& fn) {
+            if (batch.size() < 64) {
+                for (Staged& s : batch) fn(s);
+                return;
+            }
+            if (!rpool_) rpool_ = new oxh::Pool(c_->pool->size());  // the publisher's own: wpool may be busy with put()
+            const int ntasks = (int)std::min<size_t>(batch.size(), (size_t)rpool_->size() * 4);
+            rpool_->parallel_for(ntasks, [&](int t) {
+                for (size_t k = (size_t)t; k < batch.size(); k += (size_t)ntasks) fn(batch[k]);
+            });
+        };
+        each([&](Staged& s) {
+            bool ok = true;
+            if (!synced) {
+                const int fd = open(s.tmp.c_str(), O_RDONLY | O_CLOEXEC);
+                ok = fd >= 0 && fsync(fd) == 0;
+                if (fd >= 0) close(fd);
+            }
+            // 2. publish (atomic_file.rs:132-139): a failed rename removes the temp
+            if (ok && rename(s.tmp.c_str(), s.path.c_str()) == 0) {
+                result_[s.id] = kWritten;
+                if (fsync_each_) {  // 3. the rename, best effort: the parent's fsync (:141-156)
+                    const int dfd = open(s.path.substr(0, s.path.rfind('/')).c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+                    if (dfd >= 0) {
+                        (void)fsync(dfd);
+                        close(dfd);
+                    }
+                }
+            } else {
+                unlink(s.tmp.c_str());
+                result_[s.id] = kFailed;
+            }
+        });
+        // 3. the renames themselves, best effort like the reference's parent fsync (:141-156)
+        if (!fsync_each_) (void)sync_fs();
+    }
 
     // the first item with this digest publishes it; the others share its outcome
     bool claim(uint64_t id, uint64_t lo, uint64_t hi) {
@@ -2391,7 +2486,18 @@ class VersionPublisher final : public ItemSink {
     std::vector<uint64_t> owner_;  // per item: the item that publishes its content (itself if first)
     std::vector<int8_t> result_;   // per publishing item: kWritten / kExisted / kFailed
     std::vector<Staged> staged_;   // temps written, waiting for commit()
-    int root_fd_ = -1;
+    int root_fd_ = -1;             // the committer's only (syncfs)
+    const bool inline_, fsync_each_;
+    std::mutex cq_mu_;
+    std::condition_variable cq_cv_;
+    std::vector<std::vector<Staged>> cq_;  // committed slots waiting for the committer
+    bool publishing_ = false, quit_ = false;
+    std::thread committer_;
+    oxh::Pool* rpool_ = nullptr;  // renames / fallback fsyncs
+    const bool trace_ = getenv("OXH_TRACE") != nullptr;
+    std::atomic<uint64_t> put_s_{0};
+    uint64_t publish_s_ = 0, wait_s_ = 0;  // committer thread / owner thread
+    int nbatches_ = 0;
 };
 
 }  // namespace
@@ -2403,6 +2509,7 @@ int oxh_add_files(oxh_ctx* c, const char* const* paths, uint64_t n, const char* 
     VersionPublisher pub(c, versions_root ? versions_root : "", n);
     const int rc = hash_files_impl(c, paths, n, out, sizes, status, nullptr, &pub);
     if (rc) return rc;
+    pub.wait();
     pub.finish(n, out, status, stored);
     return OXH_OK;
 }

@@ -3,7 +3,7 @@ the warm C3 tree, in ONE process: context A is created with private tables (the 
 with OXH_SHARED_FDS=1 in the environment at its creation; calls alternate A, B, the CPU reference
 loop (oracle/), 7 rounds; medians printed as one JSON line. Digests checked equal.
 
-    python tools/fds_ab.py [--images 200000] [--rounds 7]
+    python tools/fds_ab.py [--images 200000] [--rounds 7] [--pool-procs 2]
 """
 from __future__ import annotations
 
@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--dir", default=os.path.join(os.environ.get("TMPDIR", "/tmp"), "oxh_c3_fds"))
     ap.add_argument("--staging-mib", default="", help="extra private-fd contexts with these slot sizes")
+    ap.add_argument("--pool-procs", type=int, default=0, help="also A/B reader-process pools of this many helpers")
     a = ap.parse_args()
 
     import numpy as np
@@ -43,6 +44,14 @@ def main():
     del os.environ["OXH_SHARED_FDS"]
     extra = {f"gpu_private_fds_staging{m}MiB": _capi.Context(0, staging_bytes=m << 20)
              for m in [int(x) for x in a.staging_mib.split(",") if x]}
+    pools = {}
+    if a.pool_procs:
+        from oxen_amd.procpool import ShardedFileHasher
+
+        pools["pool%d_private_fds" % a.pool_procs] = ShardedFileHasher(procs=a.pool_procs)
+        os.environ["OXH_SHARED_FDS"] = "1"  # the helpers inherit it at spawn
+        pools["pool%d_shared_fds" % a.pool_procs] = ShardedFileHasher(procs=a.pool_procs)
+        del os.environ["OXH_SHARED_FDS"]
     oracle.build()
     L, O = _capi.lib(), oracle.lib()
     threads = min(16, os.cpu_count() or 1)
@@ -67,6 +76,18 @@ def main():
     calls = {"gpu_private_fds": lambda: gpu(ctx_a), "gpu_shared_fds": lambda: gpu(ctx_b), "cpu_ref_loop": cpu}
     for k, c in extra.items():
         calls[k] = (lambda c=c: gpu(c))
+
+    from oxen_amd.procpool import pack_paths
+
+    blob, offs = pack_paths(paths)  # once, outside the timing (like the C-string table above)
+
+    def pooled(pool):
+        t0 = time.perf_counter()
+        out, _, st = pool.hash_files_packed(blob, offs)
+        return time.perf_counter() - t0, out, st
+
+    for k, pl in pools.items():
+        calls[k] = (lambda pl=pl: pooled(pl))
     for f in calls.values():
         f()  # warm
     ts = {k: [] for k in calls}
@@ -88,6 +109,8 @@ def main():
     ctx_b.close()
     for c in extra.values():
         c.close()
+    for pl in pools.values():
+        pl.close()
     shutil.rmtree(a.dir, ignore_errors=True)
 
 
