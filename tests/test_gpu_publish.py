@@ -36,7 +36,16 @@ def _tree(root):
     return sorted(os.path.relpath(os.path.join(dp, f), root) for dp, _, fs in os.walk(root) for f in fs)
 
 
-def test_add_files_streams_oversize_blobs_and_shares_publish_failures(cuda, oracle_lib, tmp_path):
+PUBLISH_MODES = {"committer": {}, "inline": {"OXH_PUBLISH_INLINE": "1"}, "fsync_each": {"OXH_PUBLISH_SYNC": "fsync"},
+                 "inline_fsync_each": {"OXH_PUBLISH_INLINE": "1", "OXH_PUBLISH_SYNC": "fsync"}}
+
+
+@pytest.mark.parametrize("mode", sorted(PUBLISH_MODES))
+def test_add_files_streams_oversize_blobs_and_shares_publish_failures(cuda, oracle_lib, tmp_path, monkeypatch, mode):
+    """Every publish form (committer thread or inline drain; two syncfs barriers or the reference's
+    per-blob fsync / rename / parent fsync) gives the same store and the same per-item outcomes."""
+    for k, v in PUBLISH_MODES[mode].items():
+        monkeypatch.setenv(k, v)
     from oracle import oracle
     from oxen_amd import _capi, hasher
 
