@@ -189,6 +189,8 @@ int oxh_pool_hash_files(oxh_pool* pool, const char* const* paths, const uint64_t
                         uint64_t* out, uint64_t* sizes, int32_t* status);
 /* procs = number of helpers; pids (may be NULL) receives their process ids. */
 int oxh_pool_size(oxh_pool* pool, int* procs, int* pids);
+/* Not while another thread is inside a call on the same pool (the caller owns the pool's lifetime,
+ * as with oxh_ctx_destroy). */
 int oxh_pool_destroy(oxh_pool* pool);
 
 /* Text-metadata fusion (K1T): the same digests as oxh_hash_files plus, per file, the counts liboxen's

@@ -706,6 +706,15 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
     if (lease.get(2 * sums_per * 8 * (uint64_t)n, (void**)&sums) != hipSuccess) return nomem();
     HIP_TRY(hipMemcpyAsync(d_res_all, h_res.data(), h_res.size(), hipMemcpyHostToDevice, c->stream));
 
+    // one copy-done event per item (created before any sink temp exists: a failure here leaves nothing behind)
+    std::vector<hipEvent_t> ev_copy(n, nullptr);
+    for (int q = 0; q < n; ++q)
+        if (hipEventCreateWithFlags(&ev_copy[q], hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            for (hipEvent_t e : ev_copy)
+                if (e) (void)hipEventDestroy(e);
+            return fail(OXH_ERR_HIP, "large-item events");
+        }
     struct State {
         uint64_t k = 0;  // pieces 0 .. k-1 hold P bytes each; the last one L - k*P bytes, in [1025, P + 1024]
         std::string sink_tmp;
@@ -766,14 +775,6 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
     // With OXH_BIG_DIRECT=1, pieces whose pages are in the page cache are pinned in place and copied
     // asynchronously; the next round's pieces are pinned while this round's copies run, and a round's
     // pins are released once its copies are done.
-    std::vector<hipEvent_t> ev_copy(n, nullptr);
-    for (int q = 0; q < n; ++q)
-        if (hipEventCreateWithFlags(&ev_copy[q], hipEventDisableTiming) != hipSuccess) {
-            (void)hipGetLastError();
-            for (hipEvent_t e : ev_copy)
-                if (e) (void)hipEventDestroy(e);
-            return fail(OXH_ERR_HIP, "large-item events");
-        }
     std::vector<const uint8_t*> pinned(n, nullptr), next_pin(n, nullptr);
     std::vector<std::pair<int, const uint8_t*>> to_unpin;  // (item, pinned range) of copies in flight
     auto piece_len = [&](int q, uint64_t r) { return r < st[q].k ? P : jobs[q].L - r * P; };
