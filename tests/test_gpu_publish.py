@@ -162,3 +162,33 @@ def test_host_buffers_larger_than_staging(cuda, oracle_lib, monkeypatch, piece_m
     with _capi.Context(0, staging_bytes=1 << 20) as c:
         assert hasher.hash_buffers_128bit(bufs, c) == want
         assert hasher.hash_streams_128bit(bufs, c) == want
+
+
+def test_concurrent_adds_into_one_store(cuda, oracle_lib, tmp_path):
+    """Several threads add overlapping file lists into one version store through one context (their
+    requests join the engine's live run; each call's publisher commits on its own thread): every
+    blob ends up whole under its digest, no temp is left, and each call reports every file."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import oracle
+    from oxen_amd import _capi, hasher
+
+    blobs = [_small(k) for k in range(40)] + [_big(0)]
+    paths = [_write(tmp_path, f"f{k}", b) for k, b in enumerate(blobs)]
+    want = [oracle.xxh3_128_int(b) for b in blobs]
+    root = str(tmp_path / "store" / "versions" / "files")
+    lists = [list(range(k, len(paths), 3)) + list(range(0, len(paths), 5)) for k in range(3)] + [list(range(len(paths)))]
+    with _capi.Context(0, staging_bytes=2 << 20) as c:
+        def add(idx):
+            d, _, st, stored = hasher.add_files([paths[i] for i in idx], root, c)
+            return idx, d, st, stored
+
+        with ThreadPoolExecutor(4) as ex:
+            results = list(ex.map(add, lists * 2))
+    for idx, d, st, stored in results:
+        assert st == [0] * len(idx) and d == [want[i] for i in idx]
+    assert sum(s for _, _, _, stored in results for s in stored) >= len(set(want))
+    for w, b in zip(want, blobs):
+        with open(hasher.version_path(root, w), "rb") as f:
+            assert f.read() == b
+    assert not any(".oxentmp." in f for f in _tree(root)), _tree(root)
