@@ -1,9 +1,14 @@
 // oxen_amd/host/oxen_hasher.cpp -- liboxen `util::hasher` mirror over the C ABI (see the header).
 #include "oxen_hasher.hpp"
 
+#include <dirent.h>
 #include <errno.h>
 #include <fcntl.h>
+#include <ftw.h>
+#include <sys/stat.h>
 #include <unistd.h>
+
+#include <algorithm>
 
 #include <chrono>
 #include <cstring>
@@ -412,6 +417,34 @@ void AtomicFile::write(const void* data, size_t len) {
     tmp.commit();
 }
 
+void AtomicFile::stream_from_paths(const std::vector<std::string>& paths) {
+    TempFile tmp(target_);
+    std::optional<hasher::Xxh3> h;
+    if (verify_) h.emplace(ctx_);
+    std::vector<uint8_t> buf(kStreamingBufSize);
+    for (const std::string& path : paths) {
+        const int fd = open(path.c_str(), O_RDONLY | O_CLOEXEC);
+        if (fd < 0) throw OxenError::basic_str("Could not open " + path + ": " + strerror(errno), OXH_ERR_IO);
+        for (;;) {
+            const ssize_t k = read(fd, buf.data(), buf.size());
+            if (k < 0) {
+                const int e = errno;
+                close(fd);
+                throw OxenError::basic_str("Could not read " + path + ": " + strerror(e), OXH_ERR_IO);
+            }
+            if (k == 0) break;
+            if (h) h->update(buf.data(), (size_t)k);
+            tmp.write_all(buf.data(), (size_t)k);
+        }
+        close(fd);
+    }
+    if (h) {
+        const MerkleHash actual(h->digest128());
+        if (actual != expected_) throw hash_mismatch(target_, expected_, actual);
+    }
+    tmp.commit();
+}
+
 }  // namespace util::fs
 
 namespace storage {
@@ -457,6 +490,49 @@ std::vector<std::string> LocalVersionStore::store_versions(const std::vector<std
         }
     }
     return err;
+}
+
+std::string LocalVersionStore::version_chunks_dir(const std::string& hash) const { return version_dir(hash) + "/chunks"; }
+
+std::string LocalVersionStore::version_chunk_file(const std::string& hash, uint64_t offset) const {
+    return version_chunks_dir(hash) + "/" + std::to_string(offset) + "/chunk";
+}
+
+void LocalVersionStore::store_version_chunk(const std::string& hash, uint64_t offset, const void* data, size_t len) const {
+    const std::string path = version_chunk_file(hash, offset);
+    struct stat sb;
+    if (stat(path.c_str(), &sb) == 0) return;
+    util::fs::AtomicFile(path, ctx_).write(data, len);
+}
+
+std::vector<uint64_t> LocalVersionStore::list_version_chunks(const std::string& hash) const {
+    const std::string dir = version_chunks_dir(hash);
+    DIR* d = opendir(dir.c_str());
+    if (!d) throw OxenError::basic_str("Could not read " + dir + ": " + strerror(errno), OXH_ERR_IO);
+    std::vector<uint64_t> out;
+    while (struct dirent* e = readdir(d)) {
+        const std::string name = e->d_name;
+        if (name.empty() || name.find_first_not_of("0123456789") != std::string::npos) continue;  // u64 names only
+        struct stat sb;
+        if (stat((dir + "/" + name).c_str(), &sb) != 0 || !S_ISDIR(sb.st_mode)) continue;
+        errno = 0;
+        const unsigned long long v = strtoull(name.c_str(), nullptr, 10);
+        if (errno == 0) out.push_back(v);
+    }
+    closedir(d);
+    std::sort(out.begin(), out.end());
+    return out;
+}
+
+void LocalVersionStore::combine_version_chunks(const std::string& hash) const {
+    const MerkleHash expected = MerkleHash::from_str(hash);
+    std::vector<std::string> paths;
+    for (uint64_t off : list_version_chunks(hash)) paths.push_back(version_chunk_file(hash, off));
+    util::fs::AtomicFile(version_path(hash), ctx_).with_hash(expected).stream_from_paths(paths);
+    const std::string dir = version_chunks_dir(hash);
+    if (nftw(dir.c_str(), [](const char* p, const struct stat*, int, struct FTW*) { return remove(p); }, 16,
+             FTW_DEPTH | FTW_PHYS) != 0)
+        throw OxenError::basic_str("Could not remove " + dir + ": " + strerror(errno), OXH_ERR_IO);
 }
 
 }  // namespace storage

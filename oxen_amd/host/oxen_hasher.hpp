@@ -234,6 +234,9 @@ class AtomicFile {
     }
     void stream(const Reader& reader);          // AtomicFile::stream / stream_async (:271-318, :363-463)
     void write(const void* data, size_t len);   // AtomicFile::write (:161-...)
+    // AtomicFile::stream_from_paths (:320-351): the in-order concatenation of `paths`, one source
+    // open at a time, verified as it streams (chunked-upload reassembly)
+    void stream_from_paths(const std::vector<std::string>& paths);
 
    private:
     std::string target_;
@@ -263,6 +266,14 @@ class LocalVersionStore {
     // would; result i is empty on success, else the error store_version would have thrown.
     std::vector<std::string> store_versions(const std::vector<std::string>& hashes,
                                             const std::vector<std::string_view>& datas) const;
+    // Chunked uploads (:78-92, :315-330, :367-413): chunks under {version_dir}/chunks/{offset}/chunk,
+    // written unverified; combine_version_chunks reassembles them in offset order, verifies the
+    // whole blob on the GPU (HashMismatch: nothing published, chunks kept), then removes the chunks.
+    std::string version_chunks_dir(const std::string& hash) const;
+    std::string version_chunk_file(const std::string& hash, uint64_t offset) const;
+    void store_version_chunk(const std::string& hash, uint64_t offset, const void* data, size_t len) const;
+    std::vector<uint64_t> list_version_chunks(const std::string& hash) const;
+    void combine_version_chunks(const std::string& hash) const;
 
    private:
     std::string root_;

@@ -24,6 +24,8 @@ from ._capi import OxenError
 STREAMING_BUF_SIZE = 10 * 1024 * 1024  # constants.rs:196
 ATOMIC_TEMP_INFIX = ".oxentmp."        # atomic_file.rs:25
 VERSION_FILE_NAME = "data"
+VERSION_CHUNKS_DIR = "chunks"          # constants.rs:120
+VERSION_CHUNK_FILE_NAME = "chunk"      # constants.rs:118
 
 
 class HashMismatchError(OxenError):
@@ -125,6 +127,34 @@ class AtomicFile:
                 h.close()  # the device stream is released now, not at garbage collection
             tmp.discard()
 
+    def stream_from_paths(self, paths: Sequence) -> None:
+        """stream_from_paths (atomic_file.rs:320-351): the in-order concatenation of the files at
+        `paths`, one source open at a time, hashed on the GPU as it goes to the temp and published on
+        a match -- the reassembly of a chunked upload (LocalVersionStore.combine_version_chunks)."""
+        tmp = _TempFile(self.target)
+        h = hasher.Xxh3(self.ctx) if self.expected is not None else None
+        try:
+            for path in paths:
+                with open(path, "rb") as src:
+                    while True:
+                        chunk = src.read(STREAMING_BUF_SIZE)
+                        if not chunk:
+                            break
+                        if h is not None:
+                            h.update(chunk)
+                        tmp.write_all(chunk)
+            if h is not None:
+                actual = h.digest128()
+                if actual != self.expected:
+                    raise HashMismatchError(self.target, self.expected, actual)
+            tmp.commit()
+        except OSError as e:
+            raise OxenError(str(e), _capi.OXH_ERR_IO) from e
+        finally:
+            if h is not None:
+                h.close()
+            tmp.discard()
+
     def write(self, data: bytes) -> None:
         tmp = _TempFile(self.target)
         try:
@@ -175,6 +205,46 @@ class LocalVersionStore:
         if self.version_exists(hash):
             return
         AtomicFile(self.version_path(hash), self.ctx).with_hash(_parse_hash(hash)).stream(reader)
+
+    # chunked uploads (local.rs:78-92, 315-330, 367-413): chunks land under
+    # {version_dir}/chunks/{offset}/chunk, unverified; the reassembled blob is verified once
+    def version_chunks_dir(self, hash: str) -> str:
+        return os.path.join(self.version_dir(hash), VERSION_CHUNKS_DIR)
+
+    def version_chunk_file(self, hash: str, offset: int) -> str:
+        return os.path.join(self.version_chunks_dir(hash), str(int(offset)), VERSION_CHUNK_FILE_NAME)
+
+    def store_version_chunk(self, hash: str, offset: int, data: bytes) -> None:  # :315-330
+        path = self.version_chunk_file(hash, offset)
+        if os.path.exists(path):
+            return
+        AtomicFile(path, self.ctx).write(data)
+
+    def list_version_chunks(self, hash: str) -> list:  # :367-382
+        out = []
+        with os.scandir(self.version_chunks_dir(hash)) as it:
+            for e in it:
+                if e.is_dir():
+                    try:
+                        out.append(int(e.name))
+                    except ValueError:
+                        pass
+        return sorted(out)
+
+    def combine_version_chunks(self, hash: str) -> None:  # :384-413
+        """The chunks in offset order, concatenated, hashed on the GPU and published only if the
+        digest is `hash` (HashMismatchError otherwise, and the chunks stay); then the chunks
+        directory is removed."""
+        import shutil
+
+        expected = _parse_hash(hash)
+        paths = [self.version_chunk_file(hash, o) for o in self.list_version_chunks(hash)]
+        AtomicFile(self.version_path(hash), self.ctx).with_hash(expected).stream_from_paths(paths)
+        shutil.rmtree(self.version_chunks_dir(hash), ignore_errors=False)
+
+    def get_version(self, hash: str) -> bytes:
+        with open(self.version_path(hash), "rb") as f:
+            return f.read()
 
     def store_versions(self, hashes: Sequence[str], datas: Sequence[bytes]) -> list:
         """Many received blobs: one batched GPU hash of every buffer, then each verified blob is

@@ -397,6 +397,20 @@ static void verified_publish(const std::string& scratch) {
     CHECK(read_file(store.version_path(hs[0])) == payload && store.version_exists(hs[3]) &&
           read_file(store.version_path(hs[3])).empty() && !store.version_exists(wrong));
     CHECK(list_dir(store.version_dir(hs[0])).size() == 1);  // no .oxentmp. leftovers
+
+    // chunked upload (local.rs:862-891): chunks at their byte offsets, reassembled in numeric offset
+    // order, verified, the chunks directory removed; a wrong hash publishes nothing and keeps them
+    const std::string ph = hasher::hash_buffer(payload.data(), payload.size());
+    const std::vector<uint64_t> cuts = {0, 7, 100, 150000, payload.size()};  // "100" sorts after "7" only numerically
+    LocalVersionStore store2(scratch + "/versions2");
+    for (size_t k = 0; k + 1 < cuts.size(); ++k)
+        store2.store_version_chunk(ph, cuts[k], payload.data() + cuts[k], cuts[k + 1] - cuts[k]);
+    CHECK((store2.list_version_chunks(ph) == std::vector<uint64_t>{0, 7, 100, 150000}));
+    store2.combine_version_chunks(ph);
+    CHECK(read_file(store2.version_path(ph)) == payload && list_dir(store2.version_dir(ph)).size() == 1);
+    store2.store_version_chunk(wrong, 0, data.data(), data.size());
+    CHECK(throws_oxen([&] { store2.combine_version_chunks(wrong); }, "Hash mismatch"));
+    CHECK(!store2.version_exists(wrong) && store2.list_version_chunks(wrong) == std::vector<uint64_t>{0});
 }
 
 int main(int argc, char** argv) {

@@ -127,3 +127,64 @@ def test_version_store_rejects_mismatched_content(cuda, tmp_path):
     for h in hs[:6]:
         if store.version_exists(h):
             assert os.listdir(store.version_dir(h)) == ["data"]
+
+
+@pytest.mark.gpu
+def test_stream_from_paths_concatenates_and_verifies(cuda, oracle_lib, tmp_path):
+    """atomic_file.rs:598-632 / :634-650: the in-order concatenation of chunk files is published
+    under the expected digest (hashed on the GPU), nothing else is left beside the target; a wrong
+    digest publishes nothing."""
+    from oracle import oracle
+    from oxen_amd.version_store import AtomicFile, HashMismatchError
+
+    chunks = tmp_path / "chunks"
+    chunks.mkdir()
+    parts = [b"hello ", b"brave ", b"world"]
+    paths = []
+    for i, part in enumerate(parts):
+        (chunks / str(i)).write_bytes(part)
+        paths.append(str(chunks / str(i)))
+    full = b"".join(parts)
+    target = tmp_path / "blob.bin"
+    AtomicFile(target).with_hash(oracle.xxh3_128_int(full)).stream_from_paths(paths)
+    assert target.read_bytes() == full
+    assert sorted(os.listdir(tmp_path)) == ["blob.bin", "chunks"]
+
+    (tmp_path / "chunk0").write_bytes(b"payload")
+    target2 = tmp_path / "blob2.bin"
+    with pytest.raises(HashMismatchError):
+        AtomicFile(target2).with_hash(BOGUS).stream_from_paths([str(tmp_path / "chunk0")])
+    assert not target2.exists() and not any(".oxentmp." in n for n in os.listdir(tmp_path))
+
+
+@pytest.mark.gpu
+def test_combine_version_chunks(cuda, tmp_path):
+    """local.rs:862-891: chunks stored at their byte offsets are reassembled in offset order (the
+    offsets sort numerically, not as names), verified against the blob's hash and the chunks
+    directory removed; here also with chunks larger than one streaming piece, and a mismatch that
+    publishes nothing and keeps the chunks."""
+    from oxen_amd import hasher
+    from oxen_amd.version_store import HashMismatchError, LocalVersionStore, STREAMING_BUF_SIZE
+
+    store = LocalVersionStore(tmp_path / "versions")
+    data = b"chunk-zero-byteschunk-one-bytes"
+    h = hasher.hash_buffer(data)
+    store.store_version_chunk(h, 0, data[:16])
+    store.store_version_chunk(h, 16, data[16:])
+    assert os.path.isdir(store.version_chunks_dir(h))
+    store.combine_version_chunks(h)
+    assert store.get_version(h) == data and not os.path.exists(store.version_chunks_dir(h))
+
+    big = os.urandom(2 * STREAMING_BUF_SIZE + 12345)
+    hb = hasher.hash_buffer(big)
+    cuts = [0, 7, 100_000, STREAMING_BUF_SIZE + 3, len(big)]  # offsets 7 and 100000 sort after 0, before 10 MiB
+    for a, b in zip(cuts, cuts[1:]):
+        store.store_version_chunk(hb, a, big[a:b])
+    assert store.list_version_chunks(hb) == cuts[:-1]
+    store.combine_version_chunks(hb)
+    assert store.get_version(hb) == big
+
+    store.store_version_chunk(WRONG_HASH, 0, DATA)
+    with pytest.raises(HashMismatchError):
+        store.combine_version_chunks(WRONG_HASH)
+    assert not store.version_exists(WRONG_HASH) and store.list_version_chunks(WRONG_HASH) == [0]
