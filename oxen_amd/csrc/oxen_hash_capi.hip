@@ -1295,6 +1295,15 @@ int oxh_combined_hash_device(const uint64_t* d_content, const uint64_t* d_metada
 // Host-resident buffers (oxh_hash_buffers / oxh_hash_streams): item i (lens[i] bytes) is copied by
 // copy(i, dst) straight into a pinned slot; slots are packed greedily in order, hashed on the GPU
 // while the next one fills, and items larger than a slot go through the oversize path.
+// Items of the short XXH3 paths (<= 240 B: paths, metadata JSON, most parent-node streams) are packed
+// back to back: their kernels load unaligned bytes anyway, and 256-B slots would move ~8x their bytes
+// over PCIe (a commit's 200 000 bucket paths: 6.3 MB instead of 51 MB). Longer items start on 256 B.
+// OXH_HOST_ALIGN_ALL=1: every item on 256 B (the r02 packing, for A/B).
+static uint64_t place(uint64_t off, uint64_t len) {
+    static const bool all = getenv("OXH_HOST_ALIGN_ALL") && atoi(getenv("OXH_HOST_ALIGN_ALL")) != 0;
+    return (len > 240 || all) ? align_up(off) : off;
+}
+
 static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
                            const std::function<const uint8_t*(uint64_t)>& src, uint64_t* out, bool short_only_lane) {
     Trace tr;
@@ -1318,8 +1327,8 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
                 ++i;
                 continue;
             }
-            if (align_up(bytes) + L > c->stage_bytes) break;
-            bytes = align_up(bytes) + L;
+            if (place(bytes, L) + L > c->stage_bytes) break;
+            bytes = place(bytes, L) + L;
             batch.push_back(i);
             ++i;
         }
@@ -1336,7 +1345,7 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
         uint64_t off = 0;
         bool all_short = true;
         for (size_t j = 0; j < batch.size(); ++j) {
-            off = align_up(off);
+            off = place(off, lens[batch[j]]);
             hoff[j] = off;
             hlen[j] = lens[batch[j]];
             if (hlen[j] > 240) all_short = false;
