@@ -1385,6 +1385,83 @@ int oxh_hash_buffers(oxh_ctx* c, const uint8_t* const* bufs, const uint64_t* len
     return hash_host_items(c, n, lens, [&](uint64_t i) { return bufs[i]; }, out, false);
 }
 
+// oxh_hash_streams over an arena whose items run forward (offsets non-decreasing, gaps at most as
+// large as the items): each batch is ONE span of the arena, copied into the pinned slot in large
+// pieces by the pool, with the items' offsets rebased onto it -- no per-item copy. A commit's
+// 200 000 bucket paths are such an arena (the serialised streams of commit_writer); a per-item copy
+// of them costs ~12 ns an item on the host. Items larger than a slot go the oversize path as before.
+static int hash_stream_spans(oxh_ctx* c, const uint8_t* streams, const uint64_t* offsets, const uint64_t* lens, uint64_t n,
+                             uint64_t* out) {
+    Trace tr;
+    Pending pend[NSLOT];
+    int slot = 0;
+    uint64_t i = 0;
+    std::vector<uint64_t> batch;
+    while (i < n) {
+        if (lens[i] > c->stage_bytes) {  // straight from the caller's buffer, in pieces (large_item)
+            MemSource ms(streams + offsets[i]);
+            LargeResult res;
+            if (int rc = large_item(c, lens[i], ms, false, false, nullptr, i, res)) return rc;
+            if (res.status != OXH_OK) return fail(res.status, "large host buffer: device or pinned memory unavailable");
+            out[2 * i] = res.out[0];
+            out[2 * i + 1] = res.out[1];
+            ++i;
+            continue;
+        }
+        const uint64_t base = offsets[i];
+        uint64_t end = base, k = i;
+        bool all_short = true;
+        batch.clear();
+        while (k < n && batch.size() < c->max_items && lens[k] <= c->stage_bytes &&
+               std::max(end, offsets[k] + lens[k]) - base <= c->stage_bytes) {
+            end = std::max(end, offsets[k] + lens[k]);
+            if (lens[k] > 240) all_short = false;
+            batch.push_back(k++);
+        }
+        const int s = slot;
+        slot = (slot + 1) % NSLOT;
+        const double t0 = Trace::now();
+        if (int rc = drain_slot(c, s, pend[s], out)) return rc;  // the slot's previous batch
+        const double t1 = Trace::now();
+        tr.drain += t1 - t0;
+        const uint64_t M = c->max_items;
+        uint64_t* hoff = c->h_desc[s];
+        uint64_t* hlen = c->h_desc[s] + M;
+        for (size_t j = 0; j < batch.size(); ++j) {
+            hoff[j] = offsets[batch[j]] - base;
+            hlen[j] = lens[batch[j]];
+        }
+        const uint64_t span = end - base, piece = 1ull << 20;
+        const int ntasks = (int)std::min<uint64_t>((span + piece - 1) / piece, (uint64_t)c->pool->size() * 4);
+        if (ntasks > 1) {
+            c->pool->parallel_for(ntasks, [&](int t) {
+                const uint64_t lo = span * (uint64_t)t / (uint64_t)ntasks, hi = span * (uint64_t)(t + 1) / (uint64_t)ntasks;
+                memcpy(c->h_stage[s] + lo, streams + base + lo, hi - lo);
+            });
+        } else if (span) {
+            memcpy(c->h_stage[s], streams + base, span);
+        }
+        const double t2 = Trace::now();
+        tr.fill += t2 - t1;
+        if (int rc = submit_slot(c, s, span, batch.size(), all_short, span / std::max<uint64_t>(1, batch.size()) <= kShortItemBytes,
+                                 false))
+            return rc;
+        tr.submit += Trace::now() - t2;
+        tr.batches++;
+        pend[s].busy = true;
+        pend[s].ids = batch;
+        i = k;
+    }
+    const double t3 = Trace::now();
+    for (int s = 0; s < NSLOT; ++s)
+        if (int rc = drain_slot(c, s, pend[s], out)) return rc;
+    tr.drain += Trace::now() - t3;
+    if (tr.on)
+        fprintf(stderr, "[oxh] streams (spans)=%llu batches=%d fill=%.3fs drain-wait=%.3fs submit=%.3fs\n",
+                (unsigned long long)n, tr.batches, tr.fill, tr.drain, tr.submit);
+    return OXH_OK;
+}
+
 int oxh_hash_streams(oxh_ctx* c, const uint8_t* streams, const uint64_t* offsets, const uint64_t* lens, uint64_t n,
                      uint64_t* out) {
     if (!c || (n && (!streams || !offsets || !lens || !out))) return fail(OXH_ERR_INVALID, "bad arguments");
@@ -1392,6 +1469,17 @@ int oxh_hash_streams(oxh_ctx* c, const uint8_t* streams, const uint64_t* offsets
     std::lock_guard<std::mutex> g(c->mu);
     HIP_TRY(hipSetDevice(c->device));
     STEP("hash_streams locked");
+    // spans when the items run forward through the arena without large gaps (OXH_STREAM_SPANS=0: per item)
+    static const bool spans_on = !(getenv("OXH_STREAM_SPANS") && atoi(getenv("OXH_STREAM_SPANS")) == 0);
+    bool forward = spans_on && n > 0;
+    uint64_t total = 0, maxend = 0;
+    for (uint64_t i = 0; forward && i < n; ++i) {
+        total += lens[i];
+        maxend = std::max(maxend, offsets[i] + lens[i]);
+        if (i && offsets[i] < offsets[i - 1]) forward = false;
+    }
+    if (forward && maxend - offsets[0] > 2 * total + 4096) forward = false;  // a sparse arena: copy items
+    if (forward) return hash_stream_spans(c, streams, offsets, lens, n, out);
     return hash_host_items(c, n, lens, [&](uint64_t i) { return streams + offsets[i]; }, out, true);
 }
 

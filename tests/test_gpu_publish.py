@@ -192,3 +192,47 @@ def test_concurrent_adds_into_one_store(cuda, oracle_lib, tmp_path):
         with open(hasher.version_path(root, w), "rb") as f:
             assert f.read() == b
     assert not any(".oxentmp." in f for f in _tree(root)), _tree(root)
+
+
+@pytest.mark.parametrize("layout", ["forward", "gaps", "repeats", "backward", "sparse"])
+def test_hash_streams_arena_layouts(cuda, oracle_lib, layout):
+    """oxh_hash_streams over the arena layouts a caller can pass: items running forward (copied as
+    spans), with small gaps, the same stream referenced several times, offsets running backward and
+    a sparse arena (both copied item by item); empty items, items above the 1 MiB staging slot and
+    more items than one slot's descriptor table, against the oracle."""
+    import numpy as np
+
+    from oracle import oracle
+    from oxen_amd import _capi
+    from oxen_amd.workloads import splitmix_bytes
+
+    rng = np.random.default_rng(11)
+    sizes = [int(x) for x in rng.integers(0, 300, 3000)] + [0, (1 << 20) + 77, 5000, 241, 240, 0]
+    sizes += [int(x) for x in rng.integers(1, 64, 2000)]
+    blobs = [splitmix_bytes(1300 + k, 0, s).tobytes() for k, s in enumerate(sizes)]
+    if layout == "repeats":
+        blobs = [blobs[k // 3] for k in range(len(blobs))]
+    parts, offs, pos = [], [], 0
+    for k, b in enumerate(blobs):
+        gap = {"gaps": k % 5, "sparse": 20_000}.get(layout, 0)
+        if layout == "repeats" and k % 3:
+            offs.append(offs[-1])  # the same bytes again
+            continue
+        parts.append(b"\xee" * gap)
+        pos += gap
+        offs.append(pos)
+        parts.append(b)
+        pos += len(b)
+    arena = np.frombuffer(b"".join(parts) + b"\0", dtype=np.uint8)
+    order = list(range(len(blobs)))
+    if layout == "backward":
+        order = order[::-1]
+    lens = np.array([len(blobs[k]) for k in order], dtype=np.uint64)
+    o = np.array([offs[k] for k in order], dtype=np.uint64)
+    out = np.zeros((len(order), 2), dtype=np.uint64)
+    with _capi.Context(0, staging_bytes=1 << 20) as c:  # 1024 items per slot: several batches
+        _capi.check(_capi.lib().oxh_hash_streams(c.handle, arena.ctypes.data, o.ctypes.data_as(_capi._u64p),
+                                                 lens.ctypes.data_as(_capi._u64p), len(order),
+                                                 out.ctypes.data_as(_capi._u64p)), "oxh_hash_streams")
+    got = [(int(hi) << 64) | int(lo) for lo, hi in out]
+    assert got == [oracle.xxh3_128_int(blobs[k]) for k in order]
