@@ -386,6 +386,10 @@ def main() -> None:
             roofline["profile"] = {"avg_ms": prof["avg_ms"], "calls": prof["calls"], "command": prof["command"],
                                    "source": prof["source"],
                                    "frac": round(bytes_per_rank / (prof["avg_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+            if prof.get("timed_region"):  # the profiled launches of the timed steps alone
+                tr = prof["timed_region"]
+                roofline["profile"]["timed_region"] = {"avg_ms": tr["avg_ms"], "launches": tr["launches"],
+                                                       "frac": round(bytes_per_rank / (tr["avg_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
         cpu = None
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is a rank-0, N = 1 figure
             cpu = cpu_baseline(da, digests, seed, args.cpu_budget)

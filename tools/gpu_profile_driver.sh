@@ -17,4 +17,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} -o 
 STATS=$(find gpurun_out/prof_${TAG} -name '*kernel_stats.csv' | head -1)
 cp "$STATS" gpurun_out/${TAG}_c2_kernel_stats.csv
 python3 tools/prof_summary.py --stats gpurun_out/${TAG}_c2_kernel_stats.csv --bench gpurun_out/${TAG}_prof_bench_c2.json \
-  --command "python3 $CMD" --workload c2 --out gpurun_out/${TAG}_profile_c2.json
+  --command "python3 $CMD" --workload c2 --out gpurun_out/${TAG}_profile_c2.json \
+  --trace "$(find gpurun_out/prof_${TAG} -name '*kernel_trace.csv' | head -1)" --warmup 5 --steps 20
