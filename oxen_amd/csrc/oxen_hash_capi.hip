@@ -140,8 +140,12 @@ int pick_variant(bool short_items) { return pick_variant(short_items ? ItemShape
 int launch_wave(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens, uint64_t n, uint64_t* out,
                 hipStream_t st, ItemShape shape = ItemShape::Long) {
     if (n == 0) return OXH_OK;
-    const uint64_t blocks = (n + 3) / 4;
-    hipLaunchKernelGGL(wave_kernel_for<true>(pick_variant(shape)), dim3((unsigned)blocks), dim3(256), 0, st, arena, offs,
+    // waves (items) per workgroup: OXH_K1_WG_WAVES (1, 2 or 4) for A/B; a workgroup's slot is freed
+    // only when its longest item is done
+    const char* wg = getenv("OXH_K1_WG_WAVES");
+    const int w = wg && (atoi(wg) == 1 || atoi(wg) == 2) ? atoi(wg) : 4;
+    const uint64_t blocks = (n + w - 1) / w;
+    hipLaunchKernelGGL(wave_kernel_for<true>(pick_variant(shape)), dim3((unsigned)blocks), dim3(64 * w), 0, st, arena, offs,
                        lens, n, (uint64_t)0, (uint64_t)0, out);
     HIP_TRY(hipGetLastError());
     return OXH_OK;

@@ -432,7 +432,8 @@ __device__ __forceinline__ void wave_item(const uint8_t* __restrict__ arena, con
         __syncthreads();
     }
     const int lane = threadIdx.x & 63;
-    const uint64_t item = (uint64_t)blockIdx.x * 4 + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // one item per wave; launched with 1, 2 or 4 waves per workgroup (blockDim.x = 64 * waves)
+    const uint64_t item = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (item >= n) return;
     if constexpr (Cfg<VARIANT>::STAGGER) {
         if (blockIdx.x < 2048) {

@@ -10,7 +10,8 @@ Cases (~6.4 GB device-resident each, K1 = oxh_xxh3_128_batch_device, HIP events,
   cdc_packed      lengths uniform in [4 KiB, 16 KiB) packed back to back (FastCDC-like)
   cdc_256         the same lengths at 256-B alignment
   cdc64_packed / cdc64_256   lengths uniform in [4 KiB, 128 KiB) (FastCDC at 64 KiB), likewise
-PROBE_CASES=a,b limits the run to those cases.
+PROBE_CASES=a,b limits the run to those cases. PROBE_WG=1,4 repeats every case with that many waves per
+K1 workgroup (OXH_K1_WG_WAVES), alternating.
 for each K1 variant given (default: 72 8).
 """
 from __future__ import annotations
@@ -76,11 +77,19 @@ def main():
     if only:
         layouts = {k: v for k, v in layouts.items() if k in only.split(",")}
     res = {}
+    wgs = os.environ.get("PROBE_WG", "")
+    wgs = [int(x) for x in wgs.split(",")] if wgs else [None]
     for v in variants:
         _capi.lib().oxh_set_kernel_variant(v)
         for name, (o, ln) in layouts.items():
-            res[f"{name}_v{v}"] = case(o, ln)
-            print(f"{name}_v{v}", res[f"{name}_v{v}"], file=sys.stderr, flush=True)
+            for rep in range(2 if len(wgs) > 1 else 1):
+                for w in wgs:
+                    if w is not None:
+                        os.environ["OXH_K1_WG_WAVES"] = str(w)
+                    key = f"{name}_v{v}" + (f"_wg{w}_r{rep}" if w is not None else "")
+                    res[key] = case(o, ln)
+                    print(key, res[key], file=sys.stderr, flush=True)
+    os.environ.pop("OXH_K1_WG_WAVES", None)
     _capi.lib().oxh_set_kernel_variant(0)
     print(json.dumps(res), flush=True)
 
