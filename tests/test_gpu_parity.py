@@ -62,6 +62,28 @@ def test_every_length_unaligned(cuda, golden, mode, variant):
     assert not _mismatch(got, want, lens)
 
 
+@pytest.mark.parametrize("wg_waves", ["1", "2"])
+@pytest.mark.parametrize("variant", [0, 8, 72, 104])
+def test_every_length_workgroup_width(cuda, golden, variant, wg_waves, monkeypatch):
+    """K1 launched with 1 or 2 items (waves) per workgroup instead of 4 (OXH_K1_WG_WAVES): the item
+    index comes from blockDim, so every item is still hashed exactly once; the ragged golden batch."""
+    import torch
+
+    from oxen_amd import _capi
+    from oxen_amd.device import xxh3_128_batch_device
+
+    monkeypatch.setenv("OXH_K1_WG_WAVES", wg_waves)
+    arena, offs, lens, want, _ = _golden_arena(golden, cuda)
+    prev = _capi.lib().oxh_set_kernel_variant(variant)
+    try:
+        out = xxh3_128_batch_device(arena, torch.from_numpy(offs.view(np.int64)).to(cuda),
+                                    torch.from_numpy(lens.view(np.int64)).to(cuda), mode=1)
+        got = _u64(out)
+    finally:
+        _capi.lib().oxh_set_kernel_variant(prev)
+    assert not _mismatch(got, want, lens)
+
+
 @pytest.mark.parametrize("variant", VARIANTS)
 def test_every_length_aligned(cuda, golden, variant):
     """Same vectors re-packed at 256-B aligned offsets (the coalesced dwordx4 path)."""
