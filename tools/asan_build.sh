@@ -1,13 +1,13 @@
 #!/bin/bash
-# Host-side AddressSanitizer builds of the runtime (tools/asan_gpu.sh runs the GPU suite over them).
+# Host-side AddressSanitizer builds of the runtime (tools/asan_suite.sh runs the CPU suite over them).
 # Only HOST code is instrumented: every -fsanitize on a hipcc line sits right after -Xarch_host, and
 # the host-only clang++ line carries -fno-gpu-sanitize; the device code of the kernels is unchanged.
-# Outputs go to asan/ (git-ignored, travels to the GPU box with the snapshot):
+# Outputs go to asan/ (git-ignored; gpurun-ignored, no GPU run uses them):
 #   asan/liboxen_hash.so      the C ABI runtime + kernels, host part instrumented
 #   asan/liboxen_hasher.so    the C++ mirror (liboxen::util::hasher, commit writer), instrumented
 #   asan/oxh_hash_helper      the reader-pool helper (uninstrumented main; loads the library above)
 # The shared objects link clang's libclang_rt.asan-x86_64.so, which every process also preloads
-# (tools/asan_gpu.sh): the runtime must come first in the load order.
+# (tools/asan_suite.sh): the runtime must come first in the load order.
 set -euo pipefail
 cd "$(dirname "$0")/.."
 OUT=asan
