@@ -1,0 +1,188 @@
+"""Soak the streaming engine: several threads issue mixed requests against shared contexts for a fixed
+time, and every answer is checked against digests the C oracle computed up front. GPU box only.
+
+    python tools/engine_soak.py [--seconds 240] [--threads 8] [--files 3000]
+
+Corpus: files of 0 B .. 300 KB (binary and text), a few above a 1 MiB staging slot (large-file
+path), duplicates, a missing path. Contexts: one with 1 MiB staging slots (every call cycles slots,
+seals early and takes the large-file path), one default. Requests, picked at random per iteration:
+  files      oxh_hash_files over a random subset (random order, duplicates)
+  text       oxh_hash_files_text: digests + (num_lines, num_chars)
+  add        oxh_add_files into a per-thread version store; every reported blob re-read and hashed
+  buffers    oxh_hash_buffers over random host slices
+  stream     the streaming Xxh3 over a file in random-sized updates
+  meta       oxh_hash_files_meta with the true sizes
+Prints one JSON line: per-kind counts, items checked, failures (the first few described). Exit 1 on any
+mismatch.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import random
+import shutil
+import sys
+import tempfile
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=240)
+    ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--files", type=int, default=3000)
+    ap.add_argument("--seed", type=int, default=7)
+    a = ap.parse_args()
+
+    import numpy as np
+
+    from oracle import oracle
+    from oxen_amd import _capi, hasher
+
+    rng = random.Random(a.seed)
+    base = tempfile.mkdtemp(prefix="oxh_soak_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        corpus = os.path.join(base, "corpus")
+        os.makedirs(corpus)
+        paths, want, text = [], {}, {}
+        words = [b"alpha", b"beta", b"\xc3\xa9t\xc3\xa9", b"\n", b"line\n", b"\xe2\x9c\x93", b" "]
+        for i in range(a.files):
+            p = os.path.join(corpus, f"d{i % 37}", f"f{i}.{'txt' if i % 3 == 0 else 'bin'}")
+            os.makedirs(os.path.dirname(p), exist_ok=True)
+            r = rng.random()
+            n = 0 if r < 0.02 else rng.randint(1, 240) if r < 0.2 else rng.randint(241, 300_000) if r < 0.99 \
+                else rng.randint(1_200_000, 3_000_000)
+            if i % 3 == 0:
+                data = b"".join(rng.choice(words) for _ in range(n // 4 + 1))[:n]
+            else:
+                data = rng.randbytes(n)
+            with open(p, "wb") as f:
+                f.write(data)
+            paths.append(p)
+            want[p] = oracle.xxh3_128_int(data)
+            arr = np.frombuffer(data, dtype=np.uint8)
+            text[p] = (1 + data.count(b"\n"), len(data) - int(((arr & 0xC0) == 0x80).sum()))
+        missing = os.path.join(corpus, "does-not-exist")
+
+        ctxs = [_capi.Context(0, staging_bytes=1 << 20), _capi.Context(0)]
+        lock = threading.Lock()
+        counts = {k: 0 for k in ("files", "text", "add", "buffers", "stream", "meta")}
+        checked = [0]
+        fails = []
+        deadline = time.time() + a.seconds
+
+        def fail(msg):
+            with lock:
+                if len(fails) < 20:
+                    fails.append(msg)
+
+        def worker(t):
+            try:
+                work(t)
+            except Exception as e:  # a raised OxenError is a failure too
+                fail(f"thread {t}: {e!r}")
+
+        def work(t):
+            r = random.Random(a.seed * 1000 + t)
+            store = os.path.join(base, f"store{t}")
+            while time.time() < deadline and not fails:
+                kind = r.choice(list(counts))
+                ctx = r.choice(ctxs)
+                sub = [r.choice(paths) for _ in range(r.choice((1, 7, 64, 64, 400)))]
+                n_ok = 0
+                if kind in ("files", "meta"):
+                    with_missing = r.random() < 0.2
+                    q = sub + ([missing] if with_missing else [])
+                    if kind == "files":
+                        dg, _, st = hasher.hash_files_128bit(q, ctx)
+                    else:
+                        sizes = [os.path.getsize(p) for p in sub] + ([0] if with_missing else [])
+                        dg, _, st = hasher.hash_files_given_metadata_128bit(q, sizes, ctx)
+                    for p, d, s in zip(q, dg, st):
+                        if p == missing:
+                            if s == 0:
+                                fail(f"{kind}: missing path reported OK")
+                        elif s != 0 or d != want[p]:
+                            fail(f"{kind}: {p} status {s} digest {d} want {want[p]}")
+                        else:
+                            n_ok += 1
+                elif kind == "text":
+                    dg, _, st, meta = hasher.hash_files_text_128bit(sub, ctx)
+                    for p, d, s, m in zip(sub, dg, st, meta):
+                        if s != 0 or d != want[p] or (m["text"]["num_lines"], m["text"]["num_chars"]) != text[p]:
+                            fail(f"text: {p} status {s} digest {d} meta {m} want {want[p]} {text[p]}")
+                        else:
+                            n_ok += 1
+                elif kind == "add":
+                    dg, _, st, stored = hasher.add_files(sub, store, ctx)
+                    for p, d, s in zip(sub, dg, st):
+                        if s != 0 or d != want[p]:
+                            fail(f"add: {p} status {s} digest {d} want {want[p]}")
+                            continue
+                        with open(hasher.version_path(store, d), "rb") as f:
+                            blob = f.read()
+                        if oracle.xxh3_128_int(blob) != d:
+                            fail(f"add: blob of {p} does not hash to its name")
+                        else:
+                            n_ok += 1
+                elif kind == "buffers":
+                    bufs = []
+                    for p in sub[:64]:
+                        with open(p, "rb") as f:
+                            data = f.read()
+                        lo = r.randint(0, len(data))
+                        bufs.append(data[lo:])
+                    got = hasher.hash_buffers_128bit(bufs, ctx)
+                    for b, d in zip(bufs, got):
+                        if d != oracle.xxh3_128_int(b):
+                            fail(f"buffers: slice of {len(b)} B")
+                        else:
+                            n_ok += 1
+                else:  # stream
+                    p = r.choice(paths)
+                    with open(p, "rb") as f:
+                        data = f.read()
+                    x = hasher.Xxh3(ctx)
+                    try:
+                        i = 0
+                        while i < len(data):
+                            k = r.choice((1, 63, 1000, 70_000, 1 << 20))
+                            x.update(data[i:i + k])
+                            i += k
+                        if x.digest128() != want[p]:
+                            fail(f"stream: {p}")
+                        else:
+                            n_ok += 1
+                    finally:
+                        x.close()
+                with lock:
+                    counts[kind] += 1
+                    checked[0] += n_ok
+
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(a.threads)]
+        t0 = time.time()
+        for th in ths:
+            th.start()
+        while any(th.is_alive() for th in ths):  # a progress line every 20 s (long runs must not look hung)
+            for th in ths:
+                th.join(timeout=20.0 / len(ths))
+            with lock:
+                print(json.dumps({"t": round(time.time() - t0), "requests": dict(counts), "items_checked": checked[0],
+                                  "failures": len(fails)}), file=sys.stderr, flush=True)
+        for c in ctxs:
+            c.close()
+        res = {"seconds": round(time.time() - t0, 1), "threads": a.threads, "files": a.files,
+               "requests": counts, "items_checked": checked[0], "failures": len(fails), "first_failures": fails[:5]}
+        print(json.dumps(res), flush=True)
+        sys.exit(1 if fails else 0)
+    finally:
+        shutil.rmtree(base, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()
