@@ -138,12 +138,13 @@ int pick_variant(bool short_items) { return pick_variant(short_items ? ItemShape
 
 // K1 over a descriptor table: one 64-lane wave per item, 4 waves per 256-thread workgroup.
 int launch_wave(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens, uint64_t n, uint64_t* out,
-                hipStream_t st, ItemShape shape = ItemShape::Long) {
+                hipStream_t st, ItemShape shape = ItemShape::Long, int waves = 4) {
     if (n == 0) return OXH_OK;
-    // waves (items) per workgroup: OXH_K1_WG_WAVES (1, 2 or 4) for A/B; a workgroup's slot is freed
-    // only when its longest item is done
+    // waves (items) per workgroup: 4, or the caller's choice; OXH_K1_WG_WAVES (1, 2 or 4) overrides
+    // both for A/B. A workgroup's slot is freed only when its longest item is done.
     const char* wg = getenv("OXH_K1_WG_WAVES");
-    const int w = wg && (atoi(wg) == 1 || atoi(wg) == 2) ? atoi(wg) : 4;
+    const int e = wg ? atoi(wg) : 0;
+    const int w = (e == 1 || e == 2 || e == 4) ? e : (waves == 1 || waves == 2) ? waves : 4;
     const uint64_t blocks = (n + w - 1) / w;
     hipLaunchKernelGGL(wave_kernel_for<true>(pick_variant(shape)), dim3((unsigned)blocks), dim3(64 * w), 0, st, arena, offs,
                        lens, n, (uint64_t)0, (uint64_t)0, out);
@@ -930,6 +931,15 @@ int large_item(oxh_ctx* c, uint64_t L, LargeSource& src, bool want_counts, bool 
 }
 
 }  // namespace
+
+namespace oxh {
+// FastCDC's K1 pass (fastcdc.hip): the block-wise K1 over the packed chunk table, `waves` chunks per
+// workgroup (2 when the mean chunk is small: tools/k1_small_probe.py)
+int k1_packed(const void* d_arena, const uint64_t* d_offsets, const uint64_t* d_lens, uint64_t n, uint64_t* d_out,
+              int waves, hipStream_t st) {
+    return launch_wave((const uint8_t*)d_arena, d_offsets, d_lens, n, d_out, st, ItemShape::Packed, waves);
+}
+}  // namespace oxh
 
 extern "C" {
 
