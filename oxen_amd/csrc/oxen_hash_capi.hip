@@ -2032,10 +2032,15 @@ void run_stream(oxh_ctx* c) {
         // 3. the slot being filled: seal it early (flush) when it holds enough bytes or every reader
         //    is idle and the next slot is free; submit it once sealed and its writers are done
         SlotFill& sl = fs.slot[s];
+        // Idle count FIRST, then the slot: a reader counts itself idle (in claim(), under qmu) only
+        // after its reservations in the slot word, so a word read after seeing every reader idle holds
+        // all of them. Read the other way round, a reader could reserve an item between the word load
+        // and the idle load, and step 4 closed the run over a slot it still saw empty: that item's
+        // request never completed (found by tools/engine_soak.py, once in ~157 000 requests).
+        const bool all_idle = fs.idle.load(std::memory_order_acquire) == fs.nreaders;
         // state before word: a slot seen open (state 1) shows its current generation's word
         const int sst = sl.state.load(std::memory_order_acquire);
         uint64_t w = sl.word.load(std::memory_order_acquire);
-        const bool all_idle = fs.idle.load(std::memory_order_acquire) == fs.nreaders;
         // (early flushes only help while some caller is waiting on a partial slot: a request whose
         // files are all claimed; a lone whole-list call keeps full slots until its last files)
         if (sst == 1 && !(w & kSealedBit) && w_items(w) > 0 &&
@@ -2067,7 +2072,10 @@ void run_stream(oxh_ctx* c) {
         if (all_idle && sst == 1 && !(w & kSealedBit) && w_items(w) == 0 && nbusy == 0 && fs.n_oversize.load() == 0 &&
             fs.n_changed.load() == 0) {
             std::lock_guard<std::mutex> g(c->qmu);
-            if (c->queue.empty() && fs.idle.load() == fs.nreaders) {
+            // still nothing: no request queued, every reader idle, the slot still empty (re-read
+            // under the lock the readers take to go idle)
+            if (c->queue.empty() && fs.idle.load() == fs.nreaders && w_items(sl.word.load(std::memory_order_acquire)) == 0 &&
+                fs.n_oversize.load() == 0 && fs.n_changed.load() == 0) {
                 fs.closing = true;
                 c->qcv.notify_all();
                 break;
@@ -2185,7 +2193,16 @@ static int hash_files_impl(oxh_ctx* c, const char* const* paths, uint64_t n, uin
     while (!r.cv.wait_for(lk, std::chrono::duration<double>(limit), [&] { return r.done; })) {
         lk.unlock();
         dump_engine(c, r);
+        // No engine run and the request not queued: no thread will ever complete it (the run that held
+        // it has ended and its readers are gone). An internal error, reported instead of a hang.
+        bool orphaned;
+        {
+            std::lock_guard<std::mutex> g(c->qmu);
+            orphaned = c->live == nullptr && std::find(c->queue.begin(), c->queue.end(), &r) == c->queue.end();
+        }
         lk.lock();
+        if (orphaned && !r.done)
+            return fail(OXH_ERR_HIP, "internal error: the file engine ended its run with items of this request unfinished");
     }
     return r.rc ? fail(r.rc, r.msg) : OXH_OK;
 }
