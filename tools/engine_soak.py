@@ -12,6 +12,10 @@ seals early and takes the large-file path), one default. Requests, picked at ran
   buffers    oxh_hash_buffers over random host slices
   stream     the streaming Xxh3 over a file in random-sized updates
   meta       oxh_hash_files_meta with the true sizes
+  streams    oxh_hash_streams over random byte strings (K2's path: arena spans and per-item copies)
+  modified   oxh_files_modified: equal sizes, drifted mtimes, node hashes right or off by one
+  utf8       oxh_hash_files_text_utf8 (digests, counts and the is_utf8 sniff)
+  pool       the reader-process pool (oxh_pool, 2 helpers) over a random subset
 Prints one JSON line: per-kind counts, items checked, failures (the first few described). Exit 1 on any
 mismatch.
 """
@@ -71,7 +75,15 @@ def main():
 
         ctxs = [_capi.Context(0, staging_bytes=1 << 20), _capi.Context(0)]
         lock = threading.Lock()
-        counts = {k: 0 for k in ("files", "text", "add", "buffers", "stream", "meta")}
+        counts = {k: 0 for k in ("files", "text", "add", "buffers", "stream", "meta", "streams", "modified", "utf8", "pool")}
+        from oxen_amd.procpool import ShardedFileHasher
+
+        pool = ShardedFileHasher(procs=2, devices=(0,), threads=4)
+        pool_lock = threading.Lock()  # oxh_pool serves one call at a time anyway
+
+        def utf8_ok(p):
+            with open(p, "rb") as f:
+                return oracle.is_utf8_prefix(f.read(4096))
         checked = [0]
         fails = []
         deadline = time.time() + a.seconds
@@ -143,6 +155,40 @@ def main():
                             fail(f"buffers: slice of {len(b)} B")
                         else:
                             n_ok += 1
+                elif kind == "streams":
+                    ss = [r.randbytes(r.choice((0, 5, 32, 200, 3210, 70_000))) for _ in range(r.choice((1, 50, 500)))]
+                    got = hasher.hash_streams_128bit(ss, ctx)
+                    for b, d in zip(ss, got):
+                        if d != oracle.xxh3_128_int(b):
+                            fail(f"streams: {len(b)} B")
+                        else:
+                            n_ok += 1
+                elif kind == "modified":
+                    flip = [r.random() < 0.3 for _ in sub]
+                    sizes = [os.path.getsize(p) for p in sub]
+                    nodes = [(want[p] ^ 1) if f else want[p] for p, f in zip(sub, flip)]
+                    mod, st, _ = hasher.files_modified(sub, sizes, sizes, [False] * len(sub), nodes, ctx)
+                    for p, f, m, s_ in zip(sub, flip, mod, st):
+                        if s_ != 0 or m != f:
+                            fail(f"modified: {p} status {s_} modified {m} want {f}")
+                        else:
+                            n_ok += 1
+                elif kind == "utf8":
+                    dg, _, st, meta, u8 = hasher.hash_files_text_utf8_128bit(sub, ctx)
+                    for p, d, s_, m, u in zip(sub, dg, st, meta, u8):
+                        if s_ != 0 or d != want[p] or (m["text"]["num_lines"], m["text"]["num_chars"]) != text[p] \
+                                or bool(u) != utf8_ok(p):
+                            fail(f"utf8: {p} status {s_} digest {d} meta {m} utf8 {u}")
+                        else:
+                            n_ok += 1
+                elif kind == "pool":
+                    with pool_lock:
+                        out, _, st = pool.hash_files(sub)
+                    for p, o, s_ in zip(sub, out, st):
+                        if s_ != 0 or (int(o[1]) << 64 | int(o[0])) != want[p]:
+                            fail(f"pool: {p} status {s_}")
+                        else:
+                            n_ok += 1
                 else:  # stream
                     p = r.choice(paths)
                     with open(p, "rb") as f:
@@ -176,6 +222,7 @@ def main():
                                   "failures": len(fails)}), file=sys.stderr, flush=True)
         for c in ctxs:
             c.close()
+        pool.close()
         res = {"seconds": round(time.time() - t0, 1), "threads": a.threads, "files": a.files,
                "requests": counts, "items_checked": checked[0], "failures": len(fails), "first_failures": fails[:5]}
         print(json.dumps(res), flush=True)
