@@ -570,8 +570,10 @@ struct FileSource final : LargeSource {
     uint8_t* map = nullptr;
     uint64_t len = 0;
     std::vector<unsigned char> resident;
-    FileSource(const char* path, uint64_t L, bool allow_direct) : len(L) {
-        fd = path ? open(path, O_RDONLY | O_CLOEXEC | O_NONBLOCK) : -1;
+    FileSource(const char* path, uint64_t L, bool allow_direct)
+        : FileSource(path ? open(path, O_RDONLY | O_CLOEXEC | O_NONBLOCK) : -1, L, allow_direct) {}
+    // an open descriptor (owned from here on) whose file holds L bytes
+    FileSource(int fd_, uint64_t L, bool allow_direct) : fd(fd_), len(L) {
         if (fd >= 0 && allow_direct) {
             void* m = mmap(nullptr, L, PROT_READ, MAP_SHARED, fd, 0);
             if (m != MAP_FAILED) {
@@ -1837,19 +1839,34 @@ void drain_files(FileStream& fs, int s, const SlotRun& p) {
 }
 
 // Files of the engine larger than a staging slot, up to big_files_at_once() side by side.
+int refresh_file(FileStream& fs, FileRequest* r, uint64_t i);
+
 int big_files(FileStream& fs, const std::vector<std::pair<FileRequest*, uint64_t>>& items) {
     const int n = (int)items.size();
     std::vector<std::unique_ptr<FileSource>> srcs(n);
     std::vector<LargeJob> jobs;
-    std::vector<int> who;  // jobs[k] is items[who[k]]
+    std::vector<int> who;              // jobs[k] is items[who[k]]
+    std::vector<bool> shrunk(n, false);  // now below a staging slot: read whole by refresh_file
     for (int q = 0; q < n; ++q) {
         FileRequest* r = items[q].first;
         const uint64_t i = items[q].second;
-        srcs[q].reset(new FileSource(r->paths[i], r->lens[i], r->sink == nullptr));
-        if (srcs[q]->fd < 0) {
+        // The pieces are planned from the size of the file THIS descriptor reads: the path may name a
+        // different file than the reader's stat saw (replaced since, e.g. by an editor's rename), and the
+        // reference reads whatever the file holds when it opens it (hasher.rs:150-174).
+        const int fd = open(r->paths[i], O_RDONLY | O_CLOEXEC | O_NONBLOCK);
+        struct stat sb;
+        if (fd < 0 || fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode)) {
+            if (fd >= 0) close(fd);
             r->st[i] = OXH_ERR_IO;
             continue;
         }
+        r->lens[i] = (uint64_t)sb.st_size;
+        if (r->lens[i] < fs.c->stage_bytes) {
+            close(fd);
+            shrunk[q] = true;
+            continue;
+        }
+        srcs[q].reset(new FileSource(fd, r->lens[i], r->sink == nullptr));
         LargeJob j;
         j.L = r->lens[i], j.src = srcs[q].get(), j.want_counts = r->counts != nullptr, j.want_utf8 = r->utf8 != nullptr;
         j.sink = r->sink, j.id = i;
@@ -1873,7 +1890,13 @@ int big_files(FileStream& fs, const std::vector<std::pair<FileRequest*, uint64_t
         }
         if (r->utf8) r->utf8[i] = res.utf8;
     }
-    for (int q = 0; q < n; ++q) account(fs, items[q].first, 1);
+    for (int q = 0; q < n; ++q) {
+        if (!shrunk[q]) {
+            account(fs, items[q].first, 1);
+        } else if (int rc = refresh_file(fs, items[q].first, items[q].second)) {  // accounts the item itself
+            return rc;  // a HIP error: the run fails every open request
+        }
+    }
     return OXH_OK;
 }
 

@@ -789,13 +789,16 @@ def test_big_files_side_by_side(oracle_lib, tmp_path, cuda, monkeypatch, at_once
 
 def test_hash_files_given_metadata(oracle_lib, tmp_path, cuda):
     """oxh_hash_files_meta (get_hash_given_metadata with the walk's sizes, hasher.rs:56-65): no
-    fstat per file; sizes that are stale (file grew, shrank, emptied), a directory, a missing path and
-    an oversize file are all handled so that every digest covers the file's current content."""
+    fstat per file; sizes that are stale (file grew, shrank, emptied; a walk size above a staging
+    slot for a file now below one, and a wrong size above a slot for a file still above one), a
+    directory, a missing path and an oversize file are all handled so that every digest covers the
+    file's current content."""
     from oxen_amd import _capi, hasher
     from oxen_amd.workloads import splitmix_bytes
 
     rng = np.random.default_rng(41)
     blobs = [splitmix_bytes(900 + k, 0, int(s)).tobytes() for k, s in enumerate(rng.integers(0, 300_000, 400))]
+    blobs += [splitmix_bytes(6, 0, 1000).tobytes(), splitmix_bytes(7, 0, (3 << 19) + 3).tobytes()]
     blobs += [b"", b"x", splitmix_bytes(5, 0, (3 << 20) + 9).tobytes()]  # the last one is oversize
     paths = []
     for k, b in enumerate(blobs):
@@ -807,6 +810,8 @@ def test_hash_files_given_metadata(oracle_lib, tmp_path, cuda):
     meta[4] = max(0, meta[4] - 7)  # file grew
     meta[5] = 0           # grew from empty
     meta[-3] = 10         # now empty
+    meta[-5] = 2 << 20    # the walk saw a file larger than a staging slot; it is 1000 B now
+    meta[-4] = 3 << 20    # larger than a slot either way, but not the size the walk saw
     os.mkdir(tmp_path / "adir")
     paths += [str(tmp_path / "adir"), str(tmp_path / "missing")]
     meta += [4096, 5]

@@ -16,6 +16,9 @@ seals early and takes the large-file path), one default. Requests, picked at ran
   modified   oxh_files_modified: equal sizes, drifted mtimes, node hashes right or off by one
   utf8       oxh_hash_files_text_utf8 (digests, counts and the is_utf8 sniff)
   pool       the reader-process pool (oxh_pool, 2 helpers) over a random subset
+--mutate: a mutator thread atomically replaces files of a hot tenth of the corpus (sizes across the
+1 MiB slot too) while the requests run; a digest must then be one of the file's versions (no torn
+read: the engine's re-read on a size change, read to EOF) with that version's counts and is_utf8.
 Prints one JSON line: per-kind counts, items checked, failures (the first few described). Exit 1 on any
 mismatch.
 """
@@ -41,6 +44,9 @@ def main():
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--files", type=int, default=3000)
     ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--mutate", action="store_true",
+                    help="a thread keeps replacing 10 %% of the files (new content, temp + rename): every digest must be "
+                         "one of that file's versions, with that version's text counts and is_utf8")
     a = ap.parse_args()
 
     import numpy as np
@@ -53,7 +59,11 @@ def main():
     try:
         corpus = os.path.join(base, "corpus")
         os.makedirs(corpus)
-        paths, want, text = [], {}, {}
+        paths, want, text, hist = [], {}, {}, {}
+
+        def counts_of(data):
+            arr = np.frombuffer(data, dtype=np.uint8)
+            return 1 + data.count(b"\n"), len(data) - int(((arr & 0xC0) == 0x80).sum())
         words = [b"alpha", b"beta", b"\xc3\xa9t\xc3\xa9", b"\n", b"line\n", b"\xe2\x9c\x93", b" "]
         for i in range(a.files):
             p = os.path.join(corpus, f"d{i % 37}", f"f{i}.{'txt' if i % 3 == 0 else 'bin'}")
@@ -69,9 +79,15 @@ def main():
                 f.write(data)
             paths.append(p)
             want[p] = oracle.xxh3_128_int(data)
-            arr = np.frombuffer(data, dtype=np.uint8)
-            text[p] = (1 + data.count(b"\n"), len(data) - int(((arr & 0xC0) == 0x80).sum()))
+            text[p] = counts_of(data)
+            hist[p] = {want[p]: (text[p], oracle.is_utf8_prefix(data[:4096]))}
         missing = os.path.join(corpus, "does-not-exist")
+        hot = set(paths[::10]) if a.mutate else set()
+        stable = [p for p in paths if p not in hot]
+
+        def version(p, d):  # (counts, is_utf8) of the version of p with digest d, or None
+            with lock:
+                return hist[p].get(d)
 
         ctxs = [_capi.Context(0, staging_bytes=1 << 20), _capi.Context(0)]
         lock = threading.Lock()
@@ -119,22 +135,23 @@ def main():
                         if p == missing:
                             if s == 0:
                                 fail(f"{kind}: missing path reported OK")
-                        elif s != 0 or d != want[p]:
-                            fail(f"{kind}: {p} status {s} digest {d} want {want[p]}")
+                        elif s != 0 or version(p, d) is None:
+                            fail(f"{kind}: {p} status {s} digest {d} is no version of the file")
                         else:
                             n_ok += 1
                 elif kind == "text":
                     dg, _, st, meta = hasher.hash_files_text_128bit(sub, ctx)
                     for p, d, s, m in zip(sub, dg, st, meta):
-                        if s != 0 or d != want[p] or (m["text"]["num_lines"], m["text"]["num_chars"]) != text[p]:
-                            fail(f"text: {p} status {s} digest {d} meta {m} want {want[p]} {text[p]}")
+                        v = version(p, d) if s == 0 else None
+                        if v is None or (m["text"]["num_lines"], m["text"]["num_chars"]) != v[0]:
+                            fail(f"text: {p} status {s} digest {d} meta {m} version {v}")
                         else:
                             n_ok += 1
                 elif kind == "add":
                     dg, _, st, stored = hasher.add_files(sub, store, ctx)
                     for p, d, s in zip(sub, dg, st):
-                        if s != 0 or d != want[p]:
-                            fail(f"add: {p} status {s} digest {d} want {want[p]}")
+                        if s != 0 or version(p, d) is None:
+                            fail(f"add: {p} status {s} digest {d} is no version of the file")
                             continue
                         with open(hasher.version_path(store, d), "rb") as f:
                             blob = f.read()
@@ -164,6 +181,7 @@ def main():
                         else:
                             n_ok += 1
                 elif kind == "modified":
+                    sub = [r.choice(stable) for _ in sub]
                     flip = [r.random() < 0.3 for _ in sub]
                     sizes = [os.path.getsize(p) for p in sub]
                     nodes = [(want[p] ^ 1) if f else want[p] for p, f in zip(sub, flip)]
@@ -176,8 +194,8 @@ def main():
                 elif kind == "utf8":
                     dg, _, st, meta, u8 = hasher.hash_files_text_utf8_128bit(sub, ctx)
                     for p, d, s_, m, u in zip(sub, dg, st, meta, u8):
-                        if s_ != 0 or d != want[p] or (m["text"]["num_lines"], m["text"]["num_chars"]) != text[p] \
-                                or bool(u) != utf8_ok(p):
+                        v = version(p, d) if s_ == 0 else None
+                        if v is None or (m["text"]["num_lines"], m["text"]["num_chars"]) != v[0] or bool(u) != v[1]:
                             fail(f"utf8: {p} status {s_} digest {d} meta {m} utf8 {u}")
                         else:
                             n_ok += 1
@@ -185,7 +203,7 @@ def main():
                     with pool_lock:
                         out, _, st = pool.hash_files(sub)
                     for p, o, s_ in zip(sub, out, st):
-                        if s_ != 0 or (int(o[1]) << 64 | int(o[0])) != want[p]:
+                        if s_ != 0 or version(p, int(o[1]) << 64 | int(o[0])) is None:
                             fail(f"pool: {p} status {s_}")
                         else:
                             n_ok += 1
@@ -200,7 +218,7 @@ def main():
                             k = r.choice((1, 63, 1000, 70_000, 1 << 20))
                             x.update(data[i:i + k])
                             i += k
-                        if x.digest128() != want[p]:
+                        if x.digest128() != oracle.xxh3_128_int(data):
                             fail(f"stream: {p}")
                         else:
                             n_ok += 1
@@ -210,7 +228,27 @@ def main():
                     counts[kind] += 1
                     checked[0] += n_ok
 
+        mutations = [0]
+
+        def mutator():
+            r = random.Random(a.seed + 99)
+            hot_list = sorted(hot)
+            while time.time() < deadline and not fails:
+                p = r.choice(hot_list)
+                n = r.choice((0, 100, 5000, 60_000, 300_000, 1_500_000))
+                data = r.randbytes(n) if r.random() < 0.5 else b"".join(r.choice(words) for _ in range(n // 4 + 1))[:n]
+                d = oracle.xxh3_128_int(data)
+                with lock:
+                    hist[p][d] = (counts_of(data), oracle.is_utf8_prefix(data[:4096]))
+                tmp = p + ".mut"
+                with open(tmp, "wb") as f:
+                    f.write(data)
+                os.replace(tmp, p)
+                mutations[0] += 1
+
         ths = [threading.Thread(target=worker, args=(t,)) for t in range(a.threads)]
+        if a.mutate:
+            ths.append(threading.Thread(target=mutator))
         t0 = time.time()
         for th in ths:
             th.start()
@@ -223,7 +261,7 @@ def main():
         for c in ctxs:
             c.close()
         pool.close()
-        res = {"seconds": round(time.time() - t0, 1), "threads": a.threads, "files": a.files,
+        res = {"seconds": round(time.time() - t0, 1), "threads": a.threads, "files": a.files, "mutations": mutations[0],
                "requests": counts, "items_checked": checked[0], "failures": len(fails), "first_failures": fails[:5]}
         print(json.dumps(res), flush=True)
         sys.exit(1 if fails else 0)
