@@ -4,7 +4,7 @@ every answer is checked against the C oracle over the same bytes copied to the h
     python tools/device_soak.py [--seconds 240] [--threads 6]
 
 Per iteration a thread picks one of:
-  batch      oxh_xxh3_128_batch_device over ragged items at random offsets (auto / wave / packed modes)
+  batch      oxh_xxh3_128_batch_device over ragged items at random offsets (every OXH_MODE_*)
   text       oxh_xxh3_128_text_batch_device: digests + (num_lines, num_chars)
   chunks     oxh_chunk_digests_device, fixed-size chunks of a random size
   large      oxh_xxh3_128_large_batch_device over 1-3 buffers of 2-40 MiB (block sums + chains, the
@@ -90,7 +90,7 @@ def main():
                     o = torch.tensor(offs, dtype=torch.int64, device=dev)
                     ln = torch.tensor(lens, dtype=torch.int64, device=dev)
                     if kind == "batch":
-                        got = digest_list(xxh3_128_batch_device(base, o, ln, mode=r.choice((0, 1, 3)), stream=st))
+                        got = digest_list(xxh3_128_batch_device(base, o, ln, mode=r.choice((0, 1, 2, 3, 4)), stream=st))
                     else:
                         out, cnt = xxh3_128_text_batch_device(base, o, ln, stream=st)
                         got = digest_list(out)
