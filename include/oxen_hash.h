@@ -30,15 +30,16 @@
 extern "C" {
 #endif
 
-#define OXH_ABI_VERSION 2
+#define OXH_ABI_VERSION 3
 
 /* status codes (also used per item in status[]) */
 #define OXH_OK 0
 #define OXH_ERR_INVALID 1   /* bad argument */
 #define OXH_ERR_HIP 2       /* HIP runtime error */
-#define OXH_ERR_IO 3        /* file could not be opened/read (hasher.rs:137-145, 151-164) */
+#define OXH_ERR_IO 3        /* file opened but its read failed (hasher.rs:135-139, 162-165) */
 #define OXH_ERR_NOMEM 4     /* host or device allocation failed */
 #define OXH_ERR_NODEVICE 5  /* no usable MI355X (gfx950) device */
+#define OXH_ERR_OPEN 7      /* per item: File::open failed (hasher.rs:141-145, 151-154) */
 
 /* kernel selection for the device-resident batch */
 #define OXH_MODE_AUTO 0     /* one wave per buffer (K1), lane-per-item for short-only batches */
@@ -124,12 +125,14 @@ int oxh_hash_buffers(oxh_ctx* ctx, const uint8_t* const* bufs, const uint64_t* l
 
 /* get_hash_given_metadata / u128_hash_file_contents x n (hasher.rs:56-65,102-112): reads each file
  * whole (parallel readers straight into pinned staging), overlaps H2D with hashing, and returns
- * digests, file sizes and a per-file status (OXH_OK; OXH_ERR_IO for a file that cannot be opened or
- * read; OXH_ERR_NOMEM for a file larger than a staging slot whose device / pinned buffers cannot be
- * allocated -- the other files of the call are unaffected; digest 0 on error). Files are read to
- * EOF: one whose size differs from its stat (or, below, from the caller's size) is re-read, so the
- * digest covers what the read returned, like read_to_end (hasher.rs:126-148).
- * `sizes` and `status` may be NULL. */
+ * digests, file sizes and a per-file status (OXH_OK; OXH_ERR_OPEN for a file whose open() fails --
+ * File::open in hash_small_file_contents, hasher.rs:141-145; OXH_ERR_IO for a file that opens but
+ * cannot be read -- read_to_end, hasher.rs:135-139, e.g. a directory (EISDIR); OXH_ERR_NOMEM for a
+ * file larger than a staging slot whose device / pinned buffers cannot be allocated -- the other
+ * files of the call are unaffected; digest 0 on error). Files are read to EOF: one whose size
+ * differs from its stat (or, below, from the caller's size) is re-read, so the digest covers what
+ * the read returned, like read_to_end (hasher.rs:126-148).
+ * `sizes` and `status` may be NULL. oxh_hash_files_ex also returns the errno of each failure. */
 int oxh_hash_files(oxh_ctx* ctx, const char* const* paths, uint64_t n, uint64_t* out,
                    uint64_t* sizes, int32_t* status);
 
@@ -156,6 +159,9 @@ int oxh_hash_files_meta(oxh_ctx* ctx, const char* const* paths, const uint64_t* 
  * whose content could not be published, OXH_ERR_NOMEM as for oxh_hash_files. */
 int oxh_add_files(oxh_ctx* ctx, const char* const* paths, uint64_t n, const char* versions_root,
                   uint64_t* out, uint64_t* sizes, int32_t* status, int32_t* stored);
+/* oxh_add_files plus os_error[i] as in oxh_hash_files_ex (0 for a failed publish). */
+int oxh_add_files_ex(oxh_ctx* ctx, const char* const* paths, uint64_t n, const char* versions_root,
+                     uint64_t* out, uint64_t* sizes, int32_t* status, int32_t* stored, int32_t* os_error);
 
 /* Bulk re-hash of a version store: LocalVersionStore::clean_corrupted_versions
  * (storage/local.rs:417-610, `oxen fsck`). Walks {versions_root}/{prefix}/{suffix}/data, hashes every
@@ -178,7 +184,9 @@ int oxh_clean_corrupted_versions(oxh_ctx* ctx, const char* versions_root, int dr
  * GPU of a node is fed its own contiguous share over its own PCIe link. Shares are
  * balanced by bytes when meta_sizes is given. Paths and outputs cross the process boundary through
  * one shared-memory region; calls on one pool serialise. Helpers exit on oxh_pool_destroy, or when
- * the creating process exits. A helper that dies makes the call, and every later call, fail with
+ * the creating process exits (whichever thread created the pool: a helper watches its socket and its
+ * parent process, not the creating thread). A helper that dies, or that has not answered a call
+ * within OXH_WAIT_LIMIT_S seconds (default 60), makes the call, and every later call, fail with
  * OXH_ERR_HIP. Creation fails with the first helper's error (e.g. OXH_ERR_NODEVICE without a GPU).
  * Replaces the reference's fan-out of 64-file batches over num_cpus*2 tasks of one process
  * (core/v_latest/add.rs:422-425) with a fan-out over processes and devices. */
@@ -187,6 +195,9 @@ int oxh_pool_create(const int* devices, int ndevices, int procs, int threads, ui
 /* oxh_hash_files (meta_sizes == NULL) or oxh_hash_files_meta semantics, per-file status[] included. */
 int oxh_pool_hash_files(oxh_pool* pool, const char* const* paths, const uint64_t* meta_sizes, uint64_t n,
                         uint64_t* out, uint64_t* sizes, int32_t* status);
+/* oxh_pool_hash_files plus os_error[i] as in oxh_hash_files_ex. */
+int oxh_pool_hash_files_ex(oxh_pool* pool, const char* const* paths, const uint64_t* meta_sizes, uint64_t n,
+                           uint64_t* out, uint64_t* sizes, int32_t* status, int32_t* os_error);
 /* procs = number of helpers; pids (may be NULL) receives their process ids. */
 int oxh_pool_size(oxh_pool* pool, int* procs, int* pids);
 /* Not while another thread is inside a call on the same pool (the caller owns the pool's lifetime,
@@ -206,6 +217,15 @@ int oxh_hash_files_text(oxh_ctx* ctx, const char* const* paths, uint64_t n, uint
  * mime/data-type decision of add.rs:809-810 then needs no third read of the file. */
 int oxh_hash_files_text_utf8(oxh_ctx* ctx, const char* const* paths, uint64_t n, uint64_t* out,
                              uint64_t* sizes, int32_t* status, uint64_t* counts, int32_t* is_utf8);
+/* The four calls above in one, with the OS error of every failed item: meta_sizes NULL ->
+ * oxh_hash_files, else oxh_hash_files_meta semantics; counts non-NULL -> the K1T counts; is_utf8
+ * non-NULL (needs counts) -> the sniff. os_error[i] (may be NULL) = the errno of item i's failed open
+ * (status OXH_ERR_OPEN) or read (OXH_ERR_IO; 0 when the file ended before the size it was read at),
+ * 0 otherwise -- what the io::Error in the reference's message carries: a Rust caller builds
+ * `std::io::Error::from_raw_os_error(os_error[i])` and formats hasher.rs's own text with it. */
+int oxh_hash_files_ex(oxh_ctx* ctx, const char* const* paths, const uint64_t* meta_sizes, uint64_t n,
+                      uint64_t* out, uint64_t* sizes, int32_t* status, int32_t* os_error,
+                      uint64_t* counts, int32_t* is_utf8);
 
 /* The modified check of `oxen status` (core/v_latest/status.rs:710,734), add (add.rs:723) and
  * checkout (branches.rs:524,548): util::fs::classify_modified_from_node_with_metadata
@@ -238,6 +258,11 @@ int oxh_files_modified(oxh_ctx* ctx, const char* const* paths, const uint64_t* s
                        const uint8_t* mtime_matched, const uint64_t* node_hashes, const uint8_t* node_meta_present,
                        const uint64_t* node_meta_hashes, const uint8_t* file_meta_kind, const uint64_t* file_meta_hashes,
                        uint64_t n, uint8_t* modified, int32_t* status, uint64_t* n_hashed);
+/* oxh_files_modified plus os_error[i] (may be NULL) as in oxh_hash_files_ex for items whose read failed. */
+int oxh_files_modified_ex(oxh_ctx* ctx, const char* const* paths, const uint64_t* sizes, const uint64_t* node_bytes,
+                          const uint8_t* mtime_matched, const uint64_t* node_hashes, const uint8_t* node_meta_present,
+                          const uint64_t* node_meta_hashes, const uint8_t* file_meta_kind, const uint64_t* file_meta_hashes,
+                          uint64_t n, uint8_t* modified, int32_t* status, int32_t* os_error, uint64_t* n_hashed);
 /* Device-resident is_utf8 sniff: d_flags[i] (int32) for item i of the arena (first 4 KiB). */
 int oxh_utf8_prefix_device(const void* d_arena, const uint64_t* d_offsets, const uint64_t* d_lens, uint64_t n,
                            int32_t* d_flags, void* stream);

@@ -20,6 +20,7 @@ OXH_ERR_IO = 3
 OXH_ERR_NOMEM = 4
 OXH_ERR_NODEVICE = 5
 OXH_ERR_META = 6
+OXH_ERR_OPEN = 7
 OXH_META_NONE = 0
 OXH_META_GIVEN = 1
 OXH_META_TEXT = 2
@@ -53,15 +54,22 @@ SIGNATURES = {
     "oxh_hash_buffers": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64p, _u64, _u64p]),
     "oxh_hash_files": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64, _u64p, _u64p, _i32p]),
     "oxh_hash_files_meta": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64p, _u64, _u64p, _u64p, _i32p]),
+    "oxh_hash_files_ex": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64p, _u64, _u64p, _u64p, _i32p, _i32p, _u64p,
+                                 _i32p]),
     "oxh_add_files": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64, ctypes.c_char_p, _u64p, _u64p, _i32p, _i32p]),
+    "oxh_add_files_ex": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64, ctypes.c_char_p, _u64p, _u64p, _i32p, _i32p,
+                                _i32p]),
     "oxh_clean_corrupted_versions": (_int, [_vp, ctypes.c_char_p, _int, _u64p]),
     "oxh_hash_files_text": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64, _u64p, _u64p, _i32p, _u64p]),
     "oxh_xxh3_128_text_batch_device": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
     "oxh_hash_files_text_utf8": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64, _u64p, _u64p, _i32p, _u64p, _i32p]),
     "oxh_files_modified": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64p, _u64p, _vp, _u64p, _vp, _vp, _vp, _vp,
                                   _u64, _vp, _i32p, _u64p]),
+    "oxh_files_modified_ex": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64p, _u64p, _vp, _u64p, _vp, _vp, _vp, _vp,
+                                     _u64, _vp, _i32p, _i32p, _u64p]),
     "oxh_pool_create": (_int, [_vp, _int, _int, _int, _u64, ctypes.POINTER(_vp)]),
     "oxh_pool_hash_files": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _vp, _u64, _u64p, _u64p, _i32p]),
+    "oxh_pool_hash_files_ex": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _vp, _u64, _u64p, _u64p, _i32p, _i32p]),
     "oxh_pool_size": (_int, [_vp, ctypes.POINTER(_int), _vp]),
     "oxh_pool_destroy": (_int, [_vp]),
     "oxh_utf8_prefix_device": (_int, [_vp, _vp, _vp, _u64, _vp, _vp]),

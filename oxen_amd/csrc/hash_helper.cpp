@@ -1,14 +1,18 @@
 // oxen_amd/csrc/hash_helper.cpp -> oxen_amd/oxh_hash_helper: one reader process of an oxh_pool
 // (reader_pool.cpp). Started by oxh_pool_create with its socket on fd 200 and the pool's shared
 // region on fd 201; creates one context on --device with --threads reader threads, reports, then
-// serves requests (its share [lo, hi) of a call's list through oxh_hash_files / _meta, outputs written
-// into the region in place) until told to quit, its socket closes, or its parent dies.
+// serves requests (its share [lo, hi) of a call's list through oxh_hash_files_ex, outputs written
+// into the region in place) until told to quit, its socket closes, or its parent process dies.
+// Parent death is seen as the socket's hang-up or a changed getppid() (checked every second while
+// idle), not through PR_SET_PDEATHSIG, which fires when the spawning THREAD exits: a pool created on
+// a short-lived thread (a tokio spawn_blocking worker, a Python thread) must keep its helpers.
+#include <errno.h>
+#include <poll.h>
 #include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
-#include <sys/prctl.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -43,9 +47,8 @@ bool reply(int sock, uint64_t seq, int rc, const char* msg) {
 
 int main(int argc, char** argv) {
     const int sock = oxh_pool_wire::kSockFd, mem = oxh_pool_wire::kMemFd;
-    prctl(PR_SET_PDEATHSIG, SIGKILL);
     const long ppid = arg(argc, argv, "--ppid", 0);
-    if (ppid && getppid() != (pid_t)ppid) return 1;  // the parent died before the death signal was armed
+    if (ppid && getppid() != (pid_t)ppid) return 1;  // the parent died before this helper started
     const int device = (int)arg(argc, argv, "--device", 0);
     const long threads = arg(argc, argv, "--threads", 0);
     const uint64_t staging = (uint64_t)arg(argc, argv, "--staging", 0);
@@ -60,6 +63,15 @@ int main(int argc, char** argv) {
     uint64_t cap = 0;
     std::vector<const char*> ptrs;
     for (;;) {
+        // idle: wake every second to see whether the parent process is still there (after its death
+        // this process is re-parented, and its socket may stay open in a forked child of the parent)
+        pollfd pf{sock, POLLIN, 0};
+        const int ready = poll(&pf, 1, 1000);
+        if (ready < 0 && errno != EINTR) break;
+        if (ready <= 0) {
+            if (ppid && getppid() != (pid_t)ppid) break;
+            continue;
+        }
         PoolReq q{};
         const ssize_t k = recv(sock, &q, sizeof q, 0);
         if (k != (ssize_t)sizeof q || q.quit) break;
@@ -85,8 +97,9 @@ int main(int argc, char** argv) {
         uint64_t* out = (uint64_t*)(map + q.off_out) + 2 * q.lo;
         uint64_t* sizes = (uint64_t*)(map + q.off_sizes) + q.lo;
         int32_t* status = (int32_t*)(map + q.off_status) + q.lo;
-        rc = q.has_meta ? oxh_hash_files_meta(ctx, ptrs.data(), (const uint64_t*)(map + q.off_meta) + q.lo, m, out, sizes, status)
-                        : oxh_hash_files(ctx, ptrs.data(), m, out, sizes, status);
+        int32_t* os_error = (int32_t*)(map + q.off_oserr) + q.lo;
+        rc = oxh_hash_files_ex(ctx, ptrs.data(), q.has_meta ? (const uint64_t*)(map + q.off_meta) + q.lo : nullptr, m, out,
+                               sizes, status, os_error, nullptr, nullptr);
         if (!reply(sock, q.seq, rc, rc ? oxh_last_error() : "")) break;
     }
     if (map) munmap(map, cap);

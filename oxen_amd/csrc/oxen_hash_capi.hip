@@ -560,8 +560,10 @@ struct LargeSource {
     virtual void unpin(const uint8_t*) {}
     // [off, off + n) will be read soon.
     virtual void will_need(uint64_t, uint64_t) {}
-    // Read [off, off + n) into dst; called from several threads for disjoint ranges. false = I/O error.
+    // Read [off, off + n) into dst; called from several threads for disjoint ranges. false = I/O error
+    // (os_error then holds the errno of the failed read, 0 for a file that ended early).
     virtual bool read(uint64_t off, uint64_t n, uint8_t* dst) = 0;
+    std::atomic<int> os_error{0};
 };
 
 // A regular file: preads, or mmap pages pinned in place for the copy-free path.
@@ -611,6 +613,7 @@ struct FileSource final : LargeSource {
     bool read(uint64_t off, uint64_t n, uint8_t* dst) override {
         for (uint64_t got = 0; got < n;) {
             const ssize_t x = pread(fd, dst + got, n - got, (off_t)(off + got));
+            if (x < 0) os_error.store(errno);
             if (x <= 0) return false;
             got += (uint64_t)x;
         }
@@ -632,6 +635,7 @@ struct LargeResult {
     uint64_t out[2] = {0, 0}, cnt[2] = {0, 0};  // digest; text counts (num_lines, num_chars)
     int32_t utf8 = 0;
     int status = OXH_OK;  // this item's status: OXH_OK, OXH_ERR_IO or OXH_ERR_NOMEM
+    int os_error = 0;     // errno of a failed read (OXH_ERR_IO)
 };
 
 // One large item of a large_items() batch: its source and what the caller wants, then the outcome.
@@ -676,16 +680,35 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
     };
     const uint64_t need = (uint64_t)n * (2 * slot + kRes) + 4096;
     if (c->d_big_size < need) {
+        // Regrow without a device-wide sync: every earlier large_items call on this context finished
+        // its work on d_big before it returned (both of its streams are synchronised at the end), and
+        // the buffer is stream-ordered memory of c->stream (hipMallocAsync / hipFreeAsync), so other
+        // contexts and device-resident callers on their own streams never wait for the regrowth.
         if (c->d_big) {
-            HIP_TRY(hipDeviceSynchronize());
-            (void)hipFree(c->d_big);
+            (void)hipFreeAsync(c->d_big, c->stream);
             c->d_big = nullptr;
             c->d_big_size = 0;
         }
-        if (hipMalloc(&c->d_big, need) != hipSuccess) {
-            c->d_big = nullptr;
+        void* m = nullptr;
+        const bool ok = hipMallocAsync(&m, need, c->stream) == hipSuccess && m != nullptr;
+        // the copy stream's first piece must not run ahead of the allocation
+        if (!ok || hipStreamSynchronize(c->stream) != hipSuccess) {
+            (void)hipGetLastError();
+            if (ok) {
+                (void)hipFreeAsync(m, c->stream);
+                (void)hipStreamSynchronize(c->stream);
+                (void)hipGetLastError();
+            }
+            // 2 piece buffers per file side by side did not fit: fewer files at a time (each item's
+            // result does not depend on its batch), down to one before the items fail with NOMEM
+            if (n > 1) {
+                const int h = n / 2;
+                if (int rc = large_items(c, jobs, h)) return rc;
+                return large_items(c, jobs + h, n - h);
+            }
             return nomem();
         }
+        c->d_big = (uint8_t*)m;
         c->d_big_size = need;
     }
     auto dbuf = [&](int q, int b) { return c->d_big + ((uint64_t)q * 2 + b) * slot; };
@@ -909,6 +932,7 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
         if (rc) continue;
         if (!st[q].io_ok) {
             res.status = OXH_ERR_IO;
+            res.os_error = jobs[q].src->os_error.load();
             continue;
         }
         res.out[0] = h.out[0];
@@ -1029,7 +1053,10 @@ int oxh_ctx_destroy(oxh_ctx* c) {
         if (c->ev_copied[s]) (void)hipEventDestroy(c->ev_copied[s]);
         if (c->ev_done[s]) (void)hipEventDestroy(c->ev_done[s]);
     }
-    if (c->d_big) (void)hipFree(c->d_big);
+    if (c->d_big) {  // stream-ordered memory (large_items)
+        (void)hipFreeAsync(c->d_big, c->stream);
+        (void)hipStreamSynchronize(c->stream);
+    }
     for (int b = 0; b < kNBounce; ++b) {
         if (c->h_bounce[b]) (void)hipHostFree(c->h_bounce[b]);
         if (c->ev_bounce[b]) (void)hipEventDestroy(c->ev_bounce[b]);
@@ -1556,9 +1583,11 @@ struct FileRequest {
     int32_t* status = nullptr;
     uint64_t* counts = nullptr;
     int32_t* utf8 = nullptr;
+    int32_t* os_err = nullptr;  // per item: errno of a failed open (OXH_ERR_OPEN) or read (OXH_ERR_IO)
     ItemSink* sink = nullptr;
     std::vector<uint64_t> lens;
     std::vector<int32_t> st;
+    std::vector<int32_t> eno;
     uint64_t next = 0;                   // claim cursor (under ctx->qmu)
     size_t idx = 0;                      // index in the run's request table
     std::atomic<uint64_t> remaining{0};  // items not yet accounted for
@@ -1611,6 +1640,7 @@ void finish_request(FileStream& fs, FileRequest* r) {
         }
         if (r->sizes) r->sizes[i] = r->lens[i];
         if (r->status) r->status[i] = r->st[i];
+        if (r->os_err) r->os_err[i] = r->st[i] == OXH_OK ? 0 : r->eno[i];
     }
     {
         std::lock_guard<std::mutex> g(fs.c->qmu);
@@ -1620,6 +1650,22 @@ void finish_request(FileStream& fs, FileRequest* r) {
     std::lock_guard<std::mutex> g(r->mu);  // notify under the lock: the caller frees r once it sees done
     r->done = true;
     r->cv.notify_all();
+}
+
+// Item i of r could not be hashed. `code` says which call of the reference's hash_small_file_contents
+// failed (hasher.rs:126-146): File::open (OXH_ERR_OPEN) or the read (OXH_ERR_IO); `e` is the errno its
+// io::Error carries (0: the file ended before the size it was read at).
+inline void item_failed(FileRequest* r, uint64_t i, int code, int e) {
+    r->st[i] = code;
+    r->eno[i] = e;
+}
+// The errno of an opened file that is not hashed: the fstat's own failure, or, for a file that is not
+// regular, what its read reports -- open(2) of a directory succeeds on Linux and the read fails with
+// EISDIR, as File::open + read_to_end do in the reference; other non-regular files are refused as
+// unreadable (EINVAL). Call right after the failed fstat / S_ISREG test on fd.
+inline int unreadable_errno(int fd, struct stat& sb) {
+    if (fstat(fd, &sb) != 0) return errno;
+    return S_ISDIR(sb.st_mode) ? EISDIR : EINVAL;
 }
 
 // k more items of r are fully written; the thread that accounts the last one completes r.
@@ -1726,7 +1772,7 @@ void reader_loop(FileStream& fs) {
             struct stat sb;
             const int fd = r->paths[i] ? open(r->paths[i], O_RDONLY | O_CLOEXEC | O_NONBLOCK) : -1;
             if (fd < 0) {
-                r->st[i] = OXH_ERR_IO;
+                item_failed(r, i, OXH_ERR_OPEN, r->paths[i] ? errno : EINVAL);
                 ++failed;
                 continue;
             }
@@ -1736,8 +1782,8 @@ void reader_loop(FileStream& fs) {
             // as it is at read time, like the reference's read_to_end (hasher.rs:126-148)
             const bool meta = r->meta != nullptr && r->meta[i] < c->stage_bytes;
             if (!meta && (fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode))) {
+                item_failed(r, i, OXH_ERR_IO, unreadable_errno(fd, sb));
                 close(fd);
-                r->st[i] = OXH_ERR_IO;
                 ++failed;
                 continue;
             }
@@ -1766,7 +1812,7 @@ void reader_loop(FileStream& fs) {
             while (got < want) {
                 const ssize_t k = pread(fd, dst + got, want - got, (off_t)got);
                 if (k < 0) {
-                    r->st[i] = OXH_ERR_IO;
+                    item_failed(r, i, OXH_ERR_IO, errno);
                     break;
                 }
                 if (k == 0) break;  // EOF
@@ -1855,9 +1901,13 @@ int big_files(FileStream& fs, const std::vector<std::pair<FileRequest*, uint64_t
         // reference reads whatever the file holds when it opens it (hasher.rs:150-174).
         const int fd = open(r->paths[i], O_RDONLY | O_CLOEXEC | O_NONBLOCK);
         struct stat sb;
-        if (fd < 0 || fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode)) {
-            if (fd >= 0) close(fd);
-            r->st[i] = OXH_ERR_IO;
+        if (fd < 0) {
+            item_failed(r, i, OXH_ERR_OPEN, errno);
+            continue;
+        }
+        if (fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode)) {
+            item_failed(r, i, OXH_ERR_IO, unreadable_errno(fd, sb));
+            close(fd);
             continue;
         }
         r->lens[i] = (uint64_t)sb.st_size;
@@ -1879,7 +1929,7 @@ int big_files(FileStream& fs, const std::vector<std::pair<FileRequest*, uint64_t
         const uint64_t i = items[who[k]].second;
         const LargeResult& res = jobs[k].res;
         if (res.status != OXH_OK) {
-            r->st[i] = res.status;
+            item_failed(r, i, res.status, res.os_error);
             continue;
         }
         r->out[2 * i] = res.out[0];
@@ -1911,8 +1961,9 @@ int refresh_file(FileStream& fs, FileRequest* r, uint64_t i) {
     struct stat sb;
     const int fd = open(r->paths[i], O_RDONLY | O_CLOEXEC | O_NONBLOCK);
     if (fd < 0 || fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode)) {
+        if (fd < 0) item_failed(r, i, OXH_ERR_OPEN, errno);
+        else item_failed(r, i, OXH_ERR_IO, unreadable_errno(fd, sb));
         if (fd >= 0) close(fd);
-        r->st[i] = OXH_ERR_IO;
         account(fs, r, 1);
         return OXH_OK;
     }
@@ -1927,13 +1978,14 @@ int refresh_file(FileStream& fs, FileRequest* r, uint64_t i) {
     std::vector<uint8_t> tmp(std::max<uint64_t>(L + 1, 4096));
     uint64_t got = 0;
     bool bad = false;
+    int bad_errno = 0;
     for (;;) {
         if (got == tmp.size()) {
             if (tmp.size() >= c->stage_bytes) break;  // grew past a staging slot meanwhile
             tmp.resize(std::min<uint64_t>(2 * tmp.size(), c->stage_bytes));
         }
         const ssize_t k = pread(fd, tmp.data() + got, tmp.size() - got, (off_t)got);
-        if (k < 0) bad = true;
+        if (k < 0) bad = true, bad_errno = errno;
         if (k <= 0) break;
         got += (uint64_t)k;
     }
@@ -1946,14 +1998,14 @@ int refresh_file(FileStream& fs, FileRequest* r, uint64_t i) {
     close(fd);
     r->lens[i] = got;
     if (bad) {
-        r->st[i] = OXH_ERR_IO;
+        item_failed(r, i, OXH_ERR_IO, bad_errno);
     } else {
         const uint64_t L = got;
         int32_t u8 = 0;
         const int rc = oversize_item(c, tmp.data(), L, r->out + 2 * i, r->counts ? r->counts + 2 * i : nullptr,
                                      r->utf8 ? &u8 : nullptr);
         if (rc == OXH_ERR_NOMEM) {
-            r->st[i] = OXH_ERR_NOMEM;  // this file's failure, not the run's
+            item_failed(r, i, OXH_ERR_NOMEM, ENOMEM);  // this file's failure, not the run's
         } else if (rc) {
             return rc;
         } else {
@@ -2190,7 +2242,7 @@ static void dump_engine(oxh_ctx* c, const FileRequest& r) {
 
 static int hash_files_impl(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* sizes, int32_t* status,
                            uint64_t* counts, ItemSink* sink = nullptr, int32_t* utf8 = nullptr,
-                           const uint64_t* meta = nullptr) {
+                           const uint64_t* meta = nullptr, int32_t* os_error = nullptr) {
     if (!c || (n && (!paths || !out))) return fail(OXH_ERR_INVALID, "bad arguments");
     if (n == 0) return OXH_OK;
     FileRequest r;
@@ -2202,9 +2254,11 @@ static int hash_files_impl(oxh_ctx* c, const char* const* paths, uint64_t n, uin
     r.status = status;
     r.counts = counts;
     r.utf8 = utf8;
+    r.os_err = os_error;
     r.sink = sink;
     r.lens.assign(n, 0);
     r.st.assign(n, OXH_OK);
+    r.eno.assign(n, 0);
     r.remaining.store(n);
     {
         std::lock_guard<std::mutex> g(c->qmu);
@@ -2253,6 +2307,14 @@ int oxh_hash_files_text_utf8(oxh_ctx* c, const char* const* paths, uint64_t n, u
     return hash_files_impl(c, paths, n, out, sizes, status, counts, nullptr, is_utf8);
 }
 
+int oxh_hash_files_ex(oxh_ctx* c, const char* const* paths, const uint64_t* meta_sizes, uint64_t n, uint64_t* out,
+                      uint64_t* sizes, int32_t* status, int32_t* os_error, uint64_t* counts, int32_t* is_utf8) {
+    if (is_utf8 && !counts) return fail(OXH_ERR_INVALID, "is_utf8 needs counts");
+    if (is_utf8)
+        for (uint64_t i = 0; i < n; ++i) is_utf8[i] = 0;
+    return hash_files_impl(c, paths, n, out, sizes, status, counts, nullptr, is_utf8, meta_sizes, os_error);
+}
+
 // util::fs::classify_modified_from_node_with_metadata (util/fs.rs:1580-1619) x n: the size and mtime
 // verdicts and a caller-computed metadata-hash verdict are decided on the host from what the caller's
 // walk holds; every item that still needs its file read is read ONCE, all of them in ONE engine request
@@ -2261,6 +2323,14 @@ int oxh_files_modified(oxh_ctx* c, const char* const* paths, const uint64_t* siz
                        const uint8_t* mtime_matched, const uint64_t* node_hashes, const uint8_t* node_meta_present,
                        const uint64_t* node_meta_hashes, const uint8_t* file_meta_kind, const uint64_t* file_meta_hashes,
                        uint64_t n, uint8_t* modified, int32_t* status, uint64_t* n_hashed) {
+    return oxh_files_modified_ex(c, paths, sizes, node_bytes, mtime_matched, node_hashes, node_meta_present, node_meta_hashes,
+                                 file_meta_kind, file_meta_hashes, n, modified, status, nullptr, n_hashed);
+}
+
+int oxh_files_modified_ex(oxh_ctx* c, const char* const* paths, const uint64_t* sizes, const uint64_t* node_bytes,
+                          const uint8_t* mtime_matched, const uint64_t* node_hashes, const uint8_t* node_meta_present,
+                          const uint64_t* node_meta_hashes, const uint8_t* file_meta_kind, const uint64_t* file_meta_hashes,
+                          uint64_t n, uint8_t* modified, int32_t* status, int32_t* os_error, uint64_t* n_hashed) {
     if (!c || (n && (!paths || !sizes || !node_bytes || !mtime_matched || !node_hashes || !modified)))
         return fail(OXH_ERR_INVALID, "bad arguments");
     if ((node_meta_present == nullptr) != (node_meta_hashes == nullptr))
@@ -2275,6 +2345,7 @@ int oxh_files_modified(oxh_ctx* c, const char* const* paths, const uint64_t* siz
     for (uint64_t i = 0; i < n; ++i) {
         modified[i] = sizes[i] != node_bytes[i] ? 1 : 0;  // fs.rs:1590-1592: no hashing needed
         if (status) status[i] = OXH_OK;
+        if (os_error) os_error[i] = 0;
         if (modified[i] || mtime_matched[i]) continue;     // fs.rs:1595-1597: a matched mtime is trusted
         const int kind = file_meta_kind ? file_meta_kind[i] : OXH_META_NONE;
         const bool node_has = node_meta_present && node_meta_present[i];
@@ -2295,10 +2366,10 @@ int oxh_files_modified(oxh_ctx* c, const char* const* paths, const uint64_t* siz
     const uint64_t m = idx.size();
     std::vector<const char*> p(m);
     std::vector<uint64_t> ms(m), out(2 * m), cnt(any_text ? 2 * m : 0);
-    std::vector<int32_t> st(m, OXH_OK);
+    std::vector<int32_t> st(m, OXH_OK), eno(m, 0);
     for (uint64_t k = 0; k < m; ++k) p[k] = paths[idx[k]], ms[k] = sizes[idx[k]];
     int rc = hash_files_impl(c, p.data(), m, out.data(), nullptr, st.data(), any_text ? cnt.data() : nullptr, nullptr,
-                             nullptr, ms.data());
+                             nullptr, ms.data(), eno.data());
     if (rc) return rc;
     // MetadataText of the text items whose node has a metadata hash: serde_json of GenericMetadata
     // (model/metadata/generic_metadata.rs, untagged; MetadataText's field order) hashed in one batch
@@ -2326,8 +2397,9 @@ int oxh_files_modified(oxh_ctx* c, const char* const* paths, const uint64_t* siz
     }
     for (uint64_t k = 0; k < m; ++k) {
         const uint64_t i = idx[k];
-        if (st[k] != OXH_OK) {  // the reference returns the read error for this path
+        if (st[k] != OXH_OK) {  // the reference returns the open / read error for this path
             if (status) status[i] = st[k];
+            if (os_error) os_error[i] = eno[k];
             continue;
         }
         if (meta_differs[k]) {  // fs.rs:1609-1614
@@ -2656,10 +2728,15 @@ class VersionPublisher final : public ItemSink {
 
 int oxh_add_files(oxh_ctx* c, const char* const* paths, uint64_t n, const char* versions_root, uint64_t* out,
                   uint64_t* sizes, int32_t* status, int32_t* stored) {
+    return oxh_add_files_ex(c, paths, n, versions_root, out, sizes, status, stored, nullptr);
+}
+
+int oxh_add_files_ex(oxh_ctx* c, const char* const* paths, uint64_t n, const char* versions_root, uint64_t* out,
+                     uint64_t* sizes, int32_t* status, int32_t* stored, int32_t* os_error) {
     if (n && (!versions_root || !stored || !status)) return fail(OXH_ERR_INVALID, "versions_root/status/stored is NULL");
     for (uint64_t i = 0; i < n; ++i) stored[i] = 0;
     VersionPublisher pub(c, versions_root ? versions_root : "", n);
-    const int rc = hash_files_impl(c, paths, n, out, sizes, status, nullptr, &pub);
+    const int rc = hash_files_impl(c, paths, n, out, sizes, status, nullptr, &pub, nullptr, nullptr, os_error);
     if (rc) return rc;
     pub.wait();
     pub.finish(n, out, status, stored);

@@ -15,10 +15,13 @@
 //
 // Helpers are started with posix_spawn (fork + exec in the child: nothing of this process's GPU
 // state is inherited), get the shared region and their socket as fixed descriptors, and exit when
-// the pool is destroyed, when their socket closes, or when this process dies (PR_SET_PDEATHSIG).
+// the pool is destroyed, when their socket closes, or when this process dies (the helper polls its
+// socket and checks getppid(); PR_SET_PDEATHSIG is not used: it fires when the creating THREAD
+// exits, so a pool created on a short-lived thread would lose its helpers with that thread).
 #include <dlfcn.h>
 #include <errno.h>
 #include <fcntl.h>
+#include <poll.h>
 #include <signal.h>
 #include <spawn.h>
 #include <string.h>
@@ -28,6 +31,9 @@
 #include <sys/wait.h>
 #include <time.h>
 #include <unistd.h>
+
+#include <stdio.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <mutex>
@@ -97,6 +103,34 @@ bool recv_rep(int fd, PoolRep& r) {
     }
 }
 
+// A call's reply from helper h. A helper that has not answered within OXH_WAIT_LIMIT_S seconds
+// (default 60) is reported on stderr, like a stalled request of the in-process engine, and waited
+// for further: a share of a large cold list can take that long. OXH_POOL_CALL_LIMIT_S (default 0 =
+// no limit) turns the wait into a deadline: the call then fails and the pool is marked unusable.
+// false: the helper exited, or the deadline passed.
+bool wait_rep(int fd, pid_t pid, uint64_t seq, PoolRep& r) {
+    const double report = getenv("OXH_WAIT_LIMIT_S") ? atof(getenv("OXH_WAIT_LIMIT_S")) : 60.0;
+    const double limit = getenv("OXH_POOL_CALL_LIMIT_S") ? atof(getenv("OXH_POOL_CALL_LIMIT_S")) : 0.0;
+    timespec t0;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    double next_report = report;
+    for (;;) {
+        pollfd pf{fd, POLLIN, 0};
+        const int k = poll(&pf, 1, 1000);
+        if (k > 0) return recv_rep(fd, r);
+        if (k < 0 && errno != EINTR) return false;
+        timespec t;
+        clock_gettime(CLOCK_MONOTONIC, &t);
+        const double waited = (double)(t.tv_sec - t0.tv_sec) + 1e-9 * (double)(t.tv_nsec - t0.tv_nsec);
+        if (limit > 0 && waited >= limit) return false;
+        if (report > 0 && waited >= next_report) {
+            fprintf(stderr, "[oxh] reader pool: helper pid %d has not answered call %llu after %.0f s\n", (int)pid,
+                    (unsigned long long)seq, waited);
+            next_report += report;
+        }
+    }
+}
+
 void reap(oxh_pool* p, bool polite) {
     for (auto& h : p->helpers) {
         if (h.sock >= 0) {
@@ -154,6 +188,9 @@ int grow(oxh_pool* p, uint64_t need) {
 int mark_broken(oxh_pool* p, const std::string& why) {
     p->broken = true;
     p->broken_msg = why;
+    // a helper may be stuck (the deadline case) or mid-call for another share: none of them is asked
+    for (auto& h : p->helpers)
+        if (h.pid > 0) kill(h.pid, SIGKILL);
     reap(p, false);
     return fail(OXH_ERR_HIP, why);
 }
@@ -241,6 +278,11 @@ int oxh_pool_create(const int* devices, int ndevices, int procs, int threads, ui
 
 int oxh_pool_hash_files(oxh_pool* p, const char* const* paths, const uint64_t* meta_sizes, uint64_t n, uint64_t* out,
                         uint64_t* sizes, int32_t* status) {
+    return oxh_pool_hash_files_ex(p, paths, meta_sizes, n, out, sizes, status, nullptr);
+}
+
+int oxh_pool_hash_files_ex(oxh_pool* p, const char* const* paths, const uint64_t* meta_sizes, uint64_t n, uint64_t* out,
+                           uint64_t* sizes, int32_t* status, int32_t* os_error) {
     if (!p || (n && (!paths || !out))) return fail(OXH_ERR_INVALID, "oxh_pool_hash_files: bad arguments");
     std::lock_guard<std::mutex> lk(p->mu);
     if (p->broken) return fail(OXH_ERR_HIP, "reader pool is unusable: " + p->broken_msg);
@@ -259,7 +301,8 @@ int oxh_pool_hash_files(oxh_pool* p, const char* const* paths, const uint64_t* m
     q.off_out = q.off_meta + (has_meta ? al64(8 * n) : 0);
     q.off_sizes = q.off_out + al64(16 * n);
     q.off_status = q.off_sizes + al64(8 * n);
-    q.off_blob = q.off_status + al64(4 * n);
+    q.off_oserr = q.off_status + al64(4 * n);
+    q.off_blob = q.off_oserr + al64(4 * n);
     if (int rc = grow(p, q.off_blob + blob)) return rc;
     q.cap = p->cap;
     uint64_t* offs = (uint64_t*)(p->map + q.off_offs);
@@ -299,8 +342,9 @@ int oxh_pool_hash_files(oxh_pool* p, const char* const* paths, const uint64_t* m
     std::string msg;
     for (int k : busy) {
         PoolRep r{};
-        if (!recv_rep(p->helpers[k].sock, r) || r.seq != q.seq)
-            return mark_broken(p, "reader pool helper (pid " + std::to_string(p->helpers[k].pid) + ") died during a call");
+        if (!wait_rep(p->helpers[k].sock, p->helpers[k].pid, q.seq, r) || r.seq != q.seq)
+            return mark_broken(p, "reader pool helper (pid " + std::to_string(p->helpers[k].pid) +
+                                      ") died during a call or missed OXH_POOL_CALL_LIMIT_S");
         if (r.rc != OXH_OK && rc == OXH_OK) {
             r.msg[sizeof r.msg - 1] = 0;
             rc = r.rc, msg = r.msg;
@@ -310,6 +354,7 @@ int oxh_pool_hash_files(oxh_pool* p, const char* const* paths, const uint64_t* m
     memcpy(out, p->map + q.off_out, 16 * n);
     if (sizes) memcpy(sizes, p->map + q.off_sizes, 8 * n);
     if (status) memcpy(status, p->map + q.off_status, 4 * n);
+    if (os_error) memcpy(os_error, p->map + q.off_oserr, 4 * n);
     return OXH_OK;
 }
 

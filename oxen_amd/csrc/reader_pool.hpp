@@ -19,12 +19,13 @@ constexpr int kMemFd = 201;   // the shared region
 //   out    u64[2n]  digests (lo, hi)
 //   sizes  u64[n]
 //   status i32[n]
+//   oserr  i32[n]   errno of each failed open / read (oxh_hash_files_ex)
 //   blob   the paths, back to back
 struct PoolReq {
     uint64_t seq;   // call number; the reply echoes it
     uint64_t cap;   // region size: the helper re-maps when it changed
     uint64_t n, lo, hi;
-    uint64_t off_offs, off_meta, off_out, off_sizes, off_status, off_blob;
+    uint64_t off_offs, off_meta, off_out, off_sizes, off_status, off_oserr, off_blob;
     int32_t has_meta;
     int32_t quit;   // 1: exit
 };

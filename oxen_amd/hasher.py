@@ -134,6 +134,91 @@ def hash_files_128bit(paths: Sequence[str], ctx: Optional[_capi.Context] = None)
 
 
 
+def hash_files_with_errors_128bit(paths: Sequence[str], meta_sizes: Optional[Sequence[int]] = None,
+                                  ctx: Optional[_capi.Context] = None):
+    """hash_files_128bit (meta_sizes None) or hash_files_given_metadata_128bit through oxh_hash_files_ex:
+    returns (digests, sizes, status, os_error), os_error[i] being the errno of item i's failed open
+    (status OXH_ERR_OPEN) or read (OXH_ERR_IO), from which `file_error` builds hasher.rs's message."""
+    ctx = ctx or default_context()
+    n = len(paths)
+    if n == 0:
+        return [], [], [], []
+    if meta_sizes is not None and len(meta_sizes) != n:
+        raise _capi.OxenError("paths and meta_sizes differ in length", _capi.OXH_ERR_INVALID)
+    table = _PathTable(paths)
+    meta = None if meta_sizes is None else np.ascontiguousarray(meta_sizes, dtype=np.uint64)
+    out = np.zeros((n, 2), dtype=np.uint64)
+    sizes = np.zeros(n, dtype=np.uint64)
+    status = np.zeros(n, dtype=np.int32)
+    oserr = np.zeros(n, dtype=np.int32)
+    _capi.check(_capi.lib().oxh_hash_files_ex(ctx.handle, table.arg, None if meta is None else meta.ctypes.data_as(_capi._u64p),
+                                              n, out.ctypes.data_as(_capi._u64p), sizes.ctypes.data_as(_capi._u64p),
+                                              status.ctypes.data_as(_capi._i32p), oserr.ctypes.data_as(_capi._i32p),
+                                              None, None), "oxh_hash_files_ex")
+    return _u128_list(out, status), sizes.tolist(), status.tolist(), oserr.tolist()
+
+
+# std::io::ErrorKind of an OS error (Rust std, sys/pal/unix decode_error_kind): the `kind` field of
+# the io::Error Debug text that hasher.rs puts in its open-failure message
+_IO_ERROR_KINDS = {
+    "E2BIG": "ArgumentListTooLong", "EADDRINUSE": "AddrInUse", "EADDRNOTAVAIL": "AddrNotAvailable",
+    "EBUSY": "ResourceBusy", "ECONNABORTED": "ConnectionAborted", "ECONNREFUSED": "ConnectionRefused",
+    "ECONNRESET": "ConnectionReset", "EDEADLK": "Deadlock", "EDQUOT": "FilesystemQuotaExceeded",
+    "EEXIST": "AlreadyExists", "EFBIG": "FileTooLarge", "EHOSTUNREACH": "HostUnreachable", "EINTR": "Interrupted",
+    "EINVAL": "InvalidInput", "EISDIR": "IsADirectory", "ELOOP": "FilesystemLoop", "ENOENT": "NotFound",
+    "ENOMEM": "OutOfMemory", "ENOSPC": "StorageFull", "ENOSYS": "Unsupported", "EMLINK": "TooManyLinks",
+    "ENAMETOOLONG": "InvalidFilename", "ENETDOWN": "NetworkDown", "ENETUNREACH": "NetworkUnreachable",
+    "ENOTCONN": "NotConnected", "ENOTDIR": "NotADirectory", "ENOTEMPTY": "DirectoryNotEmpty", "EPIPE": "BrokenPipe",
+    "EROFS": "ReadOnlyFilesystem", "ESPIPE": "NotSeekable", "ESTALE": "StaleNetworkFileHandle", "ETIMEDOUT": "TimedOut",
+    "ETXTBSY": "ExecutableFileBusy", "EXDEV": "CrossesDevices", "EINPROGRESS": "InProgress",
+    "EACCES": "PermissionDenied", "EPERM": "PermissionDenied", "EAGAIN": "WouldBlock", "EWOULDBLOCK": "WouldBlock",
+}
+
+
+def rust_str_debug(text: str) -> str:
+    """`{:?}` of a Rust str / Path: double quotes; backslash, double quote, newline, carriage return,
+    tab and NUL escaped, other control characters as \\u{..}."""
+    esc = {'"': '\\"', "\\": "\\\\", "\n": "\\n", "\r": "\\r", "\t": "\\t", "\0": "\\0"}
+    out = ['"']
+    for ch in text:
+        o = ord(ch)
+        if ch in esc:
+            out.append(esc[ch])
+        elif o < 0x20 or o == 0x7F or 0xD800 <= o <= 0xDFFF:
+            out.append("\\u{%x}" % o)
+        else:
+            out.append(ch)
+    out.append('"')
+    return "".join(out)
+
+
+def rust_io_error_debug(errno_value: int) -> str:
+    """`{:?}` of std::io::Error::from_raw_os_error(errno_value): `Os { code, kind, message }`."""
+    import errno as _errno
+
+    name = _errno.errorcode.get(int(errno_value), "")
+    kind = _IO_ERROR_KINDS.get(name, "Uncategorized")
+    return f"Os {{ code: {int(errno_value)}, kind: {kind}, message: {rust_str_debug(os.strerror(int(errno_value)))} }}"
+
+
+LARGE_FILE_BYTES = 1_000_000_000  # hasher.rs:56-65, 106: one-shot below, 4 KiB streamed at or above
+
+
+def file_error(path, status: int, os_error: int, size_hint: Optional[int] = None) -> OxenError:
+    """The OxenError hasher.rs returns for a file that could not be hashed: File::open failed
+    (status OXH_ERR_OPEN; hasher.rs:141-145, or :151-154 for the streamed branch a size >= 1e9 picks),
+    or the read did (OXH_ERR_IO; :135-139 / :161-165)."""
+    if status == _capi.OXH_ERR_OPEN:
+        p = rust_str_debug(os.fsdecode(path) if isinstance(path, (bytes, os.PathLike)) else str(path))
+        err = rust_io_error_debug(os_error)
+        if size_hint is not None and size_hint >= LARGE_FILE_BYTES:
+            return OxenError(f"Could not open file {p} due to {err}", _capi.OXH_ERR_OPEN)
+        return OxenError(f"util::hasher::hash_file_contents Could not open file {p} {err}", _capi.OXH_ERR_OPEN)
+    if status == _capi.OXH_ERR_NOMEM:
+        return OxenError("Could not allocate the buffers to hash a large file", _capi.OXH_ERR_NOMEM)
+    return OxenError("Could not read file for hashing", _capi.OXH_ERR_IO)
+
+
 def hash_files_given_metadata_128bit(paths: Sequence[str], meta_sizes: Sequence[int],
                                      ctx: Optional[_capi.Context] = None):
     """`get_hash_given_metadata(path, &metadata)` over many files (hasher.rs:56-65) with the sizes
@@ -167,7 +252,7 @@ TEXT = "text"  # files_modified's file_metadata marker for data type Text (Metad
 def files_modified(paths: Sequence[str], sizes: Sequence[int], node_bytes: Sequence[int],
                    mtime_matched: Sequence[bool], node_hashes: Sequence[int],
                    ctx: Optional[_capi.Context] = None, node_metadata_hashes: Optional[Sequence[Optional[int]]] = None,
-                   file_metadata: Optional[Sequence] = None):
+                   file_metadata: Optional[Sequence] = None, os_errors: Optional[list] = None):
     """`classify_modified_from_node_with_metadata` (util/fs.rs:1580-1619) over many working-tree files
     (oxh_files_modified): the modified check `oxen status` runs per tracked file
     (core/v_latest/status.rs:710,734). sizes = the walk's metadata.len(), node_bytes / node_hashes =
@@ -181,7 +266,8 @@ def files_modified(paths: Sequence[str], sizes: Sequence[int], node_bytes: Seque
       Exception       the caller's extraction failed (status[i] = OXH_ERR_META, as the reference's `?`)
     Returns (modified, status, n_hashed): only files with an equal size and a drifted mtime whose
     metadata hash does not already differ are read, all in one GPU pass; status[i] != 0 is that
-    file's error (the reference returns it)."""
+    file's error (the reference returns it); a list passed as `os_errors` receives the errno of each
+    such failure (hasher.file_error builds the reference's message from it)."""
     ctx = ctx or default_context()
     n = len(paths)
     if not (len(sizes) == len(node_bytes) == len(mtime_matched) == len(node_hashes) == n):
@@ -225,13 +311,16 @@ def files_modified(paths: Sequence[str], sizes: Sequence[int], node_bytes: Seque
         fh = _split_u128(fhv)
     modified = np.zeros(n, dtype=np.uint8)
     status = np.zeros(n, dtype=np.int32)
+    oserr = np.zeros(n, dtype=np.int32)
     hashed = (ctypes.c_uint64 * 1)()
     ptr = lambda a: None if a is None else a.ctypes.data  # noqa: E731
-    _capi.check(_capi.lib().oxh_files_modified(ctx.handle, arr, sz.ctypes.data_as(_capi._u64p),
-                                               nb.ctypes.data_as(_capi._u64p), mm.ctypes.data,
-                                               nh.ctypes.data_as(_capi._u64p), ptr(nmp), ptr(nmh), ptr(fk), ptr(fh),
-                                               n, modified.ctypes.data,
-                                               status.ctypes.data_as(_capi._i32p), hashed), "oxh_files_modified")
+    _capi.check(_capi.lib().oxh_files_modified_ex(ctx.handle, arr, sz.ctypes.data_as(_capi._u64p),
+                                                  nb.ctypes.data_as(_capi._u64p), mm.ctypes.data,
+                                                  nh.ctypes.data_as(_capi._u64p), ptr(nmp), ptr(nmh), ptr(fk), ptr(fh),
+                                                  n, modified.ctypes.data, status.ctypes.data_as(_capi._i32p),
+                                                  oserr.ctypes.data_as(_capi._i32p), hashed), "oxh_files_modified_ex")
+    if os_errors is not None:
+        os_errors[:] = oserr.tolist()
     return [bool(m) for m in modified], [int(s) for s in status], int(hashed[0])
 
 
@@ -240,13 +329,15 @@ def classify_modified_from_node_with_metadata(path, node_num_bytes: int, node_ha
                                               node_metadata_hash: Optional[int] = None, file_metadata=None) -> bool:
     """util/fs.rs:1580-1619 for one file (the batched form is files_modified); an extraction or read
     error raises OxenError like the reference's `?`."""
+    oserr: list = []
     modified, status, _ = files_modified([path], [metadata.st_size], [node_num_bytes], [mtime_matched], [node_hash],
-                                         node_metadata_hashes=[node_metadata_hash], file_metadata=[file_metadata])
+                                         node_metadata_hashes=[node_metadata_hash], file_metadata=[file_metadata],
+                                         os_errors=oserr)
     if status[0] == _capi.OXH_ERR_META:
         err = file_metadata
         raise OxenError(str(err) if str(err) else "could not compute file metadata", _capi.OXH_ERR_META)
-    if status[0] != 0:
-        raise OxenError("Could not read file for hashing", _capi.OXH_ERR_IO)
+    if status[0] != 0:  # get_hash_given_metadata(path, metadata)? (fs.rs:1616-1618)
+        raise file_error(path, status[0], oserr[0], int(metadata.st_size))
     return modified[0]
 
 
@@ -379,28 +470,27 @@ def hash_str(buffer: str) -> str:
     return hash_buffer(buffer.encode("utf-8"))
 
 
-def _hash_one_file(path) -> int:
-    digests, _, status = hash_files_128bit([path])
+def _hash_one_file(path, size_hint: Optional[int] = None) -> int:
+    digests, _, status, oserr = hash_files_with_errors_128bit([path])
     if status[0] != 0:
-        if not os.path.exists(path):
-            raise OxenError(f"util::hasher::hash_file_contents Could not open file {str(path)!r}", _capi.OXH_ERR_IO)
-        raise OxenError("Could not read file for hashing", _capi.OXH_ERR_IO)
+        raise file_error(path, status[0], oserr[0], size_hint)
     return digests[0]
 
 
 def get_hash_given_metadata(path, metadata: os.stat_result) -> int:
     """hasher.rs:56-65. Both size branches (one-shot < 1e9 B, streamed otherwise) give the same
     XXH3-128; here both go through the batched file path (K1 or, for files larger than a staging
-    slot, K1L)."""
-    del metadata  # the size decision only changes how the reference reads the file
-    return _hash_one_file(path)
+    slot, K1L). The size only picks which of hasher.rs's two open-failure messages an error gets."""
+    return _hash_one_file(path, int(metadata.st_size))
 
 
 def u128_hash_file_contents(path) -> int:
     """hasher.rs:102-112 (stats the file itself; a missing file is an error)."""
-    if not os.path.exists(path):
-        raise OxenError(f"Could not get metadata for {str(path)!r}", _capi.OXH_ERR_IO)
-    return _hash_one_file(path)
+    try:
+        size = os.stat(path).st_size
+    except OSError:
+        raise OxenError(f"Could not get metadata for {str(path)!r}", _capi.OXH_ERR_IO) from None
+    return _hash_one_file(path, size)
 
 
 def hash_file_contents(path) -> str:

@@ -116,10 +116,75 @@ std::string hash_buffer(const void* data, size_t len) { return format_hex(hash_b
 
 std::string hash_str(std::string_view s) { return hash_buffer(s.data(), s.size()); }
 
+// `{:?}` of a Rust str / Path: double quotes, \\ \" \n \r \t \0 escaped, other control characters as \u{..}
+std::string rust_str_debug(const std::string& s) {
+    std::string o = "\"";
+    for (unsigned char ch : s) {
+        switch (ch) {
+            case '"': o += "\\\""; break;
+            case '\\': o += "\\\\"; break;
+            case '\n': o += "\\n"; break;
+            case '\r': o += "\\r"; break;
+            case '\t': o += "\\t"; break;
+            case '\0': o += "\\0"; break;
+            default:
+                if (ch < 0x20 || ch == 0x7F) {
+                    char b[16];
+                    snprintf(b, sizeof b, "\\u{%x}", ch);
+                    o += b;
+                } else {
+                    o += (char)ch;
+                }
+        }
+    }
+    return o + "\"";
+}
+
+// `{:?}` of std::io::Error::from_raw_os_error(e): Os { code, kind, message }, the kind from Rust std's
+// decode_error_kind (sys/pal/unix)
+std::string rust_io_error_debug(int e) {
+    static const struct {
+        int code;
+        const char* kind;
+    } kinds[] = {
+        {E2BIG, "ArgumentListTooLong"}, {EADDRINUSE, "AddrInUse"}, {EADDRNOTAVAIL, "AddrNotAvailable"},
+        {EBUSY, "ResourceBusy"}, {ECONNABORTED, "ConnectionAborted"}, {ECONNREFUSED, "ConnectionRefused"},
+        {ECONNRESET, "ConnectionReset"}, {EDEADLK, "Deadlock"}, {EDQUOT, "FilesystemQuotaExceeded"},
+        {EEXIST, "AlreadyExists"}, {EFBIG, "FileTooLarge"}, {EHOSTUNREACH, "HostUnreachable"}, {EINTR, "Interrupted"},
+        {EINVAL, "InvalidInput"}, {EISDIR, "IsADirectory"}, {ELOOP, "FilesystemLoop"}, {ENOENT, "NotFound"},
+        {ENOMEM, "OutOfMemory"}, {ENOSPC, "StorageFull"}, {ENOSYS, "Unsupported"}, {EMLINK, "TooManyLinks"},
+        {ENAMETOOLONG, "InvalidFilename"}, {ENETDOWN, "NetworkDown"}, {ENETUNREACH, "NetworkUnreachable"},
+        {ENOTCONN, "NotConnected"}, {ENOTDIR, "NotADirectory"}, {ENOTEMPTY, "DirectoryNotEmpty"}, {EPIPE, "BrokenPipe"},
+        {EROFS, "ReadOnlyFilesystem"}, {ESPIPE, "NotSeekable"}, {ESTALE, "StaleNetworkFileHandle"},
+        {ETIMEDOUT, "TimedOut"}, {ETXTBSY, "ExecutableFileBusy"}, {EXDEV, "CrossesDevices"}, {EINPROGRESS, "InProgress"},
+        {EACCES, "PermissionDenied"}, {EPERM, "PermissionDenied"}, {EAGAIN, "WouldBlock"},
+    };
+    const char* kind = "Uncategorized";
+    for (const auto& k : kinds)
+        if (k.code == e) {
+            kind = k.kind;
+            break;
+        }
+    char buf[256];
+    const char* msg = strerror_r(e, buf, sizeof buf);  // GNU: returns the text
+    return "Os { code: " + std::to_string(e) + ", kind: " + kind + ", message: " + rust_str_debug(msg) + " }";
+}
+
+std::string file_error_text(const std::string& path, int status, int os_error, uint64_t size_hint) {
+    if (status == OXH_ERR_OPEN) {
+        const std::string p = rust_str_debug(path), err = rust_io_error_debug(os_error);
+        if (size_hint >= kLargeFileBytes) return "Could not open file " + p + " due to " + err;  // hasher.rs:151-154
+        return "util::hasher::hash_file_contents Could not open file " + p + " " + err;       // hasher.rs:141-145
+    }
+    if (status == OXH_ERR_NOMEM) return "Could not allocate the buffers to hash a large file";
+    return "Could not read file for hashing";  // hasher.rs:135-139, 161-165
+}
+
 namespace {
 // per-file outcomes of a hash_files-shaped call, with hasher.rs's error texts
 std::vector<FileHash> file_hashes(const std::vector<std::string>& paths, const std::vector<uint64_t>& out,
-                                  const std::vector<uint64_t>& sizes, const std::vector<int32_t>& status);
+                                  const std::vector<uint64_t>& sizes, const std::vector<int32_t>& status,
+                                  const std::vector<int32_t>& os_error, const std::vector<uint64_t>& size_hints);
 }  // namespace
 
 std::vector<FileHash> hash_files(const std::vector<std::string>& paths, oxh_ctx* ctx) {
@@ -128,9 +193,10 @@ std::vector<FileHash> hash_files(const std::vector<std::string>& paths, oxh_ctx*
     std::vector<const char*> cp(n);
     for (size_t i = 0; i < n; ++i) cp[i] = paths[i].c_str();
     std::vector<uint64_t> out(2 * n), sizes(n);
-    std::vector<int32_t> status(n);
-    check(oxh_hash_files(ctx, cp.data(), n, out.data(), sizes.data(), status.data()), "oxh_hash_files");
-    return file_hashes(paths, out, sizes, status);
+    std::vector<int32_t> status(n), oserr(n);
+    check(oxh_hash_files_ex(ctx, cp.data(), nullptr, n, out.data(), sizes.data(), status.data(), oserr.data(), nullptr, nullptr),
+          "oxh_hash_files_ex");
+    return file_hashes(paths, out, sizes, status, oserr, {});
 }
 
 ReaderPool::ReaderPool(int procs, const std::vector<int>& devices, int threads, uint64_t staging_bytes) {
@@ -148,27 +214,28 @@ std::vector<FileHash> ReaderPool::hash_files(const std::vector<std::string>& pat
     std::vector<const char*> cp(n);
     for (size_t i = 0; i < n; ++i) cp[i] = paths[i].c_str();
     std::vector<uint64_t> out(2 * n), sizes(n);
-    std::vector<int32_t> status(n);
-    check(oxh_pool_hash_files(p_, cp.data(), meta_sizes.empty() ? nullptr : meta_sizes.data(), n, out.data(), sizes.data(),
-                              status.data()),
-          "oxh_pool_hash_files");
-    return file_hashes(paths, out, sizes, status);
+    std::vector<int32_t> status(n), oserr(n);
+    check(oxh_pool_hash_files_ex(p_, cp.data(), meta_sizes.empty() ? nullptr : meta_sizes.data(), n, out.data(), sizes.data(),
+                                 status.data(), oserr.data()),
+          "oxh_pool_hash_files_ex");
+    return file_hashes(paths, out, sizes, status, oserr, meta_sizes);
 }
 
 namespace {
 std::vector<FileHash> file_hashes(const std::vector<std::string>& paths, const std::vector<uint64_t>& out,
-                                  const std::vector<uint64_t>& sizes, const std::vector<int32_t>& status) {
+                                  const std::vector<uint64_t>& sizes, const std::vector<int32_t>& status,
+                                  const std::vector<int32_t>& os_error, const std::vector<uint64_t>& size_hints) {
     const size_t n = paths.size();
     std::vector<FileHash> r(n);
     for (size_t i = 0; i < n; ++i) {
+        r[i].code = status[i];
         if (status[i] == OXH_OK) {
             r[i].ok = true;
             r[i].hash = to_u128(out[2 * i], out[2 * i + 1]);
             r[i].size = sizes[i];
-        } else if (access(paths[i].c_str(), F_OK) != 0) {  // File::open failed (hasher.rs:142-146)
-            r[i].error = "util::hasher::hash_file_contents Could not open file \"" + paths[i] + "\"";
-        } else {  // read_to_end failed (hasher.rs:136-139)
-            r[i].error = "Could not read file for hashing";
+        } else {  // File::open (OXH_ERR_OPEN) or the read (OXH_ERR_IO) failed, with the errno of its io::Error
+            r[i].os_error = os_error[i];
+            r[i].error = file_error_text(paths[i], status[i], os_error[i], size_hints.empty() ? 0 : size_hints[i]);
         }
     }
     return r;
@@ -176,9 +243,13 @@ std::vector<FileHash> file_hashes(const std::vector<std::string>& paths, const s
 }  // namespace
 
 namespace {
-u128 hash_one_file(const std::string& path) {
-    const std::vector<FileHash> r = hash_files({path});
-    if (!r[0].ok) throw OxenError::basic_str(r[0].error, OXH_ERR_IO);
+u128 hash_one_file(const std::string& path, uint64_t size_hint) {
+    std::vector<FileHash> r = hash_files({path});
+    if (!r[0].ok) {
+        // the size picks hasher.rs's one-shot or streamed branch, and so which open message
+        r[0].error = file_error_text(path, r[0].code, r[0].os_error, size_hint);
+        throw OxenError::basic_str(r[0].error, r[0].code);
+    }
     return r[0].hash;
 }
 }  // namespace
@@ -186,15 +257,14 @@ u128 hash_one_file(const std::string& path) {
 // Both size branches (one-shot below 1e9 B, 4 KiB streaming above) give the same XXH3-128; here
 // both go through the batched file path (K1, or the K1L piece pipeline above a staging slot).
 u128 get_hash_given_metadata(const std::string& path, const struct stat& metadata) {
-    (void)metadata;
-    return hash_one_file(path);
+    return hash_one_file(path, (uint64_t)metadata.st_size);
 }
 
 u128 u128_hash_file_contents(const std::string& path) {
     struct stat sb;
     if (stat(path.c_str(), &sb) != 0)  // util::fs::metadata(path)? (hasher.rs:105)
         throw OxenError::basic_str("Could not get metadata for \"" + path + "\"", OXH_ERR_IO);
-    return hash_one_file(path);
+    return hash_one_file(path, (uint64_t)sb.st_size);
 }
 
 std::string hash_file_contents(const std::string& path) { return format_hex(u128_hash_file_contents(path)); }
@@ -259,7 +329,7 @@ std::vector<Modified> classify_modified_batch(const std::vector<TrackedFile>& fi
     std::vector<const char*> cp(n);
     std::vector<uint64_t> sizes(n), node_bytes(n), node_hashes(2 * n), nmh(2 * n), fmh(2 * n);
     std::vector<uint8_t> mtime(n), modified(n), nmp(n), fk(n);
-    std::vector<int32_t> status(n);
+    std::vector<int32_t> status(n), oserr(n);
     for (size_t i = 0; i < n; ++i) {
         const TrackedFile& f = files[i];
         cp[i] = f.path.c_str();
@@ -275,9 +345,9 @@ std::vector<Modified> classify_modified_batch(const std::vector<TrackedFile>& fi
         fmh[2 * i] = (uint64_t)f.file_metadata.hash, fmh[2 * i + 1] = (uint64_t)(f.file_metadata.hash >> 64);
     }
     uint64_t hashed = 0;
-    check(oxh_files_modified(ctx, cp.data(), sizes.data(), node_bytes.data(), mtime.data(), node_hashes.data(), nmp.data(),
-                             nmh.data(), fk.data(), fmh.data(), n, modified.data(), status.data(), &hashed),
-          "oxh_files_modified");
+    check(oxh_files_modified_ex(ctx, cp.data(), sizes.data(), node_bytes.data(), mtime.data(), node_hashes.data(), nmp.data(),
+                                nmh.data(), fk.data(), fmh.data(), n, modified.data(), status.data(), oserr.data(), &hashed),
+          "oxh_files_modified_ex");
     if (n_hashed) *n_hashed = hashed;
     std::vector<Modified> r(n);
     for (size_t i = 0; i < n; ++i) {
@@ -286,9 +356,9 @@ std::vector<Modified> classify_modified_batch(const std::vector<TrackedFile>& fi
         if (status[i] == OXH_ERR_META) {
             r[i].ok = false;
             r[i].error = files[i].file_metadata.error.empty() ? "could not compute file metadata" : files[i].file_metadata.error;
-        } else if (status[i] != OXH_OK) {
+        } else if (status[i] != OXH_OK) {  // get_hash_given_metadata(path, metadata)? (fs.rs:1616-1618)
             r[i].ok = false;
-            r[i].error = "Could not read file for hashing";  // hasher.rs:136-139
+            r[i].error = hasher::file_error_text(files[i].path, status[i], oserr[i], files[i].size);
         }
     }
     return r;
@@ -511,12 +581,14 @@ std::vector<uint64_t> LocalVersionStore::list_version_chunks(const std::string& 
     if (!d) throw OxenError::basic_str("Could not read " + dir + ": " + strerror(errno), OXH_ERR_IO);
     std::vector<uint64_t> out;
     while (struct dirent* e = readdir(d)) {
+        // name.parse::<u64>(): an optional '+' then ASCII digits, below 2^64
         const std::string name = e->d_name;
-        if (name.empty() || name.find_first_not_of("0123456789") != std::string::npos) continue;  // u64 names only
-        struct stat sb;
-        if (stat((dir + "/" + name).c_str(), &sb) != 0 || !S_ISDIR(sb.st_mode)) continue;
+        const std::string digits = !name.empty() && name[0] == '+' ? name.substr(1) : name;
+        if (digits.empty() || digits.find_first_not_of("0123456789") != std::string::npos) continue;
+        struct stat sb;  // DirEntry::file_type(): the entry itself, a symlink is not a directory
+        if (lstat((dir + "/" + name).c_str(), &sb) != 0 || !S_ISDIR(sb.st_mode)) continue;
         errno = 0;
-        const unsigned long long v = strtoull(name.c_str(), nullptr, 10);
+        const unsigned long long v = strtoull(digits.c_str(), nullptr, 10);
         if (errno == 0) out.push_back(v);
     }
     closedir(d);

@@ -89,7 +89,18 @@ struct FileHash {
     u128 hash = 0;
     uint64_t size = 0;
     std::string error;
+    int code = 0;      // OXH_OK, OXH_ERR_OPEN (File::open failed), OXH_ERR_IO (the read failed), OXH_ERR_NOMEM
+    int os_error = 0;  // the errno of the failed open / read
 };
+// hasher.rs picks its one-shot (< 1e9 B) or streamed branch by the file's size (:56-65, 106)
+constexpr uint64_t kLargeFileBytes = 1000000000ull;
+// The text of the OxenError hasher.rs returns for a file that could not be hashed: File::open failed
+// (OXH_ERR_OPEN: "util::hasher::hash_file_contents Could not open file {path:?} {err:?}", or "Could not
+// open file {path:?} due to {err:?}" on the streamed branch), else "Could not read file for hashing".
+std::string file_error_text(const std::string& path, int status, int os_error, uint64_t size_hint);
+// Rust `{:?}` of a str / Path, and of std::io::Error::from_raw_os_error(e)
+std::string rust_str_debug(const std::string& s);
+std::string rust_io_error_debug(int e);
 std::vector<FileHash> hash_files(const std::vector<std::string>& paths, oxh_ctx* ctx = nullptr);
 
 // The add loop's hash stage over helper processes (oxh_pool_*): the list split into contiguous

@@ -10,7 +10,7 @@ one-process floor; the pool runs P helper processes, each with its own context, 
 contiguous share of the list. Helper p uses devices[p % len(devices)]: on a node with several GPUs
 every GPU gets its own share over its own PCIe link.
 
-This module is a thin ctypes mirror; a Rust liboxen binds the same four functions.
+This module is a thin ctypes mirror; a Rust liboxen binds the same functions.
 """
 from __future__ import annotations
 
@@ -57,14 +57,17 @@ class ShardedFileHasher:
         _capi.check(_capi.lib().oxh_pool_size(self._h, ctypes.byref(n), pids), "oxh_pool_size")
         return list(pids[: n.value])
 
-    def hash_files_packed(self, blob: np.ndarray, offsets: np.ndarray, meta_sizes: Optional[np.ndarray] = None):
-        """Paths packed by `pack_paths`. Returns (out (n, 2) uint64 lo/hi, sizes, status)."""
+    def hash_files_packed(self, blob: np.ndarray, offsets: np.ndarray, meta_sizes: Optional[np.ndarray] = None,
+                          with_errors: bool = False):
+        """Paths packed by `pack_paths`. Returns (out (n, 2) uint64 lo/hi, sizes, status), plus os_error
+        (the errno of each failed open / read, oxh_pool_hash_files_ex) when with_errors."""
         n = len(offsets)
         out = np.zeros((n, 2), dtype=np.uint64)
         sizes = np.zeros(n, dtype=np.uint64)
         status = np.zeros(n, dtype=np.int32)
+        oserr = np.zeros(n, dtype=np.int32)
         if n == 0:
-            return out, sizes, status
+            return (out, sizes, status, oserr) if with_errors else (out, sizes, status)
         if self._h is None:
             raise _capi.OxenError("pool is closed", _capi.OXH_ERR_INVALID)
         blob = np.ascontiguousarray(blob, dtype=np.uint8)
@@ -72,16 +75,17 @@ class ShardedFileHasher:
         meta = None if meta_sizes is None else np.ascontiguousarray(meta_sizes, dtype=np.uint64)
         if meta is not None and len(meta) != n:
             raise _capi.OxenError("paths and meta_sizes differ in length", _capi.OXH_ERR_INVALID)
-        _capi.check(_capi.lib().oxh_pool_hash_files(self._h, ptrs.ctypes.data_as(ctypes.POINTER(ctypes.c_char_p)),
-                                                    None if meta is None else meta.ctypes.data, n,
-                                                    out.ctypes.data_as(_capi._u64p), sizes.ctypes.data_as(_capi._u64p),
-                                                    status.ctypes.data_as(_capi._i32p)), "oxh_pool_hash_files")
-        return out, sizes, status
+        _capi.check(_capi.lib().oxh_pool_hash_files_ex(self._h, ptrs.ctypes.data_as(ctypes.POINTER(ctypes.c_char_p)),
+                                                       None if meta is None else meta.ctypes.data, n,
+                                                       out.ctypes.data_as(_capi._u64p), sizes.ctypes.data_as(_capi._u64p),
+                                                       status.ctypes.data_as(_capi._i32p),
+                                                       oserr.ctypes.data_as(_capi._i32p)), "oxh_pool_hash_files_ex")
+        return (out, sizes, status, oserr) if with_errors else (out, sizes, status)
 
-    def hash_files(self, paths: Sequence, meta_sizes: Optional[Sequence[int]] = None):
+    def hash_files(self, paths: Sequence, meta_sizes: Optional[Sequence[int]] = None, with_errors: bool = False):
         blob, offs = pack_paths(paths)
         meta = None if meta_sizes is None else np.ascontiguousarray(meta_sizes, dtype=np.uint64)
-        return self.hash_files_packed(blob, offs, meta)
+        return self.hash_files_packed(blob, offs, meta, with_errors)
 
     def close(self) -> None:
         if getattr(self, "_h", None):

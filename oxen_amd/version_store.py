@@ -179,6 +179,17 @@ def _parse_hash(h: str) -> int:
     return v
 
 
+def parse_u64(name: str):
+    """`name.parse::<u64>()` (Rust core's from_str_radix): an optional '+' then ASCII digits only, below
+    2**64; anything else (a '-', whitespace, '_', non-ASCII digits, which Python's int() would accept)
+    is None."""
+    digits = name[1:] if name.startswith("+") else name
+    if not digits or not digits.isascii() or not digits.isdigit():
+        return None
+    v = int(digits)
+    return v if v < (1 << 64) else None
+
+
 class LocalVersionStore:
     """storage/local.rs: version paths and the verified content-addressed writes."""
 
@@ -224,11 +235,11 @@ class LocalVersionStore:
         out = []
         with os.scandir(self.version_chunks_dir(hash)) as it:
             for e in it:
-                if e.is_dir():
-                    try:
-                        out.append(int(e.name))
-                    except ValueError:
-                        pass
+                # DirEntry::file_type() does not follow symlinks; the name must parse as Rust's u64
+                if e.is_dir(follow_symlinks=False):
+                    v = parse_u64(e.name)
+                    if v is not None:
+                        out.append(v)
         return sorted(out)
 
     def combine_version_chunks(self, hash: str) -> None:  # :384-413

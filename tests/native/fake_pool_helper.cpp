@@ -3,13 +3,17 @@
 // spawning, the shared region and its growth, share splitting, per-call sequence numbers, per-file
 // statuses, helper death -- are tested on any host (tests/test_procpool.py, OXH_HELPER=<this>).
 // Test infrastructure only: it computes no digest; "out" is (size, index of the file in the call)
-// so the test can check that every item landed in its own slot.
+// so the test can check that every item landed in its own slot. A missing path gets OXH_ERR_OPEN (7)
+// with its stat errno, a directory OXH_ERR_IO (3) with EISDIR, like the real helper's engine.
+// OXH_FAKE_STALL_S=s: every call's reply is held back s seconds (the pool's deadline test).
+// Like the real helper it watches its socket and getppid() instead of PR_SET_PDEATHSIG.
+#include <errno.h>
+#include <poll.h>
 #include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
-#include <sys/prctl.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -31,11 +35,14 @@ static bool reply(int sock, uint64_t seq, int rc, const char* msg) {
 }
 
 int main(int argc, char** argv) {
-    prctl(PR_SET_PDEATHSIG, SIGKILL);
     const int sock = oxh_pool_wire::kSockFd, mem = oxh_pool_wire::kMemFd;
     int device = 0;
-    for (int i = 1; i < argc; ++i)
+    long ppid = 0;
+    for (int i = 1; i < argc; ++i) {
         if (strncmp(argv[i], "--device=", 9) == 0) device = atoi(argv[i] + 9);
+        if (strncmp(argv[i], "--ppid=", 7) == 0) ppid = atol(argv[i] + 7);
+    }
+    const int stall = getenv("OXH_FAKE_STALL_S") ? atoi(getenv("OXH_FAKE_STALL_S")) : 0;
     // OXH_FAKE_FAIL_DEVICE=d: the helper on device d reports a start-up failure (status 5)
     const char* fd = getenv("OXH_FAKE_FAIL_DEVICE");
     if (fd && atoi(fd) == device) {
@@ -46,6 +53,13 @@ int main(int argc, char** argv) {
     uint8_t* map = nullptr;
     uint64_t cap = 0;
     for (;;) {
+        pollfd pf{sock, POLLIN, 0};
+        const int ready = poll(&pf, 1, 1000);
+        if (ready < 0 && errno != EINTR) break;
+        if (ready <= 0) {
+            if (ppid && getppid() != (pid_t)ppid) break;  // the parent process is gone
+            continue;
+        }
         PoolReq q{};
         if (recv(sock, &q, sizeof q, 0) != (ssize_t)sizeof q || q.quit) break;
         if (q.cap != cap) {
@@ -64,14 +78,18 @@ int main(int argc, char** argv) {
         uint64_t* out = (uint64_t*)(map + q.off_out);
         uint64_t* sizes = (uint64_t*)(map + q.off_sizes);
         int32_t* status = (int32_t*)(map + q.off_status);
+        int32_t* os_error = (int32_t*)(map + q.off_oserr);
         for (uint64_t i = q.lo; i < q.hi; ++i) {
             struct stat sb;
-            const bool ok = stat(blob + offs[i], &sb) == 0 && S_ISREG(sb.st_mode);
-            status[i] = ok ? 0 : 3;
+            const bool found = stat(blob + offs[i], &sb) == 0;
+            const bool ok = found && S_ISREG(sb.st_mode);
+            status[i] = ok ? 0 : found ? 3 : 7;
+            os_error[i] = ok ? 0 : found ? EISDIR : errno;
             sizes[i] = ok ? (uint64_t)sb.st_size : 0;
             out[2 * i] = ok ? (uint64_t)sb.st_size : 0;
             out[2 * i + 1] = ok ? i + (meta ? (1ull << 40) : 0) : 0;
         }
+        if (stall) sleep((unsigned)stall);
         if (!reply(sock, q.seq, 0, "")) break;
     }
     return 0;

@@ -6,6 +6,7 @@
 // Built by oxen_amd/build.py (g++ against liboxen_hasher.so + liboxen_hash.so); run by
 // tests/test_native_mirror.py on the GPU box. argv[1] = tests/golden. Exit status 0 = all passed.
 #include <dirent.h>
+#include <errno.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -41,6 +42,18 @@ static bool throws_oxen(F f, const char* needle = nullptr) {
         f();
     } catch (const OxenError& e) {
         return !needle || strstr(e.what(), needle) != nullptr;
+    }
+    return false;
+}
+
+// the exact message
+template <class F>
+static bool throws_oxen(F f, const std::string& exact) {
+    try {
+        f();
+    } catch (const OxenError& e) {
+        if (exact != e.what()) fprintf(stderr, "  message: %s\n  expected: %s\n", e.what(), exact.c_str());
+        return exact == e.what();
     }
     return false;
 }
@@ -168,15 +181,26 @@ static void file_errors(const std::string& golden) {
     const std::string missing = golden + "/no-such-file";
     CHECK(throws_oxen([&] { hasher::hash_file_contents(missing); }, "Could not get metadata"));
     struct stat sb {};
-    CHECK(throws_oxen([&] { hasher::get_hash_given_metadata(missing, sb); }, "Could not open file"));
+    // hasher.rs:141-145: File::open's io::Error in its Debug form (the errno crosses the ABI)
+    const std::string enoent = "Os { code: 2, kind: NotFound, message: \"No such file or directory\" }";
+    CHECK(throws_oxen([&] { hasher::get_hash_given_metadata(missing, sb); },
+                      "util::hasher::hash_file_contents Could not open file \"" + missing + "\" " + enoent));
+    struct stat big {};
+    big.st_size = 2000000000;  // the streamed branch's message (hasher.rs:151-154)
+    CHECK(throws_oxen([&] { hasher::get_hash_given_metadata(missing, big); },
+                      "Could not open file \"" + missing + "\" due to " + enoent));
     CHECK(throws_oxen([&] { hasher::get_hash_given_metadata(golden, sb); }, "Could not read file for hashing"));
+    CHECK(hasher::rust_str_debug("a\"b\\c\nd\x01") == "\"a\\\"b\\\\c\\nd\\u{1}\"");
+    CHECK(hasher::rust_io_error_debug(40) == "Os { code: 40, kind: FilesystemLoop, message: \"Too many levels of symbolic links\" }");
+    CHECK(hasher::rust_io_error_debug(24) == "Os { code: 24, kind: Uncategorized, message: \"Too many open files\" }");
     std::vector<int> sleeps;
     CHECK(throws_oxen([&] { hasher::hash_file_contents_with_retry(missing, 5, [&](int s) { sleeps.push_back(s); }); }));
     CHECK((sleeps == std::vector<int>{2, 4, 8, 16, 32, 64}));  // hasher.rs:32-54
     const auto r = hasher::hash_files({golden + "/data_test/text/hello.txt", missing, golden});
     CHECK(r.size() == 3 && r[0].ok && r[0].size == 5 && !r[1].ok && !r[2].ok);
-    CHECK(r[1].error.find("Could not open file") != std::string::npos);
-    CHECK(r[2].error == "Could not read file for hashing");
+    CHECK(r[1].error == "util::hasher::hash_file_contents Could not open file \"" + missing + "\" " + enoent);
+    CHECK(r[1].code == OXH_ERR_OPEN && r[1].os_error == ENOENT);
+    CHECK(r[2].error == "Could not read file for hashing" && r[2].code == OXH_ERR_IO && r[2].os_error == EISDIR);
 }
 
 // The reader-process pool (oxh_pool_*) through liboxen::util::hasher::ReaderPool: the same outcomes
@@ -272,11 +296,13 @@ static void modified_check(const std::string& golden) {
     CHECK(r[1].ok && r[1].modified);
     CHECK(r[2].ok && !r[2].modified);
     CHECK(r[3].ok && r[3].modified);
-    CHECK(!r[4].ok && !r[4].modified && r[4].error == "Could not read file for hashing");
+    CHECK(!r[4].ok && !r[4].modified && r[4].code == OXH_ERR_OPEN &&
+          r[4].error == "util::hasher::hash_file_contents Could not open file \"" + golden +
+                            "/no/such/file\" Os { code: 2, kind: NotFound, message: \"No such file or directory\" }");
     struct stat sb;
     CHECK(stat(hello.c_str(), &sb) == 0 && !fs::classify_modified_from_node_with_metadata(hello, 5, h, sb, false));
     CHECK(throws_oxen([&] { fs::classify_modified_from_node_with_metadata(golden + "/no/such/file", (uint64_t)sb.st_size, h, sb, false); },
-                      "Could not read file for hashing"));
+                      ("Could not open file \"" + golden + "/no/such/file\"").c_str()));
 
     // the metadata-hash step (fs.rs:1599-1614): hello.txt is MetadataText {1 line, 5 chars}
     const u128 mh = liboxen::util::hasher::get_metadata_hash(std::string("{\"text\":{\"num_lines\":1,\"num_chars\":5}}"));
@@ -411,6 +437,12 @@ static void verified_publish(const std::string& scratch) {
     store2.store_version_chunk(wrong, 0, data.data(), data.size());
     CHECK(throws_oxen([&] { store2.combine_version_chunks(wrong); }, "Hash mismatch"));
     CHECK(!store2.version_exists(wrong) && store2.list_version_chunks(wrong) == std::vector<uint64_t>{0});
+    // names parse as Rust's u64 (an optional '+', ASCII digits, < 2^64); a symlink is not a chunk dir
+    const std::string cdir = store2.version_chunks_dir(wrong);
+    for (const char* name : {"+5", "-1", "1_0", " 7", "007", "18446744073709551616", "x"})
+        CHECK(mkdir((cdir + "/" + name).c_str(), 0755) == 0);
+    CHECK(symlink((cdir + "/0").c_str(), (cdir + "/99").c_str()) == 0);
+    CHECK((store2.list_version_chunks(wrong) == std::vector<uint64_t>{0, 5, 7}));
 }
 
 int main(int argc, char** argv) {

@@ -29,3 +29,66 @@ def test_k1_items_over_a_descriptor_window(cuda, oracle_lib, lens):
         assert np.array_equal(got, want), mode
     del da
     torch.cuda.empty_cache()
+
+
+def test_k1l_default_pieces_device(cuda, oracle_lib, monkeypatch):
+    """K1L as it ships -- OXH_BIG_PIECE_MIB unset (1 GiB pieces) -- over buffers
+    larger than one piece: 2 GiB + 4 097 B at a misaligned start (two full pieces and a last piece of
+    4 097 B) and 1 GiB - 1 B (one piece), through oxh_xxh3_128_large_batch_device."""
+    import torch
+
+    from oxen_amd.device import fill_splitmix, large_digests_device
+
+    monkeypatch.delenv("OXH_BIG_PIECE_MIB", raising=False)
+    sizes = [2 * GIB + 4097, GIB - 1]
+    starts = [5, 0]
+    bufs, views = [], []
+    for i, (n, s) in enumerate(zip(sizes, starts)):
+        b = torch.empty(n + 64, dtype=torch.uint8, device=cuda)
+        fill_splitmix(b, 900 + i)
+        bufs.append(b)
+        views.append(b[s:s + n])
+    got = large_digests_device(views, sizes).cpu().numpy().view(np.uint64).reshape(-1, 2)
+    torch.cuda.synchronize()
+    for i, (b, n, s) in enumerate(zip(bufs, sizes, starts)):
+        host = b.cpu().numpy()
+        want = oracle_lib.batch(host, np.array([s], dtype=np.uint64), np.array([n], dtype=np.uint64), 8)
+        assert np.array_equal(got[i], want[0]), (i, n)
+        del host
+    del bufs, views
+    torch.cuda.empty_cache()
+
+
+def test_k1l_default_pieces_file(cuda, oracle_lib, tmp_path, monkeypatch):
+    """The C5 whole-file digest path as it ships (hasher.rs:150-174's branch): one 2.5 GiB file --
+    sparse, with written regions at the start, across both 1 GiB piece boundaries and at the end --
+    through oxh_hash_files (three 1 GiB-piece rounds of the large-file pipeline) and oxh_add_files
+    (the same pieces also streamed to the blob's temp, renamed once the digest is known), checked
+    against the oracle's read of the file and of the published blob."""
+    import os
+
+    from oxen_amd import hasher
+    from oxen_amd.workloads import splitmix_bytes
+
+    monkeypatch.delenv("OXH_BIG_PIECE_MIB", raising=False)
+    size = 5 * GIB // 2 + 333
+    p = tmp_path / "big.parquet"
+    with open(p, "wb") as fh:
+        fh.truncate(size)
+        for off in (0, GIB - 2000, GIB + 77, 2 * GIB - 4096, size - 5000):
+            fh.seek(off)
+            fh.write(splitmix_bytes(off, 0, 4096).tobytes()[: size - off])
+    out, sizes, status = oracle_lib.hash_files([str(p)], threads=8)
+    want_int = (int(out[0, 1]) << 64) | int(out[0, 0])
+    assert int(status[0]) == 0 and int(sizes[0]) == size
+    d, sz, st = hasher.hash_files_128bit([str(p)])
+    assert st == [0] and sz == [size] and d == [want_int]
+    root = tmp_path / "versions"
+    root.mkdir()
+    d2, sz2, st2, stored = hasher.add_files([str(p)], str(root))
+    assert st2 == [0] and d2 == [want_int] and stored == [True]
+    blob = hasher.version_path(str(root), want_int)
+    out_b, sizes_b, status_b = oracle_lib.hash_files([blob], threads=8)
+    assert int(status_b[0]) == 0 and int(sizes_b[0]) == size
+    assert (int(out_b[0, 1]) << 64) | int(out_b[0, 0]) == want_int
+    os.remove(blob)

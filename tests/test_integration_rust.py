@@ -1,0 +1,131 @@
+"""The Rust `extern "C"` block a liboxen maintainer would add declares exactly what
+include/oxen_hash.h exports, with the same C types spelled in Rust (VERDICT r03 missing #1).
+
+There is no Rust toolchain in this image, so the block is checked mechanically: every header function
+is declared in the block (or named on its `test-only` line), with the same arity, the same parameter
+and return types under the C -> Rust mapping below, and every `OXH_*` constant the block defines has
+the header's value. A header change that the binding does not follow fails here.
+"""
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "oxen_hash.h")
+INTEGRATION = os.path.join(ROOT, "INTEGRATION.md")
+
+C_BASE = {
+    "int": "c_int", "int32_t": "i32", "uint32_t": "u32", "uint64_t": "u64", "uint8_t": "u8", "char": "c_char",
+    "void": "c_void", "oxh_ctx": "OxhCtx", "oxh_pool": "OxhPool", "oxh_xxh3_stream": "OxhStream",
+}
+
+
+def c_to_rust(ctype: str) -> str:
+    """`const char* const*` -> `*const *const c_char`; `uint64_t*` -> `*mut u64`; `void` -> `()`."""
+    toks = re.findall(r"\*|const|\w+", ctype)
+    base_const = False
+    base = None
+    i = 0
+    while i < len(toks) and toks[i] != "*":
+        if toks[i] == "const":
+            base_const = True
+        else:
+            base = toks[i]
+        i += 1
+    assert base in C_BASE, (ctype, base)
+    rust = C_BASE[base]
+    if i == len(toks):
+        return "()" if base == "void" else rust
+    pointee_const = base_const
+    while i < len(toks):
+        assert toks[i] == "*", ctype
+        rust = ("*const " if pointee_const else "*mut ") + rust
+        i += 1
+        pointee_const = i < len(toks) and toks[i] == "const"
+        if pointee_const:
+            i += 1
+    return rust
+
+
+def header_functions() -> dict:
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
+    text = re.sub(r"//[^\n]*", " ", text)
+    text = re.sub(r"^\s*#[^\n]*", " ", text, flags=re.M)
+    out = {}
+    for m in re.finditer(r"([A-Za-z_][\w\s\*]*?)\b(oxh_\w+)\s*\(([^)]*)\)\s*;", text):
+        ret, name, params = " ".join(m.group(1).split()), m.group(2), " ".join(m.group(3).split())
+        ret = ret.replace("extern \"C\"", "").strip()
+        args = []
+        if params and params != "void":
+            for p in params.split(","):
+                p = p.strip()
+                pname = re.findall(r"(\w+)$", p)[0]
+                args.append(c_to_rust(p[: -len(pname)]))
+        out[name] = (c_to_rust(ret), args)
+    return out
+
+
+def rust_block() -> str:
+    text = open(INTEGRATION).read()
+    sec = text[text.index("## 1. `extern \"C\"` declarations"): text.index("## 2. Call sites")]
+    return sec[sec.index("```rust") + 7: sec.index("```", sec.index("```rust") + 7)]
+
+
+def rust_functions(block: str) -> dict:
+    ext = block[block.index('extern "C" {'):]
+    ext = ext[: ext.index("\n}\n")]
+    ext = re.sub(r"//[^\n]*", " ", ext)
+    out = {}
+    for m in re.finditer(r"\bfn\s+(oxh_\w+)\s*\(([^)]*)\)\s*(?:->\s*([^;]+))?;", ext, flags=re.S):
+        name, params, ret = m.group(1), " ".join(m.group(2).split()), m.group(3)
+        args = []
+        for p in [q for q in params.split(",") if q.strip()]:
+            _, t = p.split(":", 1)
+            args.append(" ".join(t.split()))
+        assert name not in out, f"{name} declared twice"
+        out[name] = (" ".join(ret.split()) if ret else "()", args)
+    return out
+
+
+def test_type_mapping_itself():
+    assert c_to_rust("const char* const*") == "*const *const c_char"
+    assert c_to_rust("oxh_ctx**") == "*mut *mut OxhCtx"
+    assert c_to_rust("const void* const*") == "*const *const c_void"
+    assert c_to_rust("const uint64_t*") == "*const u64"
+    assert c_to_rust("int32_t*") == "*mut i32"
+    assert c_to_rust("void*") == "*mut c_void"
+    assert c_to_rust("uint64_t") == "u64"
+
+
+def test_rust_block_matches_the_header():
+    hdr = header_functions()
+    assert "oxh_xxh3_128_batch_device" in hdr and len(hdr) >= 40, sorted(hdr)
+    block = rust_block()
+    rs = rust_functions(block)
+    test_only = set(re.search(r"//\s*test-only, not bound:\s*([\w, ]+)", block).group(1).replace(" ", "").split(","))
+    assert test_only == {"oxh_fill_splitmix", "oxh_set_kernel_variant"}, test_only
+    assert not (test_only & set(rs)), test_only & set(rs)
+    missing = sorted(set(hdr) - set(rs) - test_only)
+    assert not missing, f"header exports not bound in INTEGRATION.md: {missing}"
+    extra = sorted(set(rs) - set(hdr))
+    assert not extra, f"bound but not in the header: {extra}"
+    for name, (ret, args) in rs.items():
+        hret, hargs = hdr[name]
+        assert len(args) == len(hargs), (name, args, hargs)
+        assert ret == hret, (name, ret, hret)
+        for k, (a, h) in enumerate(zip(args, hargs)):
+            assert a == h, f"{name} parameter {k}: Rust {a!r}, header {h!r}"
+
+
+def test_rust_constants_match_the_header():
+    hdr = open(HEADER).read()
+    defines = {m.group(1): int(m.group(2), 0) for m in
+               re.finditer(r"^#define\s+(OXH_[A-Z0-9_]+)\s+(-?(?:0x)?[0-9A-Fa-f]+)(?:ull)?\b", hdr, re.M)}
+    consts = {m.group(1): int(m.group(2)) for m in
+              re.finditer(r"pub const (OXH_[A-Z0-9_]+):\s*\w+\s*=\s*(\d+);", rust_block())}
+    assert {"OXH_OK", "OXH_ERR_IO", "OXH_ERR_OPEN", "OXH_ABI_VERSION"} <= set(consts)
+    status_codes = {k for k in defines if k.startswith("OXH_ERR_")}
+    assert status_codes <= set(consts), status_codes - set(consts)
+    for k, v in consts.items():
+        assert k in defines, k
+        assert defines[k] == v, (k, v, defines[k])

@@ -66,7 +66,7 @@ def _fake_want(paths, meta):
     sizes = [os.path.getsize(p) if os.path.isfile(p) else None for p in paths]
     out = np.array([[s or 0, (i + (1 << 40 if meta else 0)) if s is not None else 0] for i, s in enumerate(sizes)],
                    dtype=np.uint64).reshape(-1, 2)
-    return out, np.array([s or 0 for s in sizes], dtype=np.uint64), np.array([0 if s is not None else 3 for s in sizes], dtype=np.int32)
+    return out, np.array([s or 0 for s in sizes], dtype=np.uint64), np.array([0 if s is not None else 7 for s in sizes], dtype=np.int32)
 
 
 @pytest.mark.parametrize("procs,devices", [(1, (0,)), (3, (0, 1)), (4, (2, 3, 5))])
@@ -122,6 +122,71 @@ def test_pool_fake_helper_concurrency_and_death(fake_helper, tmp_path):
         assert e.value.code == _capi.OXH_ERR_NODEVICE and "no device" in str(e.value)
     finally:
         del os.environ["OXH_FAKE_FAIL_DEVICE"]
+
+
+def test_pool_created_on_a_thread_that_exits(fake_helper, tmp_path):
+    """a pool created on a short-lived thread (a tokio spawn_blocking worker, a Python
+    worker thread) keeps its helpers after that thread exits: the helpers watch their socket and
+    their parent PROCESS, not the creating thread (PR_SET_PDEATHSIG would have killed them)."""
+    import threading
+    import time
+
+    from oxen_amd.procpool import ShardedFileHasher
+
+    paths = _tree(tmp_path, 50)
+    box = {}
+    t = threading.Thread(target=lambda: box.setdefault("pool", ShardedFileHasher(procs=2, threads=1)))
+    t.start()
+    t.join()
+    pool = box["pool"]
+    try:
+        time.sleep(1.5)  # a helper killed by its creator thread's exit would be gone by now
+        for pid in pool.pids():
+            os.kill(pid, 0)  # still alive
+        got = pool.hash_files(paths)
+        for g, w in zip(got, _fake_want(paths, False)):
+            assert np.array_equal(g, w)
+    finally:
+        pool.close()
+
+
+def test_pool_reports_open_and_read_errors(fake_helper, tmp_path):
+    """oxh_pool_hash_files_ex carries each failure's errno across the process boundary: a missing path
+    is an open failure (OXH_ERR_OPEN, ENOENT), a directory a read failure (OXH_ERR_IO, EISDIR)."""
+    import errno
+
+    from oxen_amd import _capi
+    from oxen_amd.procpool import ShardedFileHasher
+
+    f = tmp_path / "ok.bin"
+    f.write_bytes(b"x" * 10)
+    (tmp_path / "adir").mkdir()
+    paths = [str(f), str(tmp_path / "nope"), str(tmp_path / "adir")]
+    with ShardedFileHasher(procs=2, threads=1) as pool:
+        out, sizes, status, oserr = pool.hash_files(paths, with_errors=True)
+    assert status.tolist() == [0, _capi.OXH_ERR_OPEN, _capi.OXH_ERR_IO]
+    assert oserr.tolist() == [0, errno.ENOENT, errno.EISDIR]
+
+
+def test_pool_call_deadline(fake_helper, tmp_path, monkeypatch):
+    """a helper that stops answering no longer hangs the caller forever when a deadline is
+    set (OXH_POOL_CALL_LIMIT_S): the call fails with OXH_ERR_HIP and the pool is marked unusable."""
+    import time
+
+    from oxen_amd import _capi
+    from oxen_amd.procpool import ShardedFileHasher
+
+    paths = _tree(tmp_path, 20)
+    monkeypatch.setenv("OXH_FAKE_STALL_S", "30")
+    monkeypatch.setenv("OXH_POOL_CALL_LIMIT_S", "2")
+    with ShardedFileHasher(procs=1, threads=1) as pool:
+        t0 = time.monotonic()
+        with pytest.raises(_capi.OxenError) as e:
+            pool.hash_files(paths)
+        assert e.value.code == _capi.OXH_ERR_HIP
+        assert time.monotonic() - t0 < 15
+        with pytest.raises(_capi.OxenError, match="unusable"):
+            pool.hash_files(paths)
 
 
 def test_pool_rejects_bad_arguments(built_lib, monkeypatch):

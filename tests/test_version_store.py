@@ -188,3 +188,24 @@ def test_combine_version_chunks(cuda, tmp_path):
     with pytest.raises(HashMismatchError):
         store.combine_version_chunks(WRONG_HASH)
     assert not store.version_exists(WRONG_HASH) and store.list_version_chunks(WRONG_HASH) == [0]
+
+
+def test_list_version_chunks_parses_like_rust(tmp_path):
+    """ADVICE r03: chunk directory names are parsed as `name.parse::<u64>()` (local.rs:367-382): an
+    optional '+' and ASCII digits below 2**64; entries that are not directories themselves (a file, a
+    symlink to a directory: DirEntry::file_type does not follow it) are skipped. Python's int() would
+    also have taken '-1', ' 7', '1_0' and non-ASCII digits. No hashing: runs anywhere."""
+    from oxen_amd.version_store import LocalVersionStore, parse_u64
+
+    store = LocalVersionStore(tmp_path / "versions")
+    d = store.version_chunks_dir(WRONG_HASH)
+    os.makedirs(d)
+    for name in ["-1", "+5", "1_0", " 7", "7 ", "٣", "18446744073709551616", "18446744073709551615", "007", "x",
+                 "+", "", "12"]:
+        if name:
+            os.makedirs(os.path.join(d, name))
+    with open(os.path.join(d, "42"), "w") as f:
+        f.write("a file, not a chunk directory")
+    os.symlink(os.path.join(d, "12"), os.path.join(d, "99"))
+    assert store.list_version_chunks(WRONG_HASH) == [5, 7, 12, 18446744073709551615]
+    assert [parse_u64(s) for s in ["0", "+0", "-0", "00", "+-1", "1e3"]] == [0, 0, None, 0, None, None]
