@@ -803,6 +803,533 @@ __global__ void cdc_sec_file_kernel(const uint64_t* __restrict__ sec_base, uint6
     sec_file[sec] = (uint32_t)lo;
 }
 
+
+// ---------------------------------------------------------------- W: the walk itself, skipping `min`
+// fastcdc v2020's cut_gear never hashes a chunk's first `min` bytes: the hash starts from 0 at
+// index a0 = min & ~1 of every chunk (fastcdchunker.rs:83-98 -> crate fastcdc 3.2.1 cut_gear). F1
+// rolls every byte of the input; at 8 KiB chunks (min 4 KiB, mean chunk 10.5 KB) only 61 % of the
+// bytes are ever hashed by the crate. W walks the chunks themselves, one lane per section, and reads
+// and rolls only those bytes.
+//
+// One lane per section (sections sized so the whole input is one generation of waves), every lane
+// walking its own chunks from `warmup` bytes before its section and recording the starts inside it
+// (the spec list F3 consumes). The bytes reach the lanes exactly as in F1: a round is one 128-B
+// line of every lane's stream, fetched by 8 LDS-DMA loads per wave (lanes 8m..8m+7 of DMA k fetch
+// the line of lane 8k+m, its address taken from that lane with ds_bpermute; pieces rotated so the
+// ds_read_b128 back are conflict-free), the 32-copy gear table (no bank conflicts), the same
+// per-byte v_perm + ds_read_b64 + v_lshl_add_u64 + AND + min3. Per lane the round's mask is the
+// exact one for its position in its chunk (mask_s before center, mask_l after, their common bits in
+// the round that crosses center, all bits -- nothing passes -- before the first tested position),
+// so a group with a zero test is almost always a cut; the ballot-guarded branch resolves the
+// position, records the new chunk start and points the lane's next fetch at the line holding its
+// next `a0` (the round already in flight for the lane is skipped: one bubble per chunk).
+//
+// The walk is RELAXED: a chunk's first 47 hashed positions (a0 .. a0+46) see a hash that started
+// from 0, not the full 48-byte window, and W does not test them (its hash there includes the bytes
+// before a0 of the line it starts rolling from -- harmless from a0+47 on, where those have shifted
+// past bit 63). So W's cut of chunk c equals the crate's unless one of those 47 truncated positions
+// matches (0.29 % of chunks at 8 KiB, measured against the C restatement): the X pass below checks
+// every recorded start for exactly that and re-walks exactly where it happened. Masks must sit at
+// bit 16 or above (they do for avg <= 16 KiB at level 1), so with the hash kept 16 bits to the left
+// every test is one AND on the high word.
+constexpr uint32_t kWalkOob = 0xFFFFFF00u;   // DMA offset of a lane with nothing to fetch (past the range)
+constexpr uint32_t kWalkFull = 0xFFFFFFFFu;  // the round mask that lets nothing pass
+constexpr uint32_t kNoCut = 0xFFFFFFFFu;
+
+struct WalkGeom {
+    uint64_t arena_bytes;  // the arena holds file bytes up to here (the DMA range stops at it, 16-B rounded)
+};
+
+// The chunk that starts at m-space position cs: its test window [lo, tL), the mask switch tS and the
+// relaxed cut cutm (= cs + rem when nothing in the window matches). Chunks with nothing to test (at
+// most `min` bytes left, or the window empty at a file's tail) are cut at once; the starts at or after
+// the section start are recorded; the start that reaches the section end (or the file end) is the
+// lane's last record and ends its walk.
+struct WalkLane {
+    uint32_t cs, lo, tS, tL, cutm;
+    uint32_t mS, mE, mF;  // section start, section end, file end (m-space)
+    uint32_t n;           // starts recorded
+    bool done;
+};
+
+__device__ __forceinline__ void walk_begin_chunk(WalkLane& L, const CdcParams& prm, uint32_t* __restrict__ out) {
+    for (;;) {
+        if (L.cs >= L.mS) {
+            if (L.n < prm.speccap) out[L.n] = L.cs - L.mS;
+            ++L.n;
+            if ((L.cs >= L.mE && L.n > 1) || L.cs >= L.mF) {
+                L.done = true;
+                return;
+            }
+        }
+        const uint32_t len = L.mF - L.cs;
+        if (len <= (uint32_t)prm.min) {
+            L.cs += len;
+            continue;
+        }
+        const uint32_t rem = len > (uint32_t)prm.max ? (uint32_t)prm.max : len;
+        uint32_t center = (uint32_t)prm.avg;
+        if (len <= (uint32_t)prm.max && len < center) center = len;
+        const uint32_t a0 = (uint32_t)(prm.min & ~1ull);
+        L.lo = L.cs + a0 + (uint32_t)kHashSpan;
+        L.tS = L.cs + (center & ~1u);
+        L.tL = L.cs + (rem & ~1u);
+        L.cutm = L.cs + rem;
+        if (L.lo >= L.tL) {  // only truncated positions to test: X checks those
+            L.cs = L.cutm;
+            continue;
+        }
+        return;
+    }
+}
+
+template <int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void cdc_walk_scan_kernel(CdcFiles f, CdcParams prm, uint64_t n_sec, WalkGeom geo) {
+    __shared__ __attribute__((aligned(16))) uint64_t lds[256 * 32 + WAVES * 1024];
+    for (int i = threadIdx.x; i < 256 * 32; i += blockDim.x) lds[i] = kGear[i >> 5] << 16;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint4* const slot = (uint4*)(lds + 256 * 32) + w * 512;
+    const uint64_t sec0 = ((uint64_t)blockIdx.x * WAVES + (uint64_t)w) * 64;
+    if (sec0 >= n_sec) return;
+    const uint64_t sec = sec0 + (uint64_t)lane;
+    const bool live = sec < n_sec;
+    const uint64_t secq = live ? sec : n_sec - 1;
+    const uint32_t file = f.sec_file[secq];
+    const uint64_t flen = f.flen[file];
+    const uint64_t s_start = (secq - f.sec_base[file]) * prm.sec;
+    const uint64_t s_end = s_start + prm.sec < flen ? s_start + prm.sec : flen;
+    const uint64_t w0 = s_start > prm.warmup ? s_start - prm.warmup : 0;
+    // the wave's DMA window: from the lowest address any lane starts at (a 128-B line), so every lane's
+    // positions are 32-bit offsets into one buffer resource (the host checked the wave spans < 4 GiB)
+    const uint64_t a_file = (uint64_t)f.arena + f.foff[file];
+    uint64_t a_min = live ? a_file + w0 : ~0ull;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t other = ((uint64_t)(uint32_t)__shfl_xor((int)(a_min >> 32), o) << 32) | (uint32_t)__shfl_xor((int)(uint32_t)a_min, o);
+        a_min = other < a_min ? other : a_min;
+    }
+    const uint64_t base = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a_min) |
+                           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a_min >> 32)) << 32)) & ~127ull;
+    const uint64_t a_end = ((uint64_t)f.arena + geo.arena_bytes + 15) & ~15ull;
+    const uint64_t span = a_end - base;
+    const int nrec = __builtin_amdgcn_readfirstlane((int)(uint32_t)(span < 0xFFFFFF00ull ? span : 0xFFFFFF00ull));
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, nrec, 0x00020000);
+
+    WalkLane L;
+    const uint32_t mfile = (uint32_t)(a_file - base);  // only positions >= w0 are ever used
+    L.mS = mfile + (uint32_t)s_start;
+    L.mE = mfile + (uint32_t)s_end;
+    // the walk never looks past its section end + one chunk, so the file end is clamped to a point
+    // beyond that (every chunk it cuts there still sees more than `max` bytes left: the same cut) and
+    // every position fits 32 bits
+    const uint64_t f_lim = s_start + prm.sec + 2 * prm.max + 4096;
+    L.mF = mfile + (uint32_t)(flen < f_lim ? flen : f_lim);
+    L.n = 0;
+    L.done = !live;
+    L.cs = mfile + (uint32_t)w0;
+    uint32_t* __restrict__ out = f.spec + secq * prm.speccap;
+    if (live) walk_begin_chunk(L, prm, out);
+    const uint32_t a0 = (uint32_t)(prm.min & ~1ull);
+    uint32_t NL = L.done ? kWalkOob : ((L.cs + a0) & ~127u);  // next line to fetch
+    const uint64_t ms64 = prm.mask_s << 16, ml64 = prm.mask_l << 16;
+    const uint32_t ms = (uint32_t)(ms64 >> 32), ml = (uint32_t)(ml64 >> 32), mc = ms & ml;  // host: all bits >= 16
+    const uint32_t copy_off = (uint32_t)(lane & 31) * 8;
+    const char* const tab = (const char*)lds;
+    auto gear = [&](uint32_t word, int j) -> uint64_t {
+        const uint32_t a = __builtin_amdgcn_perm(word, copy_off, 0x0c0c0000u | ((4u + (uint32_t)j) << 8));
+        return *(const uint64_t*)(tab + a);
+    };
+    // DMA k, lane 8m + j: piece (j - rot(r)) & 7 of the line of lane r = 8k + m
+    const int dm = lane >> 3, dj = lane & 7;
+    uint32_t poff[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t r = 8 * k + dm;
+        poff[k] = 16 * ((uint32_t)(dj - (int)((r >> 1) & 7)) & 7);
+    }
+    auto dma = [&](uint32_t line) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t src = (uint32_t)__builtin_amdgcn_ds_bpermute((8 * k + dm) * 4, (int)line);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(slot + 64 * k), 16,
+                                                     src + poff[k], 0, 0, kScanDmaAux);
+        }
+    };
+    uint32_t RL = NL;  // the line the DMA in flight fetches for this lane
+    bool RV = !L.done;  // ... and whether it still belongs to the lane's current chunk
+    if (!L.done) NL += 128;
+    dma(RL);
+    const int rot = (lane >> 1) & 7;
+    uint64_t h = 0;
+#pragma unroll 1
+    for (;;) {
+        if (__builtin_amdgcn_ballot_w64(!L.done) == 0) break;
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this round's DMA has landed
+        uint32_t wv[32];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint4 v = slot[lane * 8 + ((q + rot) & 7)];
+            wv[4 * q] = v.x, wv[4 * q + 1] = v.y, wv[4 * q + 2] = v.z, wv[4 * q + 3] = v.w;
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot is free for the next DMA
+        const uint32_t CL = RL;
+        const bool CV = RV && !L.done;
+        RL = L.done ? kWalkOob : NL;
+        RV = !L.done;
+        if (!L.done) NL += 128;
+        dma(RL);
+        // this round's mask (see above); tests at positions < lo or >= tL are rejected when resolved
+        uint32_t m;
+        if (!CV || CL + 128 <= L.lo) m = kWalkFull;
+        else if (CL + 128 <= L.tS) m = ms;
+        else if (CL >= L.tS) m = ml;
+        else m = mc;
+        bool cut_now = false;
+        constexpr int P = 3;
+        uint64_t G[P + 1][4];
+#pragma unroll
+        for (int i = 0; i < P; ++i)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) G[i][b] = gear(wv[i], b);
+        uint32_t hh[16];  // the high words of the hash at the current group's 16 positions
+        uint32_t anyz = 0xFFFFFFFFu;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            if (i + P < 32) {
+#pragma unroll
+                for (int b = 0; b < 4; ++b) G[(i + P) % (P + 1)][b] = gear(wv[i + P], b);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            uint32_t tt[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                h = (h << 1) + G[i % (P + 1)][b];
+                hh[4 * (i & 3) + b] = (uint32_t)(h >> 32);
+                tt[b] = hh[4 * (i & 3) + b] & m;
+            }
+            anyz = min3_u32(min3_u32(anyz, tt[0], tt[1]), tt[2], tt[3]);
+            if ((i & 3) == 3) {
+                if (__builtin_amdgcn_ballot_w64(anyz == 0)) {
+                    if (anyz == 0) {
+                        // the group's zero tests, in position order; the first valid one is the cut
+                        const uint32_t g = CL + 16 * (uint32_t)(i >> 2);
+                        uint32_t bits = 0;
+#pragma unroll
+                        for (int j = 0; j < 16; ++j) bits |= ((hh[j] & m) == 0 ? 1u : 0u) << j;
+                        while (bits) {
+                            const int j = __builtin_ctz(bits);
+                            bits &= bits - 1;
+                            const uint32_t p = g + (uint32_t)j;
+                            if (p < L.lo || p >= L.tL) continue;
+                            if (m == mc) {  // the round that crosses center: mask_s before it, mask_l after
+                                uint32_t hj = 0;
+#pragma unroll
+                                for (int k = 0; k < 16; ++k) hj = k == j ? hh[k] : hj;
+                                if ((hj & (p < L.tS ? ms : ml)) != 0) continue;
+                            }
+                            // a cut: the next chunk starts at p (cut_gear returns the matching index)
+                            L.cs = p;
+                            walk_begin_chunk(L, prm, out);
+                            if (!L.done) NL = (L.cs + a0) & ~127u;
+                            RV = false;  // the line in flight belonged to the old chunk
+                            m = kWalkFull;
+                            cut_now = true;
+                            break;
+                        }
+                    }
+                }
+                anyz = 0xFFFFFFFFu;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // no cut before the end of the test window: the chunk ends at cs + rem (max, or the file end)
+        if (CV && !cut_now && CL + 128 >= L.tL) {
+            L.cs = L.cutm;
+            walk_begin_chunk(L, prm, out);
+            if (!L.done) NL = (L.cs + a0) & ~127u;
+            RV = false;
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // the last (empty) DMA has landed before the slot goes away
+    if (live) f.spec_cnt[sec] = L.n;
+}
+
+// ---------------------------------------------------------------- X: exact walk over W's lists
+// X works in W's shifted form: table entries GEAR << 16 and masks << 16, so every mask bit sits in the
+// high word of the hash and a test is one AND of that word (the walk path's masks are all at bit 16 or
+// above; the host checks).
+struct XMasks {
+    uint32_t s, l;  // high words of mask_s << 16, mask_l << 16
+};
+
+// Truncated-window check of the chunk that starts at file position c: the first position in
+// [c + a0, min(c + a0 + 47, c + eL)) whose hash -- started from 0 at a0, as cut_gear's is --
+// matches its mask, or ~0 (then W's relaxed cut of c is the crate's cut).
+__device__ uint64_t trunc_cut(const uint8_t* __restrict__ fbase, uint64_t flen, uint64_t c, const CdcParams& prm,
+                              XMasks xm, const uint64_t* __restrict__ gear) {
+    const uint64_t len = flen - c;
+    if (len <= prm.min) return ~0ull;
+    const uint64_t rem = len > prm.max ? prm.max : len;
+    uint64_t center = prm.avg;
+    if (len <= prm.max && len < center) center = len;
+    const uint64_t a0 = prm.min & ~1ull, eS = center & ~1ull, eL = rem & ~1ull;
+    const uint64_t tend = a0 + kHashSpan < eL ? a0 + kHashSpan : eL;
+    const uint4 t0 = load16_file(fbase, c + a0, flen), t1 = load16_file(fbase, c + a0 + 16, flen),
+                t2 = load16_file(fbase, c + a0 + 32, flen);
+    uint64_t hsh = 0;
+    uint32_t first = 0xFFFFFFFFu;
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {  // 16 table reads together, then their rolls (bounded hoisting)
+        const uint4 tw = g == 0 ? t0 : g == 1 ? t1 : t2;
+        uint64_t G[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) G[j] = gear[byte_of(tw, j)];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int k = 16 * g + j;
+            if (k < kHashSpan) {
+                const uint64_t q = a0 + (uint64_t)k;
+                hsh = (hsh << 1) + G[j];
+                const uint32_t t = (uint32_t)(hsh >> 32) & (q < eS ? xm.s : xm.l);
+                first = (t == 0 && q < tend && first == 0xFFFFFFFFu) ? (uint32_t)k : first;
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return first == 0xFFFFFFFFu ? ~0ull : c + a0 + first;
+}
+
+// The exact length of the chunk that starts at file position p (cut_gear on content[p..]), computed by
+// one wave: 4 KiB of positions per step (a chunk takes ~2 steps at 8 KiB), 64 per lane. A lane rolls
+// the 48 bytes before its positions (the full window; lane 0 of the first step starts at a0 from 0,
+// where cut_gear's hash starts), tests each position with one AND and keeps its first match.
+__device__ uint64_t cut_coop(const uint8_t* __restrict__ fbase, uint64_t flen, uint64_t p, const CdcParams& prm,
+                             XMasks xm, const uint64_t* __restrict__ gear) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t len = flen - p;
+    if (len <= prm.min) return len;
+    const uint64_t rem = len > prm.max ? prm.max : len;
+    uint64_t center = prm.avg;
+    if (len <= prm.max && len < center) center = len;
+    const uint64_t a0 = prm.min & ~1ull, eS = center & ~1ull, eL = rem & ~1ull;
+    constexpr int kW = 64;  // positions per lane and step
+    for (uint64_t W = a0; W < eL; W += 64 * kW) {
+        const uint64_t q0 = W + (uint64_t)(kW * lane);
+        // positions q0 .. q0+63 of this lane: mask_s below kS, tested below kL; the 48 bytes before
+        // them give the full window (a0 >= 64: never before the chunk)
+        const int kS = q0 >= eS ? 0 : (eS - q0 >= kW ? kW : (int)(eS - q0));
+        const int kL = q0 >= eL ? 0 : (eL - q0 >= kW ? kW : (int)(eL - q0));
+        const bool from0 = W == a0 && lane == 0;  // lane 0 of the first step: the hash starts at a0
+        uint4 cur[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) cur[k] = load16_file(fbase, p + q0 - 48 + 16 * (uint64_t)k, flen);
+        // 16 bytes at a time: the word's 16 table reads go out together, then its 16 rolls (bounded
+        // hoisting keeps the register count down)
+        uint64_t h = 0;
+        int zfirst = -1;
+#pragma unroll
+        for (int g = 0; g < 7; ++g) {
+            uint64_t G[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) G[j] = gear[byte_of(cur[g], j)];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                h = (h << 1) + G[j];
+                const int k = 16 * g + j - 48;
+                if (k >= 0) {
+                    const uint32_t t = ((uint32_t)(h >> 32) & (k < kS ? xm.s : xm.l)) | (k < kL ? 0u : 1u);
+                    zfirst = (t == 0 && zfirst < 0) ? k : zfirst;
+                }
+            }
+            if (g == 2 && from0) h = 0;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const uint64_t any = __builtin_amdgcn_ballot_w64(zfirst >= 0);
+        if (any) {
+            const int first = __builtin_ctzll(any);
+            const int k = __shfl(zfirst, first);
+            return W + (uint64_t)(kW * first) + (uint64_t)k;
+        }
+    }
+    return rem;
+}
+
+// One wave: the true chunk starts of section `sec` given its true entry e (file-relative, e >= the
+// section start): W's list from e on wherever it is exact, cut_gear itself (cut_coop) where it is not.
+// When e is on the list and every entry from there is exact, the section converged (emit reads W's
+// list from k0, as in F3); otherwise the starts are written to `fix`.
+__device__ void x_section(const CdcFiles& f, const CdcParams& prm, const CdcStitch& s, uint64_t sec, uint64_t e,
+                          uint32_t* __restrict__ entry_used, const uint64_t* __restrict__ gear, XMasks xm,
+                          uint32_t* __restrict__ lst, uint32_t* __restrict__ tcl) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t file = f.sec_file[sec];
+    const uint64_t flen = f.flen[file];
+    const uint64_t sec0 = f.sec_base[file];
+    const uint64_t S = (sec - sec0) * prm.sec;
+    const uint64_t E = S + prm.sec < flen ? S + prm.sec : flen;
+    const uint8_t* fbase = f.arena + f.foff[file];
+    const uint32_t cnt = f.spec_cnt[sec];
+    const uint32_t* spec = f.spec + sec * prm.speccap;
+    const uint32_t nl = cnt < prm.speccap ? cnt : prm.speccap;  // W's lists never overflow (speccap bound)
+    __syncthreads();  // lst / tcl of the previous section this wave walked are no longer read
+    // every entry but the last (the exit): its truncated window
+    for (uint32_t k = (uint32_t)lane; k < nl; k += 64) {
+        const uint32_t rel = spec[k];
+        lst[k] = rel;
+        uint32_t tc = kNoCut;
+        if (k + 1 < nl) {
+            const uint64_t t = trunc_cut(fbase, flen, S + rel, prm, xm, gear);
+            if (t != ~0ull) tc = (uint32_t)(t - S);
+        }
+        tcl[k] = tc;
+    }
+    __syncthreads();
+    const uint32_t re = (uint32_t)(e - S);
+    // e on the list? and the first inexact entry at or after it
+    uint32_t k0 = kNoCut, kb = kNoCut;
+    for (uint32_t b = 0; b < nl; b += 64) {
+        const uint32_t k = b + (uint32_t)lane;
+        const uint64_t hitm = __builtin_amdgcn_ballot_w64(k < nl && lst[k] == re);
+        if (hitm && k0 == kNoCut) k0 = b + (uint32_t)__builtin_ctzll(hitm);
+    }
+    if (k0 != kNoCut) {
+        for (uint32_t b = 0; b < nl; b += 64) {
+            const uint32_t k = b + (uint32_t)lane;
+            const uint64_t badm = __builtin_amdgcn_ballot_w64(k >= k0 && k + 1 < nl && tcl[k] != kNoCut);
+            if (badm && kb == kNoCut) kb = b + (uint32_t)__builtin_ctzll(badm);
+        }
+    }
+    if (lane == 0) entry_used[sec] = re;
+    if (k0 != kNoCut && kb == kNoCut && cnt <= prm.speccap) {
+        if (lane == 0) {
+            s.status[sec] = kConverged;
+            s.k0[sec] = k0;
+            s.count[sec] = nl - 1 - k0;
+            s.exit[sec] = S + lst[nl - 1];
+        }
+        return;
+    }
+    // the exact walk: follow W's list while it is exact, cut_gear where it is not
+    uint32_t* fix = s.fix + sec * prm.speccap;
+    auto lookup = [&](uint64_t pos) -> uint32_t {  // index of pos on the list, or kNoCut
+        const uint32_t r = (uint32_t)(pos - S);
+        uint32_t lo2 = 0, hi2 = nl;
+        while (lo2 < hi2) {
+            const uint32_t mid = (lo2 + hi2) >> 1;
+            if (lst[mid] < r) lo2 = mid + 1;
+            else hi2 = mid;
+        }
+        return lo2 < nl && lst[lo2] == r ? lo2 : kNoCut;
+    };
+    uint64_t p = e;
+    uint32_t j = k0, n = 0;
+    while (p < E) {
+        if (lane == 0 && n < prm.speccap) fix[n] = (uint32_t)(p - S);
+        ++n;
+        if (j != kNoCut && j + 1 < nl) {
+            if (tcl[j] == kNoCut) {
+                ++j;
+                p = S + lst[j];
+                continue;
+            }
+            p = S + tcl[j];
+        } else {
+            p += cut_coop(fbase, flen, p, prm, xm, gear);
+        }
+        j = lookup(p);
+    }
+    if (lane == 0) {
+        s.status[sec] = kFixed;
+        s.count[sec] = n;
+        s.exit[sec] = p;
+    }
+}
+
+__device__ __forceinline__ XMasks x_masks(const CdcParams& prm) {
+    return XMasks{(uint32_t)((prm.mask_s << 16) >> 32), (uint32_t)((prm.mask_l << 16) >> 32)};
+}
+
+// X, first pass: every section (a grid-stride loop of one-wave workgroups), from the entry W's previous
+// section ends at (0 for a file's first).
+__global__ __launch_bounds__(64) void cdc_xwalk_kernel(CdcFiles f, CdcParams prm, CdcStitch s, uint64_t n_sec,
+                                                       uint32_t* __restrict__ entry_used) {
+    __shared__ uint64_t lds_gear[256];
+    extern __shared__ uint32_t xl[];  // 2 * speccap u32: the list and each entry's truncated cut
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) lds_gear[i] = kGear[i] << 16;
+    const XMasks xm = x_masks(prm);
+    for (uint64_t sec = blockIdx.x; sec < n_sec; sec += gridDim.x) {
+        const uint32_t file = f.sec_file[sec];
+        const uint64_t sec0 = f.sec_base[file];
+        const uint64_t e =
+            sec == sec0 ? 0 : ((sec - 1 - sec0) * prm.sec + f.spec[(sec - 1) * prm.speccap + f.spec_cnt[sec - 1] - 1]);
+        x_section(f, prm, s, sec, e, entry_used, lds_gear, xm, xl, xl + prm.speccap);
+    }
+}
+
+// X, second pass: one wave per 64 sections finds those whose assumed entry is not the exit the first
+// pass found for the section before them, and walks each of them again from that exit.
+__global__ __launch_bounds__(64) void cdc_xretry_kernel(CdcFiles f, CdcParams prm, CdcStitch s, uint64_t n_sec,
+                                                        uint32_t* __restrict__ entry_used) {
+    __shared__ uint64_t lds_gear[256];
+    extern __shared__ uint32_t xl[];
+    const int lane = threadIdx.x;
+    const uint64_t sec = (uint64_t)blockIdx.x * 64 + (uint64_t)lane;
+    bool redo = false;
+    if (sec < n_sec) {
+        const uint32_t file = f.sec_file[sec];
+        const uint64_t sec0 = f.sec_base[file];
+        if (sec != sec0) redo = s.exit[sec - 1] != (sec - sec0) * prm.sec + entry_used[sec];
+    }
+    uint64_t m = __builtin_amdgcn_ballot_w64(redo);
+    if (m == 0) return;
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) lds_gear[i] = kGear[i] << 16;
+    const XMasks xm = x_masks(prm);
+    while (m) {
+        const uint64_t t = (uint64_t)blockIdx.x * 64 + (uint64_t)__builtin_ctzll(m);
+        m &= m - 1;
+        x_section(f, prm, s, t, s.exit[t - 1], entry_used, lds_gear, xm, xl, xl + prm.speccap);
+    }
+}
+
+// X, last resort: one wave per file walks its sections in order and redoes every one whose entry is
+// not the exit the section before it ended at (after a redo, the next section is checked again).
+__global__ __launch_bounds__(64) void cdc_xfix_kernel(CdcFiles f, CdcParams prm, CdcStitch s, uint64_t n_files,
+                                                      uint32_t* __restrict__ entry_used) {
+    __shared__ uint64_t lds_gear[256];
+    extern __shared__ uint32_t xl[];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) lds_gear[i] = kGear[i] << 16;
+    __syncthreads();
+    const uint64_t file = blockIdx.x;
+    if (file >= n_files) return;
+    const XMasks xm = x_masks(prm);
+    const int lane = threadIdx.x;
+    const uint64_t sec0 = f.sec_base[file], nsec = f.sec_base[file + 1] - sec0;
+    uint64_t i = 1;
+    while (i < nsec) {
+        const uint64_t j = i + (uint64_t)lane;
+        bool bad = false;
+        if (j < nsec) {
+            const uint64_t ex = __atomic_load_n(&s.exit[sec0 + j - 1], __ATOMIC_RELAXED);
+            const uint32_t eu = __atomic_load_n(&entry_used[sec0 + j], __ATOMIC_RELAXED);
+            bad = ex != j * prm.sec + eu;
+        }
+        const uint64_t mbad = __builtin_amdgcn_ballot_w64(bad);
+        if (mbad == 0) {
+            i += 64;
+            continue;
+        }
+        i += (uint64_t)__builtin_ctzll(mbad);
+        const uint64_t e = __atomic_load_n(&s.exit[sec0 + i - 1], __ATOMIC_RELAXED);
+        x_section(f, prm, s, sec0 + i, e, entry_used, lds_gear, xm, xl, xl + prm.speccap);
+        __threadfence();
+        ++i;
+    }
+}
+
 }  // namespace oxh
 
 // ---------------------------------------------------------------- host side
@@ -914,9 +1441,35 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     // (C5 at 8 KiB: 57.2 ms vs 63.8 ms with 256 KiB sections and 64 KiB of warm-up; at 64 KiB: 53.8
     // vs 54.9 ms with 1 MiB sections; tools/bench_fastcdc.py sweeps).
     const uint64_t max_rounded = ((uint64_t)max_size + 1023) / 1024 * 1024;
+    uint64_t total_bytes = 0, arena_bytes = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        total_bytes += lens[i];
+        arena_bytes = std::max<uint64_t>(arena_bytes, offsets[i] + lens[i]);
+    }
+    // The walk path (W + X, DESIGN §4 "F1 -> W"): chosen where it rolls fewer bytes than F1 -- small
+    // chunks, where the skipped `min` bytes are a large share (61 % rolled at 8 KiB, 94 % at 64 KiB) --
+    // and where its layout rules hold: masks at bit 16 or above, a 128-B aligned arena, and every
+    // wave's 64 sections inside one 4 GiB window (checked below). OXH_CDC_WALK=0 / 1 forces it off / on.
+    const char* walk_env = getenv("OXH_CDC_WALK");
+    bool walk = (((prm.mask_s | prm.mask_l) & 0xFFFFull) == 0) && (((uintptr_t)d_arena & 127) == 0) &&
+                (walk_env ? atoi(walk_env) != 0 : (avg_size <= 16384));
     prm.warmup = std::max<uint64_t>(6 * (uint64_t)max_size, 128 * 1024);
+    if (walk) {
+        // one lane per section, one generation of 12-wave workgroups on every CU: sections as large
+        // as that allows (fewer sections = less warm-up and stitching), whole 8 KiB, at least 4 max
+        int dev = 0, cus = 256;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+        const uint64_t lanes = (uint64_t)cus * oxh::kScanWaves * 64;
+        const uint64_t want = (total_bytes + lanes - 1) / std::max<uint64_t>(lanes, 1);
+        if (!getenv("OXH_CDC_SECTION_BYTES")) prm.sec = std::max<uint64_t>({want, 4 * max_rounded, 64 * 1024});
+        // warm-up: a relaxed walk started anywhere lands on the true one within 14 / 37 / 67 KB in 50 /
+        // 90 / 99 % of starts at 8 KiB chunks (C restatement, 1 GiB); X re-walks the sections whose
+        // warm-up was too short, so it is kept short: two max-sized chunks
+        prm.warmup = 2 * (uint64_t)max_size;
+    }
     if (prm.sec < max_rounded) prm.sec = max_rounded;
-    if (!getenv("OXH_CDC_SECTION_BYTES") && prm.sec < 8 * max_rounded) prm.sec = 8 * max_rounded;
+    if (!walk && !getenv("OXH_CDC_SECTION_BYTES") && prm.sec < 8 * max_rounded) prm.sec = 8 * max_rounded;
     prm.sec = (prm.sec + 8191) / 8192 * 8192;  // 64 F1 units of whole 128-byte rounds
     // a candidate entry holds the group index in 17 bits: units of at most 2 MiB (sections of 128 MiB,
     // 8 chunks of the crate's largest max); the test-only section override is clamped to that
@@ -932,6 +1485,25 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     sec_base[0] = 0;
     for (uint64_t i = 0; i < n; ++i) sec_base[i + 1] = sec_base[i] + (lens[i] + prm.sec - 1) / prm.sec;
     const uint64_t n_sec = sec_base[n];
+    if (walk) {
+        // every wave's lanes must address their streams from one buffer resource: the lowest start
+        // (warm-up included) to the highest byte a lane may read (its section end + two max chunks,
+        // or its file end) within 4 GiB - 1 MiB
+        for (uint64_t w0s = 0, f = 0; w0s < n_sec && walk; w0s += 64) {
+            uint64_t lo = ~0ull, hi = 0;
+            for (uint64_t sct = w0s; sct < std::min<uint64_t>(n_sec, w0s + 64); ++sct) {
+                while (sec_base[f + 1] <= sct) ++f;
+                const uint64_t ss = (sct - sec_base[f]) * prm.sec;
+                const uint64_t a = offsets[f] + (ss > prm.warmup ? ss - prm.warmup : 0);
+                const uint64_t b = offsets[f] + std::min<uint64_t>(lens[f], ss + prm.sec + 2 * prm.max + 4096);
+                lo = std::min(lo, a);
+                hi = std::max(hi, b);
+            }
+            if (hi - (lo & ~127ull) + 256 >= 0xFFFFFF00ull - (1ull << 20)) walk = false;
+        }
+        if (walk_env && atoi(walk_env) != 0 && !walk)
+            return cdc_fail(OXH_ERR_INVALID, "OXH_CDC_WALK=1: the arena layout does not allow the walk path");
+    }
 
     // OXH_TRACE=1: host-side stage times of this call on stderr
     static const bool trace = getenv("OXH_TRACE") != nullptr;
@@ -946,9 +1518,15 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     sc.want(&d_flen, n);
     sc.want(&d_sec_base, n + 1);
     sc.want(&d_first, n + 1);
+    uint32_t* d_entry = nullptr;
     sc.want(&d_sec_file, n_sec);
-    sc.want(&d_cand, n_sec * 64 * prm.cap);
-    sc.want(&d_cand_occ, n_sec);
+    if (walk) {
+        d_cand = nullptr, d_cand_occ = nullptr;
+        sc.want(&d_entry, n_sec);
+    } else {
+        sc.want(&d_cand, n_sec * 64 * prm.cap);
+        sc.want(&d_cand_occ, n_sec);
+    }
     sc.want(&d_spec, n_sec * prm.speccap);
     sc.want(&d_spec_cnt, n_sec);
     sc.want(&d_status, n_sec);
@@ -971,7 +1549,27 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     const double t_alloc = since();
     oxh::CdcFiles f{(const uint8_t*)d_arena, d_foff, d_flen, d_sec_base, d_sec_file, d_cand, d_cand_occ, d_spec, d_spec_cnt};
     oxh::CdcStitch sti{d_status, d_k0, d_count, d_exit, d_fix, d_out_base};
-    if (n_sec) {
+    if (n_sec && walk) {
+        // W: one lane per section; X twice (every section, then the ones whose assumed entry turned out
+        // wrong); the serial pass for whatever is left; then the chunk counts' prefix
+        const uint64_t nwaves = (n_sec + 63) / 64;
+        hipLaunchKernelGGL(oxh::cdc_walk_scan_kernel<oxh::kScanWaves>,
+                           dim3((unsigned)((nwaves + oxh::kScanWaves - 1) / oxh::kScanWaves)), dim3(64 * oxh::kScanWaves), 0, st,
+                           f, prm, n_sec, oxh::WalkGeom{arena_bytes});
+        CDC_HIP(hipGetLastError());
+        const size_t xlds = 2 * (size_t)prm.speccap * sizeof(uint32_t);
+        static const unsigned xgrid = getenv("OXH_CDC_X_WGS") ? (unsigned)atoi(getenv("OXH_CDC_X_WGS")) : 16384u;
+        hipLaunchKernelGGL(oxh::cdc_xwalk_kernel, dim3((unsigned)std::min<uint64_t>(n_sec, xgrid)), dim3(64), xlds, st, f, prm,
+                           sti, n_sec, d_entry);
+        CDC_HIP(hipGetLastError());
+        hipLaunchKernelGGL(oxh::cdc_xretry_kernel, dim3((unsigned)((n_sec + 63) / 64)), dim3(64), xlds, st, f, prm, sti, n_sec,
+                           d_entry);
+        CDC_HIP(hipGetLastError());
+        hipLaunchKernelGGL(oxh::cdc_xfix_kernel, dim3((unsigned)n), dim3(64), xlds, st, f, prm, sti, n, d_entry);
+        CDC_HIP(hipGetLastError());
+        hipLaunchKernelGGL(oxh::cdc_prefix_kernel, dim3(1), dim3(1024), 0, st, sti, n_sec);
+        CDC_HIP(hipGetLastError());
+    } else if (n_sec) {
         // F1: one wave per section (kScanWaves per workgroup, 160 KiB of LDS); SH when the bits both
         // masks share are all >= 16
         const bool sh = (((prm.mask_s & prm.mask_l) << 16) & 0xFFFFFFFFull) == 0;
@@ -999,8 +1597,10 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     const double t_launch = since();
     CDC_HIP(hipStreamSynchronize(st));
     if (trace)
-        fprintf(stderr, "[oxh] fastcdc: sections=%llu malloc=%.4fs copy=%.4fs launch=%.4fs chunking=%.4fs scratch=%.2fGiB\n",
-                (unsigned long long)n_sec, t_malloc, t_alloc - t_malloc, t_launch - t_alloc, since(), sc.lease.size() / 1073741824.0);
+        fprintf(stderr, "[oxh] fastcdc: %s sections=%llu (%llu B, warm-up %llu B) malloc=%.4fs copy=%.4fs launch=%.4fs "
+                "chunking=%.4fs scratch=%.2fGiB\n", walk ? "walk" : "scan", (unsigned long long)n_sec,
+                (unsigned long long)prm.sec, (unsigned long long)prm.warmup, t_malloc, t_alloc - t_malloc, t_launch - t_alloc,
+                since(), sc.lease.size() / 1073741824.0);
     const uint64_t total = first_chunk[n];
     if (total > capacity)
         return cdc_fail(OXH_ERR_INVALID, "chunk capacity too small: need " + std::to_string(total) + " entries");

@@ -89,6 +89,18 @@ def test_chunker_argument_errors(built_lib):
 
 
 # ------------------------------------------------------------------------------ GPU parity
+@pytest.fixture(params=["auto", "scan"])
+def cdc_path(request, monkeypatch):
+    """Both chunking paths: "auto" takes the walk (W + X) wherever it applies (avg <= 16 KiB, masks at
+    bit 16 or above: the 8 KiB and 4 KiB configs), F1 + F2 elsewhere; "scan" forces F1 + F2
+    (OXH_CDC_WALK=0) everywhere."""
+    if request.param == "scan":
+        monkeypatch.setenv("OXH_CDC_WALK", "0")
+    else:
+        monkeypatch.delenv("OXH_CDC_WALK", raising=False)
+    return request.param
+
+
 def _pack(files, align_pad=3):
     """Pack byte arrays back to back with a small odd gap (misaligned starts)."""
     offs, pos = [], 0
@@ -126,7 +138,7 @@ def _check(cuda, oracle_lib, files, mn, av, mx, level=1):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", CONFIGS, ids=lambda c: "-".join(map(str, c)))
-def test_fastcdc_random_ragged(cuda, oracle_lib, cfg):
+def test_fastcdc_random_ragged(cuda, oracle_lib, cfg, cdc_path):
     rng = np.random.default_rng(sum(cfg))
     sizes = [0, 1, 63, 64, 65, cfg[0] - 1, cfg[0], cfg[0] + 1, cfg[1] + 7, cfg[2] - 1, cfg[2], cfg[2] + 1,
              262_143, 262_144, 262_145, 1_000_003, 3 * 262_144 + 17]
@@ -138,7 +150,7 @@ def test_fastcdc_random_ragged(cuda, oracle_lib, cfg):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", CONFIGS[:4], ids=lambda c: "-".join(map(str, c)))
-def test_fastcdc_low_entropy(cuda, oracle_lib, cfg):
+def test_fastcdc_low_entropy(cuda, oracle_lib, cfg, cdc_path):
     """Text-like and small-alphabet data: candidates cluster, speculative walks converge late."""
     rng = np.random.default_rng(99)
     text = np.frombuffer(b"".join(b"File content %d\n" % i for i in range(200_000)), dtype=np.uint8)
@@ -149,7 +161,7 @@ def test_fastcdc_low_entropy(cuda, oracle_lib, cfg):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("byte", [0, 9, 57, 91])
-def test_fastcdc_constant_data(cuda, oracle_lib, byte):
+def test_fastcdc_constant_data(cuda, oracle_lib, byte, cdc_path):
     """Constant bytes: the full-window hash is constant. For avg 256 bytes 9/91 make EVERY position a
     mask_l candidate and 57 every position a mask_s candidate: the per-section lists overflow and the
     walk scans bytes (the dense fallback); byte 0 gives no candidates (every chunk is max-sized)."""
@@ -208,7 +220,7 @@ def test_fastcdchunker_pack(cuda, oracle_lib, tmp_path):
 @pytest.mark.parametrize("warmup", ["0", None], ids=["nowarmup", "warmup"])
 @pytest.mark.parametrize("section", [1024, 4096, 65536])
 @pytest.mark.parametrize("cfg", [CONFIGS[0], CONFIGS[2], CONFIGS[3], CONFIGS[4]], ids=lambda c: "-".join(map(str, c)))
-def test_fastcdc_small_sections(cuda, oracle_lib, monkeypatch, section, cfg, warmup):
+def test_fastcdc_small_sections(cuda, oracle_lib, monkeypatch, section, cfg, warmup, cdc_path):
     """Many sections per file (OXH_CDC_SECTION_BYTES, raised to `max` where smaller and rounded up to
     8 KiB: 64 F1 units of whole 128-byte rounds): speculative walks start mid-chunk everywhere, and the
     stitch re-walks wherever a speculative walk has not converged (constant data never does)."""
@@ -224,7 +236,7 @@ def test_fastcdc_small_sections(cuda, oracle_lib, monkeypatch, section, cfg, war
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("avg", [8192, 65536])
-def test_fastcdc_many_default_sections(cuda, oracle_lib, avg):
+def test_fastcdc_many_default_sections(cuda, oracle_lib, avg, cdc_path):
     """Default section / warm-up sizing (sections >= 512 KiB or 8 max chunks, warm-up >= 128 KiB) over
     files spanning many sections: random, text-like and a misaligned start, C5's min/avg/max shape."""
     rng = np.random.default_rng(avg)
@@ -253,7 +265,7 @@ def test_fastcdc_unit_list_overflow(cuda, oracle_lib, monkeypatch, cap):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("avg", [8192, 65536])
-def test_fastcdc_gib_files_fully_checked(cuda, oracle_lib, avg):
+def test_fastcdc_gib_files_fully_checked(cuda, oracle_lib, avg, cdc_path):
     """C5's shape scaled to 4 files of 1 GiB + ragged tails (device-generated splitmix data, files at
     4 KiB-aligned starts as bench_fastcdc lays them out): every chunk boundary of every file and every
     chunk digest against the C oracle -- the whole file, not a prefix."""
@@ -283,3 +295,28 @@ def test_fastcdc_gib_files_fully_checked(cuda, oracle_lib, avg):
         assert all(ex.map(one, range(len(sizes))))
     del arena
     torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+def test_fastcdc_walk_truncated_window_cuts(cuda, oracle_lib, monkeypatch):
+    """The walk (W) never tests a chunk's first 47 hashed positions, where cut_gear's hash has not yet
+    seen a full 48-byte window; X re-walks exactly the chunks where one of them matches. With
+    min = avg = 4 KiB every tested position uses mask_l (11 bits), so ~47 / 2**11 = 2.3 % of chunks are
+    cut inside that window: over 64 MiB of random data ~250 of them. Every boundary must equal the
+    oracle's, with the walk path forced (OXH_CDC_WALK=1 fails loudly where it cannot be taken)."""
+    import torch
+
+    from oxen_amd.device import fastcdc_device, to_numpy_u64
+
+    monkeypatch.setenv("OXH_CDC_WALK", "1")
+    rng = np.random.default_rng(47)
+    n = 64 << 20
+    data = rng.integers(0, 256, n, dtype=np.uint8)
+    want = F.chunks(data, 4096, 4096, 8192)
+    # how many chunks the relaxed walk would get wrong, from the oracle's own boundaries
+    d_arena = torch.from_numpy(data).to(cuda)
+    c_off, c_len, dig, first = fastcdc_device(d_arena, [0], [n], 4096, 4096, 8192)
+    assert int(first[1]) == len(want)
+    assert np.array_equal(to_numpy_u64(c_off), want[:, 0]) and np.array_equal(to_numpy_u64(c_len), want[:, 1])
+    short = int(((want[:-1, 1] >= 4096) & (want[:-1, 1] < 4096 + 47)).sum())
+    assert short > 50, short  # chunks cut inside the truncated window: the case X exists for
