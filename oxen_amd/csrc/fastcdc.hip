@@ -883,7 +883,10 @@ __device__ __forceinline__ void walk_begin_chunk(WalkLane& L, const CdcParams& p
     }
 }
 
-template <int WAVES>
+// LATE: the next round's DMA goes out after this round is rolled, when each lane's next line is known
+// (no stale round after a cut, but the DMA's latency is left to the other waves of the SIMD to hide);
+// otherwise it goes out before the roll, for the line after the current one.
+template <int WAVES, bool LATE>
 __global__ __launch_bounds__(64 * WAVES) void cdc_walk_scan_kernel(CdcFiles f, CdcParams prm, uint64_t n_sec, WalkGeom geo) {
     __shared__ __attribute__((aligned(16))) uint64_t lds[256 * 32 + WAVES * 1024];
     for (int i = threadIdx.x; i < 256 * 32; i += blockDim.x) lds[i] = kGear[i >> 5] << 16;
@@ -976,10 +979,12 @@ __global__ __launch_bounds__(64 * WAVES) void cdc_walk_scan_kernel(CdcFiles f, C
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot is free for the next DMA
         const uint32_t CL = RL;
         const bool CV = RV && !L.done;
-        RL = L.done ? kWalkOob : NL;
-        RV = !L.done;
-        if (!L.done) NL += 128;
-        dma(RL);
+        if constexpr (!LATE) {
+            RL = L.done ? kWalkOob : NL;
+            RV = !L.done;
+            if (!L.done) NL += 128;
+            dma(RL);
+        }
         // this round's mask (see above); tests at positions < lo or >= tL are rejected when resolved
         uint32_t m;
         if (!CV || CL + 128 <= L.lo) m = kWalkFull;
@@ -1050,6 +1055,12 @@ __global__ __launch_bounds__(64 * WAVES) void cdc_walk_scan_kernel(CdcFiles f, C
             walk_begin_chunk(L, prm, out);
             if (!L.done) NL = (L.cs + a0) & ~127u;
             RV = false;
+        }
+        if constexpr (LATE) {
+            RL = L.done ? kWalkOob : NL;
+            RV = !L.done;
+            if (!L.done) NL += 128;
+            dma(RL);
         }
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // the last (empty) DMA has landed before the slot goes away
@@ -1553,7 +1564,9 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
         // W: one lane per section; X twice (every section, then the ones whose assumed entry turned out
         // wrong); the serial pass for whatever is left; then the chunk counts' prefix
         const uint64_t nwaves = (n_sec + 63) / 64;
-        hipLaunchKernelGGL(oxh::cdc_walk_scan_kernel<oxh::kScanWaves>,
+        static const bool late = getenv("OXH_CDC_WALK_LATE") && atoi(getenv("OXH_CDC_WALK_LATE")) != 0;
+        auto walk_kernel = late ? oxh::cdc_walk_scan_kernel<oxh::kScanWaves, true> : oxh::cdc_walk_scan_kernel<oxh::kScanWaves, false>;
+        hipLaunchKernelGGL(walk_kernel,
                            dim3((unsigned)((nwaves + oxh::kScanWaves - 1) / oxh::kScanWaves)), dim3(64 * oxh::kScanWaves), 0, st,
                            f, prm, n_sec, oxh::WalkGeom{arena_bytes});
         CDC_HIP(hipGetLastError());

@@ -16,6 +16,10 @@ seals early and takes the large-file path), one default. Requests, picked at ran
   modified   oxh_files_modified: equal sizes, drifted mtimes, node hashes right or off by one
   utf8       oxh_hash_files_text_utf8 (digests, counts and the is_utf8 sniff)
   pool       the reader-process pool (oxh_pool, 2 helpers) over a random subset
+--regrow: a thread keeps creating a context with 1 MiB staging slots, hashing 1, 2, then 4 of the
+corpus's large files side by side (each step regrows the context's large-file piece buffers:
+stream-ordered, no device-wide sync) and destroying it again -- while the other threads (and any
+device-resident callers in other processes) run.
 --mutate: a mutator thread atomically replaces files of a hot tenth of the corpus (sizes across the
 1 MiB slot too) while the requests run; a digest must then be one of the file's versions (no torn
 read: the engine's re-read on a size change, read to EOF) with that version's counts and is_utf8.
@@ -47,6 +51,8 @@ def main():
     ap.add_argument("--mutate", action="store_true",
                     help="a thread keeps replacing 10 %% of the files (new content, temp + rename): every digest must be "
                          "one of that file's versions, with that version's text counts and is_utf8")
+    ap.add_argument("--regrow", action="store_true",
+                    help="a thread keeps creating contexts whose large-file piece buffers regrow (1, 2, 4 files side by side)")
     a = ap.parse_args()
 
     import numpy as np
@@ -229,6 +235,25 @@ def main():
                     checked[0] += n_ok
 
         mutations = [0]
+        regrows = [0]
+
+        def regrower():
+            r = random.Random(a.seed + 7)
+            big = [p for p in stable if os.path.getsize(p) > (1 << 20)]
+            while time.time() < deadline and not fails and big:
+                c = _capi.Context(0, staging_bytes=1 << 20)
+                try:
+                    for k in (1, 2, 4):
+                        q = [r.choice(big) for _ in range(k)]
+                        dg, _, st = hasher.hash_files_128bit(q, c)
+                        for p, d, s_ in zip(q, dg, st):
+                            if s_ != 0 or d != want[p]:
+                                fail(f"regrow: {p} status {s_} digest {d}")
+                        with lock:
+                            checked[0] += len(q)
+                finally:
+                    c.close()
+                regrows[0] += 1
 
         def mutator():
             r = random.Random(a.seed + 99)
@@ -249,6 +274,8 @@ def main():
         ths = [threading.Thread(target=worker, args=(t,)) for t in range(a.threads)]
         if a.mutate:
             ths.append(threading.Thread(target=mutator))
+        if a.regrow:
+            ths.append(threading.Thread(target=regrower))
         t0 = time.time()
         for th in ths:
             th.start()
@@ -262,6 +289,7 @@ def main():
             c.close()
         pool.close()
         res = {"seconds": round(time.time() - t0, 1), "threads": a.threads, "files": a.files, "mutations": mutations[0],
+               "regrow_contexts": regrows[0], "big_piece_mib": os.environ.get("OXH_BIG_PIECE_MIB", "1024 (default)"),
                "requests": counts, "items_checked": checked[0], "failures": len(fails), "first_failures": fails[:5]}
         print(json.dumps(res), flush=True)
         sys.exit(1 if fails else 0)
