@@ -112,6 +112,24 @@ def test_big_file_allocation_failure_is_per_file(cuda, oracle_lib, tmp_path, mon
             assert f.read() == big
 
 
+def test_big_files_fall_back_to_fewer_side_by_side(cuda, oracle_lib, tmp_path, monkeypatch):
+    """large files share one piece pipeline, 2 device piece buffers each. When the buffers
+    for all of them do not fit (here 4 files x 2 x 40 GiB pieces, more than the device holds), the
+    engine takes fewer side by side, down to one, instead of failing every file with OXH_ERR_NOMEM."""
+    from oracle import oracle
+    from oxen_amd import _capi, hasher
+
+    from oxen_amd.workloads import splitmix_bytes
+
+    bigs = [splitmix_bytes(800 + k, 0, (5 << 20) + 1000 * k + 7).tobytes() for k in range(4)]
+    paths = [_write(tmp_path, f"b{k}", b) for k, b in enumerate(bigs)]
+    monkeypatch.setenv("OXH_BIG_FILES", "4")
+    monkeypatch.setenv("OXH_BIG_PIECE_MIB", str(40 << 10))
+    with _capi.Context(0, staging_bytes=4 << 20) as c:
+        d, sz, st = hasher.hash_files_128bit(paths, c)
+    assert st == [0] * 4 and d == [oracle.xxh3_128_int(b) for b in bigs]
+
+
 def test_files_are_read_to_eof_whatever_the_stat_size(cuda, oracle_lib, tmp_path):
     """read_to_end semantics (hasher.rs:126-148): /proc/version stats as 0 bytes but reads as text;
     the fstat path and the caller-metadata path both hash what the read returns."""

@@ -53,7 +53,8 @@ def sharded(a, paths, meta, nbytes, cpu_call, drop_cache):
     blob, offs = pack_paths(paths)  # packed once, outside the timing (as c_paths is)
     for P in [int(x) for x in a.procs.split(",") if x]:
         th = max(1, a.threads // P)
-        pools = {"gpu": ShardedFileHasher(procs=P, threads=th, staging_bytes=a.pool_staging_mib << 20),
+        devs = tuple(int(x) for x in a.devices.split(","))
+        pools = {"gpu": ShardedFileHasher(procs=P, devices=devs, threads=th, staging_bytes=a.pool_staging_mib << 20),
                  "cpu": CpuShardedLoop(procs=P, threads=th)}
         try:
             ts = {"gpu": [], "cpu": []}
@@ -94,6 +95,7 @@ def main():
     ap.add_argument("--procs", default="2,4", help="reader process counts for the sharded runs")
     ap.add_argument("--only-procs", action="store_true", help="skip the add / fsck / staging parts")
     ap.add_argument("--pool-staging-mib", type=int, default=0, help="staging slot size of the pool's helpers (0 = default)")
+    ap.add_argument("--devices", default="0", help="GPUs of the pool's helpers (helper p on devices[p %% len]), e.g. 0,1,2,3,4,5,6,7")
     a = ap.parse_args()
 
     import numpy as np
