@@ -1239,16 +1239,30 @@ __device__ void x_section(const CdcFiles& f, const CdcParams& prm, const CdcStit
     uint64_t p = e;
     uint32_t j = k0, n = 0;
     while (p < E) {
-        if (lane == 0 && n < prm.speccap) fix[n] = (uint32_t)(p - S);
-        ++n;
         if (j != kNoCut && j + 1 < nl) {
-            if (tcl[j] == kNoCut) {
-                ++j;
-                p = S + lst[j];
-                continue;
+            // p = list entry j: entries j .. r-1 up to the next inexact one (r), all inside the section
+            // (only the list's last entry, the exit, is past its end), are true starts: copied at once
+            uint32_t r = nl - 1;
+            for (uint32_t b = j; b < nl - 1; b += 64) {
+                const uint32_t k = b + (uint32_t)lane;
+                const uint64_t badm = __builtin_amdgcn_ballot_w64(k < nl - 1 && tcl[k] != kNoCut);
+                if (badm) {
+                    r = b + (uint32_t)__builtin_ctzll(badm);
+                    break;
+                }
             }
-            p = S + tcl[j];
+            for (uint32_t k = j + (uint32_t)lane; k < r; k += 64)
+                if (n + (k - j) < prm.speccap) fix[n + (k - j)] = lst[k];
+            n += r - j;
+            p = S + lst[r];
+            if (r == nl - 1) break;  // the exit
+            // entry r is a true start whose truncated window cuts it short
+            if (lane == 0 && n < prm.speccap) fix[n] = lst[r];
+            ++n;
+            p = S + tcl[r];
         } else {
+            if (lane == 0 && n < prm.speccap) fix[n] = (uint32_t)(p - S);
+            ++n;
             p += cut_coop(fbase, flen, p, prm, xm, gear);
         }
         j = lookup(p);
