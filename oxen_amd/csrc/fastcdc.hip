@@ -51,7 +51,7 @@ namespace oxh {
 
 int set_error(int code, const std::string& msg);  // oxen_hash_capi.hip: oxh_last_error() text
 int k1_packed(const void* d_arena, const uint64_t* d_offsets, const uint64_t* d_lens, uint64_t n, uint64_t* d_out,
-              int waves, hipStream_t st);  // oxen_hash_capi.hip
+              uint64_t mean_len, hipStream_t st);  // oxen_hash_capi.hip
 
 // fastcdc::v2020::MASKS, indexed by the number of one bits (entries 0..4 are padding)
 static constexpr uint64_t kCdcMasks[26] = {
@@ -1638,13 +1638,11 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
         CDC_HIP(hipGetLastError());
     }
     if (d_digests && total) {
-        // chunks sit back to back at arbitrary byte offsets: the block-wise K1 (OXH_MODE_WAVE_PACKED's
-        // kernel); at a mean chunk below 16 KiB two chunks per workgroup instead of four, so a
-        // workgroup's slot waits on fewer ragged chunks (+2-3 % on packed 4-16 KiB items,
-        // profiles/r03c_k1_wg_waves.txt)
+        // chunks sit back to back at arbitrary byte offsets: K1R at small chunks, the block-wise K1
+        // otherwise (oxh::k1_packed)
         uint64_t bytes = 0;
         for (uint64_t i = 0; i < n; ++i) bytes += lens[i];
-        rc = oxh::k1_packed(d_arena, d_chunk_offsets, d_chunk_lens, total, d_digests, bytes / total < 16384 ? 2 : 4, st);
+        rc = oxh::k1_packed(d_arena, d_chunk_offsets, d_chunk_lens, total, d_digests, bytes / total, st);
         if (rc) return cdc_fail(rc, std::string("chunk digests: ") + oxh_last_error());
     }
     CDC_HIP(hipStreamSynchronize(st));

@@ -105,6 +105,9 @@ WaveKernel wave_kernel_for(int variant) {
         case 74: return oxh::xxh3_wave_kernel<DESC, 74>;
         case 40: return oxh::xxh3_wave_kernel<DESC, 40>;
         case 104: return oxh::xxh3_wave_kernel<DESC, 104>;
+        case 256: return oxh::xxh3_wave_kernel<DESC, 256>;
+        case 260: return oxh::xxh3_wave_kernel<DESC, 260>;
+        case 264: return oxh::xxh3_wave_kernel<DESC, 264>;
         default: return oxh::xxh3_wave_kernel<DESC, 0>;
     }
 }
@@ -126,6 +129,7 @@ constexpr uint64_t kShortItemBytes = 16384;
 constexpr int kVariantShort = 72;    // Cfg: row-wise, depth 2, keys in LDS
 constexpr int kVariantLong = 8;      // Cfg: row-wise, depth 2, keys from the constant table
 constexpr int kVariantPacked = 104;  // Cfg: block-wise, depth 2, keys in LDS
+constexpr int kVariantRows = 264;    // Cfg: K1R (a 16-lane row per item), depth 2
 
 enum class ItemShape { Long, Short, Packed };
 
@@ -135,18 +139,22 @@ int pick_variant(ItemShape shape) {
     return shape == ItemShape::Packed ? kVariantPacked : shape == ItemShape::Short ? kVariantShort : kVariantLong;
 }
 int pick_variant(bool short_items) { return pick_variant(short_items ? ItemShape::Short : ItemShape::Long); }
+// K1R variants (bit 8) hash four items per wave, one per 16-lane row
+uint64_t items_per_wave(int variant) { return (variant & 256) ? 4 : 1; }
 
 // K1 over a descriptor table: one 64-lane wave per item, 4 waves per 256-thread workgroup.
 int launch_wave(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens, uint64_t n, uint64_t* out,
-                hipStream_t st, ItemShape shape = ItemShape::Long, int waves = 4) {
+                hipStream_t st, ItemShape shape = ItemShape::Long, int waves = 4, int variant = 0) {
     if (n == 0) return OXH_OK;
     // waves (items) per workgroup: 4, or the caller's choice; OXH_K1_WG_WAVES (1, 2 or 4) overrides
     // both for A/B. A workgroup's slot is freed only when its longest item is done.
     const char* wg = getenv("OXH_K1_WG_WAVES");
     const int e = wg ? atoi(wg) : 0;
     const int w = (e == 1 || e == 2 || e == 4) ? e : (waves == 1 || waves == 2) ? waves : 4;
-    const uint64_t blocks = (n + w - 1) / w;
-    hipLaunchKernelGGL(wave_kernel_for<true>(pick_variant(shape)), dim3((unsigned)blocks), dim3(64 * w), 0, st, arena, offs,
+    const int v = (variant && g_variant.load() == 0) ? variant : pick_variant(shape);
+    const uint64_t per_wg = (uint64_t)w * items_per_wave(v);
+    const uint64_t blocks = (n + per_wg - 1) / per_wg;
+    hipLaunchKernelGGL(wave_kernel_for<true>(v), dim3((unsigned)blocks), dim3(64 * w), 0, st, arena, offs,
                        lens, n, (uint64_t)0, (uint64_t)0, out);
     HIP_TRY(hipGetLastError());
     return OXH_OK;
@@ -179,8 +187,10 @@ int launch_text(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens
 // Fixed-size chunks of one buffer (no descriptor table): chunk i = [i*chunk, min((i+1)*chunk, total)).
 int launch_chunks(const uint8_t* buf, uint64_t n, uint64_t chunk, uint64_t total, uint64_t* out, hipStream_t st) {
     if (n == 0) return OXH_OK;
-    const uint64_t blocks = (n + 3) / 4;
-    hipLaunchKernelGGL(wave_kernel_for<false>(pick_variant(chunk <= kShortItemBytes)), dim3((unsigned)blocks), dim3(256), 0, st, buf,
+    const int v = pick_variant(chunk <= kShortItemBytes);
+    const uint64_t per_wg = 4 * items_per_wave(v);
+    const uint64_t blocks = (n + per_wg - 1) / per_wg;
+    hipLaunchKernelGGL(wave_kernel_for<false>(v), dim3((unsigned)blocks), dim3(256), 0, st, buf,
                        (const uint64_t*)nullptr, (const uint64_t*)nullptr, n, chunk, total, out);
     HIP_TRY(hipGetLastError());
     return OXH_OK;
@@ -959,11 +969,16 @@ int large_item(oxh_ctx* c, uint64_t L, LargeSource& src, bool want_counts, bool 
 }  // namespace
 
 namespace oxh {
-// FastCDC's K1 pass (fastcdc.hip): the block-wise K1 over the packed chunk table, `waves` chunks per
-// workgroup (2 when the mean chunk is small: tools/k1_small_probe.py)
+// FastCDC's K1 pass (fastcdc.hip) over the packed chunk table. Below a 16 KiB mean chunk K1R (four
+// chunks per wave, one per 16-lane row: tools/k1_small_probe.py, profiles/r04g_k1_small_probe.json),
+// otherwise the block-wise K1 (one chunk per wave; K1R's four streams per wave lose 10 % on 16-128 KiB
+// items); 2 waves per workgroup below 16 KiB, else 4. OXH_K1_PACKED_VARIANT forces a K1 shape (A/B).
 int k1_packed(const void* d_arena, const uint64_t* d_offsets, const uint64_t* d_lens, uint64_t n, uint64_t* d_out,
-              int waves, hipStream_t st) {
-    return launch_wave((const uint8_t*)d_arena, d_offsets, d_lens, n, d_out, st, ItemShape::Packed, waves);
+              uint64_t mean_len, hipStream_t st) {
+    const bool small = mean_len < kShortItemBytes;
+    const char* e = getenv("OXH_K1_PACKED_VARIANT");
+    const int v = (e && atoi(e)) ? atoi(e) : small ? kVariantRows : kVariantPacked;
+    return launch_wave((const uint8_t*)d_arena, d_offsets, d_lens, n, d_out, st, ItemShape::Packed, small ? 2 : 4, v);
 }
 }  // namespace oxh
 

@@ -96,6 +96,8 @@ __device__ __forceinline__ void bcast_rows64(uint64_t x, uint64_t t[4], int lane
 //             instruction. At a start that is not 128-B aligned a row-wise instruction touches 12
 //             lines per KiB, a block-wise one 9 (tools/k1_small_probe.py).
 //   bit 6     1 = stripe keys read from an LDS copy of the secret at each use (fewer VGPRs)
+//   bit 8     1 = K1R, one 16-lane row per item and four items per wave (rows_item below; bits 1-3
+//             as above, the others unused)
 // Measured on MI355X (C2, tools/readbw.py, profiles/r01_readbw*.json): nt loads ~+11 % over
 // default-policy loads; 4 rounds in flight (2 waves/SIMD at 180 VGPRs) ~+4 % over 2 rounds (5 waves/SIMD).
 template <int V>
@@ -106,6 +108,7 @@ struct Cfg {
     static constexpr bool KEYS_LDS = ((V >> 6) & 1) != 0;
     static constexpr bool STAGGER = ((V >> 4) & 1) != 0;
     static constexpr bool BLOCKWISE = ((V >> 5) & 1) != 0;
+    static constexpr bool ROWS = ((V >> 8) & 1) != 0;
 };
 
 template <bool ALIGNED, bool NT = false>
@@ -477,13 +480,194 @@ __device__ __forceinline__ void wave_item(const uint8_t* __restrict__ arena, con
     else wave_long<VARIANT, TEXT, false>(p, len, o, lane, lds_sec, TEXT ? counts + 2 * item : nullptr);
 }
 
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// K1R: one 16-lane row per item, four items per wave -- small items packed back to back (FastCDC
+// chunks). Row g = lane/16 owns item 4w + g; inside the row q = (lane/4)%4 and k = lane%4 as in K1.
+// One iteration moves every row one 1 KiB block along its own item: load j (0..3) reads 16 B at
+// block + (4j+q)*64 + 16k, 256 contiguous bytes of the row's item per instruction, and the lane sums
+// stripes {q, q+4, q+8, q+12}; two DPP row rotations finish the block sum inside the row and the
+// row's lanes run that block's scramble for their 2 accumulators. Nothing crosses a row. K1 on such
+// items issues ~290 VALU instructions per 4 KiB round -- the reduce-scatter and broadcast across rows
+// and 4 chain steps per round on every lane -- and is VALU-issue bound there (SQ_ACTIVE_INST_VALU at
+// the SIMDs' issue capacity, profiles/r04e_cdc_pmc.txt); here a 4 KiB iteration (one block of each
+// of 4 items) costs about a third of that.
+// The four items run in lockstep to the wave's longest one; a row whose item is done idles (its loads
+// go to kOOB and are dropped). All rows address their items through ONE buffer descriptor (it is
+// wave-uniform) over [lowest start, highest end) of the four; items further apart than that allows
+// (not the case in a chunk table) are hashed by one lane each (correct, slow: K1 is the shape for
+// such batches). Byte-shifted items load from the dword below their start and re-align in registers with
+// v_alignbyte_b32 (the shift is per lane, 0 for aligned items), as K1's BS path does.
+template <bool DESC, int VARIANT>
+__device__ __forceinline__ void rows_item(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offsets,
+                                          const uint64_t* __restrict__ lens, uint64_t n, uint64_t chunk,
+                                          uint64_t total, uint64_t* __restrict__ out) {
+    constexpr int D = Cfg<VARIANT>::DEPTH;
+    constexpr bool NT = Cfg<VARIANT>::NT;
+    const int lane = threadIdx.x & 63;
+    const int q = (lane >> 2) & 3, k = lane & 3, tr = lane & 15;
+    const bool row_head = tr == 0, row_tail = tr == 15;
+    const uint64_t first =
+        ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * 4;
+    if (first >= n) return;
+    const uint64_t item = first + (uint64_t)(lane >> 4);
+    const bool valid = item < n;
+    uint64_t off = 0, len = 0;
+    if (valid) {
+        if constexpr (DESC) {
+            off = offsets[item];
+            len = lens[item];
+        } else {
+            off = item * chunk;
+            len = (total - off < chunk) ? total - off : chunk;
+        }
+    }
+    const bool lng = valid && len > 240;
+    const uint64_t start = reinterpret_cast<uint64_t>(arena + off);
+    // loads start at the item's dword boundary, bs bytes before the item
+    const uint32_t bs = (uint32_t)(start & 3);
+    const uint64_t astart = start - bs;
+    // the four rows' long items under one descriptor: [lowest aligned start, highest end)
+    uint64_t wlo = ~0ull, whi = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint64_t a = readlane64(lng ? astart : ~0ull, 16 * r);
+        const uint64_t e = readlane64(lng ? start + len : 0, 16 * r);
+        wlo = a < wlo ? a : wlo;
+        whi = e > whi ? e : whi;
+    }
+    if (whi != 0 && whi - wlo >= (1ull << 32) - (1ull << 20)) {
+        // items too far apart for one descriptor (not a chunk table): each row's first lane hashes
+        // its item alone -- correct for any layout, slow; K1 (one wave per item) is the path for that
+        if (valid && row_head) {
+            const U128 h = xxh3_lane_any(arena + off, len);
+            out[2 * item] = h.lo;
+            out[2 * item + 1] = h.hi;
+        }
+        return;
+    }
+    uint64_t key0[4], key1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        key0[j] = kSecW[4 * j + q + 2 * k];
+        key1[j] = kSecW[4 * j + q + 2 * k + 1];
+    }
+    const uint64_t sk0 = kSecW[16 + 2 * k], sk1 = kSecW[16 + 2 * k + 1];
+    if (whi != 0) {
+        const bool act = lng;
+        const uint64_t base = wlo, span = (whi - wlo + 3) & ~3ull;
+        const uint32_t vb = act ? (uint32_t)(astart - base) : 0;  // < 4 GiB - 1 MiB
+        // blocks followed by a scramble (< 2^32: an item below 4 TiB) and stripes of block nb
+        const uint32_t nb = act ? (uint32_t)((len - 1) >> 10) : 0;
+        const uint32_t ns = act ? (uint32_t)(((len - 1) - ((uint64_t)nb << 10)) >> 6) : 0;
+        uint32_t B = 0;  // the pass's last iteration: its longest item's partial block
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)nb, 16 * r);
+            B = x > B ? x : B;
+        }
+        const bool shifted = act && bs != 0;
+        // pieces j < jpart of the partial block are live (stripe 4j+q < ns)
+        const uint32_t jpart = act ? (ns > (uint32_t)q ? (ns - (uint32_t)q + 3) >> 2 : 0u) : 0u;
+        uint64_t a0 = kInitW[2 * k], a1 = kInitW[2 * k + 1];
+        // pieces j < live_n(b) of iteration b are live: 4 in a full block, jpart in the partial one
+        auto live_n = [&](uint32_t b) -> uint32_t { return (act & (b < nb)) ? 4u : (b == nb) ? jpart : 0u; };
+        const __amdgpu_buffer_rsrc_t rsrc =
+            __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), (short)0, (int)(uint32_t)span, kRsrcFlags);
+        // Byte-shifted rows load every piece 4 bytes late: the lane then holds dwords w1..w4 of the
+        // five its piece spans (w0 = the dword holding the piece's first byte) and takes w0 from the
+        // previous lane's w4 (DPP row_ror:1); the row's first lane takes it from the last lane of the
+        // previous load, and for load 0 from the previous iteration (`carry`; before the first, one
+        // dword load). No load ever reads past a live piece, and no extra loads are needed per
+        // iteration. v_perm_b32 then picks bytes bs..bs+3 of each dword pair; an aligned row loads on
+        // time and picks bytes 4..7 (the loaded dword itself).
+        const uint32_t late = shifted ? 4u : 0u;
+        const uint32_t psel = 0x03020100u + 0x01010101u * (shifted ? bs : 4u);
+        auto load_iter = [&](uint32_t b, uint4 (&dst)[4]) {
+            const uint32_t vo = vb + (b << 10) + (uint32_t)(q * 64 + k * 16) + late;
+            const uint32_t jn = live_n(b);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) dst[j] = bload16<NT>(rsrc, (uint32_t)j < jn ? vo + (uint32_t)j * 256u : kOOB);
+        };
+        uint32_t carry = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (shifted & row_head) ? vb : kOOB, 0, 0);
+        auto fold = [&](uint4 (&src)[4], uint32_t b) {
+            uint32_t pw[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pw[j] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)src[j].w, 0x121, 0xf, 0xf, false);
+            const uint32_t jn = live_n(b);
+            uint64_t s0 = 0, s1 = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t w0 = row_head ? (j == 0 ? carry : pw[j - 1]) : pw[j];
+                const uint4 a = src[j];
+                const uint4 d = make_uint4(__builtin_amdgcn_perm(a.x, w0, psel), __builtin_amdgcn_perm(a.y, a.x, psel),
+                                           __builtin_amdgcn_perm(a.z, a.y, psel), __builtin_amdgcn_perm(a.w, a.z, psel));
+                if ((uint32_t)j < jn) accum16(d, key0[j], key1[j], s0, s1);
+            }
+            carry = pw[3];
+            s0 += dpp64<DPP_ROW_ROR4>(s0);
+            s1 += dpp64<DPP_ROW_ROR4>(s1);
+            s0 += dpp64<DPP_ROW_ROR8>(s0);
+            s1 += dpp64<DPP_ROW_ROR8>(s1);
+            const bool full = act & (b < nb), part = act & (b == nb);
+            const uint64_t t0 = a0 + s0, t1 = a1 + s1;
+            const uint64_t c0 = scramble1(t0, sk0), c1 = scramble1(t1, sk1);
+            a0 = full ? c0 : (part ? t0 : a0);
+            a1 = full ? c1 : (part ? t1 : a1);
+        };
+        // the last stripe (at len - 64, secret offset 121), fetched with the first iterations
+        const uint4 last = bload16<false>(rsrc, act ? vb + bs + (uint32_t)len - 64 + 16 * (uint32_t)k : kOOB);
+        {
+            uint4 ring[D][4];
+#pragma unroll
+            for (int d = 0; d < D; ++d) load_iter((uint32_t)d, ring[d]);
+            // one loop to the end, the last group's folds guarded: with a separate tail after the loop
+            // hipcc copied the whole ring at loop entry (an LDS re-alignment form went 108 -> 156 VGPRs)
+            for (uint32_t b = 0; b <= B; b += D) {
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    if (b + d <= B) fold(ring[d], b + d);
+                    load_iter(b + d + D, ring[d]);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }
+        {
+            const uint64_t w0 = ((uint64_t)last.y << 32) | last.x, w1 = ((uint64_t)last.w << 32) | last.z;
+            const uint64_t k0 = w0 ^ kLastW[2 * k], k1 = w1 ^ kLastW[2 * k + 1];
+            a0 += mul32x32(k0) + w1;
+            a1 += mul32x32(k1) + w0;
+        }
+        uint64_t mlo = mul_fold64(a0 ^ kMrgLo[2 * k], a1 ^ kMrgLo[2 * k + 1]);
+        uint64_t mhi = mul_fold64(a0 ^ kMrgHi[2 * k], a1 ^ kMrgHi[2 * k + 1]);
+        mlo += dpp64<DPP_QUAD_XOR1>(mlo);
+        mhi += dpp64<DPP_QUAD_XOR1>(mhi);
+        mlo += dpp64<DPP_QUAD_XOR2>(mlo);
+        mhi += dpp64<DPP_QUAD_XOR2>(mhi);
+        if (act && row_head) {
+            out[2 * item] = avalanche_xxh3(len * P64_1 + mlo);
+            out[2 * item + 1] = avalanche_xxh3(~(len * P64_2) + mhi);
+        }
+    }
+    if (valid && !lng && row_head) {
+        const U128 h = xxh3_lane_short(arena + off, len);
+        out[2 * item] = h.lo;
+        out[2 * item + 1] = h.hi;
+    }
+}
+
 template <bool DESC, int VARIANT>
 __global__ __launch_bounds__(256) void xxh3_wave_kernel(const uint8_t* __restrict__ arena,
                                                         const uint64_t* __restrict__ offsets,
                                                         const uint64_t* __restrict__ lens, uint64_t n,
                                                         uint64_t chunk, uint64_t total,
                                                         uint64_t* __restrict__ out) {
-    wave_item<DESC, VARIANT, false>(arena, offsets, lens, n, chunk, total, out, nullptr);
+    if constexpr (Cfg<VARIANT>::ROWS) rows_item<DESC, VARIANT>(arena, offsets, lens, n, chunk, total, out);
+    else wave_item<DESC, VARIANT, false>(arena, offsets, lens, n, chunk, total, out, nullptr);
 }
 
 // K1T: K1 + text metadata counts in the same HBM pass (descriptor tables only).
@@ -831,6 +1015,12 @@ template __global__ void xxh3_wave_kernel<true, 104>(const uint8_t*, const uint6
 template __global__ void xxh3_wave_kernel<false, 104>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 template __global__ void xxh3_wave_kernel<true, 74>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 template __global__ void xxh3_wave_kernel<false, 74>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<true, 256>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<false, 256>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<true, 260>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<false, 260>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<true, 264>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<false, 264>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 template __global__ void xxh3_text_wave_kernel<0>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t*, uint64_t*);
 template __global__ void xxh3_text_wave_kernel<72>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t*, uint64_t*);
 template __global__ void xxh3_text_wave_kernel<8>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t*, uint64_t*);

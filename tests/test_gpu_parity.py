@@ -39,7 +39,8 @@ def _mismatch(got, want, lens):
     return [int(lens[i]) for i in bad[:20]]
 
 
-VARIANTS = [0, 1, 2, 4, 8, 12, 40, 64, 72, 74, 104]  # K1 variants (xxh3_kernels.hip Cfg); 0 is the shipped path
+# K1 variants (xxh3_kernels.hip Cfg; 0 is the shipped path); 256 / 260 / 264 are K1R (a row per item)
+VARIANTS = [0, 1, 2, 4, 8, 12, 40, 64, 72, 74, 104, 256, 260, 264]
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2, 3])
@@ -63,7 +64,7 @@ def test_every_length_unaligned(cuda, golden, mode, variant):
 
 
 @pytest.mark.parametrize("wg_waves", ["1", "2"])
-@pytest.mark.parametrize("variant", [0, 8, 72, 104])
+@pytest.mark.parametrize("variant", [0, 8, 72, 104, 264])
 def test_every_length_workgroup_width(cuda, golden, variant, wg_waves, monkeypatch):
     """K1 launched with 1 or 2 items (waves) per workgroup instead of 4 (OXH_K1_WG_WAVES): the item
     index comes from blockDim, so every item is still hashed exactly once; the ragged golden batch."""
@@ -182,19 +183,26 @@ def test_c2_full_size_sampled(cuda, oracle_lib):
     torch.cuda.empty_cache()
 
 
-def test_chunk_digests(cuda, oracle_lib):
+@pytest.mark.parametrize("variant", [0, 264, 136, 392])
+def test_chunk_digests(cuda, oracle_lib, variant):
+    """Fixed-size chunk digests (no descriptor table), with the default K1 and with K1R forced."""
     import torch
 
+    from oxen_amd import _capi
     from oxen_amd.device import chunk_digests_device, fill_splitmix
 
     n = (5 << 20) + 123
     buf = torch.empty((n + 7) // 8 * 8, dtype=torch.uint8, device=cuda)
     fill_splitmix(buf, 77)
     host = buf[:n].cpu().numpy()
-    for chunk in [8192, 65536, 1000]:
-        got = _u64(chunk_digests_device(buf, chunk, nbytes=n))
-        want = oracle_lib.chunk_digests(host, chunk, threads=8)
-        assert np.array_equal(got, want), chunk
+    prev = _capi.lib().oxh_set_kernel_variant(variant)
+    try:
+        for chunk in [8192, 65536, 1000, 200, 1 << 20]:
+            got = _u64(chunk_digests_device(buf, chunk, nbytes=n))
+            want = oracle_lib.chunk_digests(host, chunk, threads=8)
+            assert np.array_equal(got, want), chunk
+    finally:
+        _capi.lib().oxh_set_kernel_variant(prev)
 
 
 @pytest.mark.parametrize("piece_mib", [None, "1", "3"], ids=["one-piece", "1MiB-pieces", "3MiB-pieces"])
@@ -963,6 +971,65 @@ def test_files_modified_metadata_hash_step(oracle_lib, tmp_path, cuda):
         assert not hasher.classify_modified_from_node_with_metadata(paths[0], 0, committed[0], os.stat(paths[0]), False,
                                                                     node_metadata_hash=_text_meta_hash(oracle_lib, b""),
                                                                     file_metadata=meta)
+
+
+@pytest.mark.parametrize("variant", [0, 264, 260, 256])
+def test_k1r_lockstep_rows(cuda, oracle_lib, variant):
+    """K1R runs a wave's four items in lockstep to the longest: MiB items next to tiny ones, short-path
+    items (<= 240 B) in the same wave, every byte shift, a batch size that leaves the last wave with 1-3
+    rows, and items in reverse order and overlapping (the descriptor spans [lowest start, highest end))."""
+    import torch
+
+    from oxen_amd import _capi
+    from oxen_amd.device import fill_splitmix, xxh3_128_batch_device
+
+    rng = np.random.default_rng(264)
+    lens = rng.integers(241, 12_000, 4001).astype(np.uint64)
+    lens[5::16] = rng.integers(1 << 20, 3 << 20, len(lens[5::16]))
+    lens[7::9] = rng.integers(0, 241, len(lens[7::9]))
+    lens[::37] = 1024 * rng.integers(1, 9, len(lens[::37])) + rng.integers(0, 2, len(lens[::37]))  # block edges
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64) + 1
+    offs[1000:1400] = offs[1000:1400][::-1].copy()  # reverse order inside some waves
+    offs[2000:2100] = offs[2000]  # overlapping items
+    total = int((offs + lens).max()) + 64
+    arena = torch.empty(total, dtype=torch.uint8, device=cuda)
+    fill_splitmix(arena, 99)
+    prev = _capi.lib().oxh_set_kernel_variant(variant)
+    try:
+        got = _u64(xxh3_128_batch_device(arena, torch.from_numpy(offs.view(np.int64)).to(cuda),
+                                         torch.from_numpy(lens.view(np.int64)).to(cuda), mode=_capi.OXH_MODE_WAVE_PACKED))
+    finally:
+        _capi.lib().oxh_set_kernel_variant(prev)
+    want = oracle_lib.batch(arena.cpu().numpy(), offs, lens, threads=8)
+    bad = np.nonzero((got != want).any(axis=1))[0]
+    assert not len(bad), [(int(i), int(lens[i]), int(offs[i]) % 4) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("variant", [264, 260])
+def test_k1r_items_far_apart(cuda, oracle_lib, variant):
+    """K1R with a wave's items more than 4 GiB apart (one descriptor cannot span them): each row's item
+    is hashed alone, still bit-exact."""
+    import torch
+
+    from oxen_amd import _capi
+    from oxen_amd.device import fill_splitmix, xxh3_128_batch_device
+
+    size = (4 << 30) + (64 << 20)
+    arena = torch.empty(size, dtype=torch.uint8, device=cuda)
+    fill_splitmix(arena, 5)
+    offs = np.array([3, (4 << 30) + 17, 1 << 20, (4 << 30) + (1 << 20) + 2, 77, 5000], dtype=np.uint64)
+    lens = np.array([70_001, 5_000, 200, 1 << 20, 1025, 90], dtype=np.uint64)
+    prev = _capi.lib().oxh_set_kernel_variant(variant)
+    try:
+        got = _u64(xxh3_128_batch_device(arena, torch.from_numpy(offs.view(np.int64)).to(cuda),
+                                         torch.from_numpy(lens.view(np.int64)).to(cuda), mode=_capi.OXH_MODE_WAVE_PACKED))
+    finally:
+        _capi.lib().oxh_set_kernel_variant(prev)
+    for i, (o, L) in enumerate(zip(offs, lens)):
+        b = arena[int(o):int(o) + int(L)].cpu().numpy().tobytes()
+        assert (int(got[i, 0]), int(got[i, 1])) == oracle_lib.xxh3_128(b), i
+    del arena
+    torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("mode", ["short", "packed", "auto"])

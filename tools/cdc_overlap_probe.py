@@ -1,5 +1,5 @@
-"""Does the FastCDC scan (F1, VALU-bound at ~55 % of HBM peak) overlap with K1 over the chunks
-(HBM-bound)? C5 shape (16 x 8 GiB device-resident), two ways:
+"""Does FastCDC chunking (the scan F1 or the walk W, both VALU-bound) overlap with K1 over the chunks
+(K1R: HBM/TA-bound, VALU issue ~55 %)? C5 shape (16 x 8 GiB device-resident), two ways:
 
   serial   one oxh_fastcdc_device call with digests (F1 -> F2/F3 -> emit -> K1 on one stream)
   overlap  files in G groups; group g is chunked (no digests) on stream A while K1 hashes group
@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cu-split", default="0", help="comma list of k: stream A gets CUs with i %% 8 < k, "
                     "stream B the rest (hipExtStreamCreateWithCUMask); 0 = unmasked torch streams")
+    ap.add_argument("--k1-variant", type=int, default=0,
+                    help="K1 shape for the overlap runs' separate K1 launches (oxh_set_kernel_variant; 0 = "
+                    "OXH_MODE_WAVE_PACKED's default, 264 = K1R, the serial call's choice at small chunks)")
     args = ap.parse_args()
 
     import torch
@@ -85,6 +88,7 @@ def main():
         want = fp(dig, int(first[-1]))
         res[f"c{chunk}_serial_s"] = round(float(np.median(times)), 4)
         del out, dig
+        prev_variant = _capi.lib().oxh_set_kernel_variant(args.k1_variant)
         for split, G in [(k, int(g)) for k in splits for g in args.groups.split(",")]:
             if split:
                 sa = masked_stream([i for i in range(n_cu) if i % 8 < split])
@@ -114,8 +118,10 @@ def main():
             res[tag + "_s"] = round(float(np.median(times)), 4)
             res[tag + "_same"] = ok
             del outs
+        _capi.lib().oxh_set_kernel_variant(prev_variant)
         print(json.dumps(res), flush=True)
     res["GB"] = round(total / 1e9, 1)
+    res["k1_variant"] = args.k1_variant
     print(json.dumps(res), flush=True)
 
 
