@@ -141,6 +141,15 @@ int pick_variant(ItemShape shape) {
 int pick_variant(bool short_items) { return pick_variant(short_items ? ItemShape::Short : ItemShape::Long); }
 // K1R variants (bit 8) hash four items per wave, one per 16-lane row
 uint64_t items_per_wave(int variant) { return (variant & 256) ? 4 : 1; }
+// a variant wave_kernel_for instantiates, else 0 (its default kernel), so the launch geometry always
+// matches the kernel that runs
+int known_variant(int v) {
+    switch (v) {
+        case 1: case 2: case 4: case 8: case 12: case 40: case 64: case 72: case 74: case 104:
+        case 256: case 260: case 264: return v;
+        default: return 0;
+    }
+}
 
 // K1 over a descriptor table: one 64-lane wave per item, 4 waves per 256-thread workgroup.
 int launch_wave(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens, uint64_t n, uint64_t* out,
@@ -151,7 +160,7 @@ int launch_wave(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens
     const char* wg = getenv("OXH_K1_WG_WAVES");
     const int e = wg ? atoi(wg) : 0;
     const int w = (e == 1 || e == 2 || e == 4) ? e : (waves == 1 || waves == 2) ? waves : 4;
-    const int v = (variant && g_variant.load() == 0) ? variant : pick_variant(shape);
+    const int v = known_variant((variant && g_variant.load() == 0) ? variant : pick_variant(shape));
     const uint64_t per_wg = (uint64_t)w * items_per_wave(v);
     const uint64_t blocks = (n + per_wg - 1) / per_wg;
     hipLaunchKernelGGL(wave_kernel_for<true>(v), dim3((unsigned)blocks), dim3(64 * w), 0, st, arena, offs,
@@ -187,7 +196,7 @@ int launch_text(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens
 // Fixed-size chunks of one buffer (no descriptor table): chunk i = [i*chunk, min((i+1)*chunk, total)).
 int launch_chunks(const uint8_t* buf, uint64_t n, uint64_t chunk, uint64_t total, uint64_t* out, hipStream_t st) {
     if (n == 0) return OXH_OK;
-    const int v = pick_variant(chunk <= kShortItemBytes);
+    const int v = known_variant(pick_variant(chunk <= kShortItemBytes));
     const uint64_t per_wg = 4 * items_per_wave(v);
     const uint64_t blocks = (n + per_wg - 1) / per_wg;
     hipLaunchKernelGGL(wave_kernel_for<false>(v), dim3((unsigned)blocks), dim3(256), 0, st, buf,

@@ -183,9 +183,10 @@ def test_c2_full_size_sampled(cuda, oracle_lib):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("variant", [0, 264, 136, 392])
+@pytest.mark.parametrize("variant", [0, 264, 392])
 def test_chunk_digests(cuda, oracle_lib, variant):
-    """Fixed-size chunk digests (no descriptor table), with the default K1 and with K1R forced."""
+    """Fixed-size chunk digests (no descriptor table), with the default K1, with K1R forced, and with a
+    variant number that no kernel has (392: the default kernel runs, with its own launch geometry)."""
     import torch
 
     from oxen_amd import _capi
