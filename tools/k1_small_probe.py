@@ -9,6 +9,7 @@ Cases (~6.4 GB device-resident each, K1 = oxh_xxh3_128_batch_device, HIP events,
                   byte-shift path; 4 / 16 / 64 / 128: dword-aligned loads that straddle lines)
   cdc_packed      lengths uniform in [4 KiB, 16 KiB) packed back to back (FastCDC-like)
   cdc_256         the same lengths at 256-B alignment
+  cdc_packed_w64sort  cdc_packed, listed in length order within windows of 64 items (K1R lockstep)
   cdc64_packed / cdc64_256   lengths uniform in [4 KiB, 128 KiB) (FastCDC at 64 KiB), likewise
 PROBE_CASES=a,b limits the run to those cases. PROBE_WG=1,4 repeats every case with that many waves per
 K1 workgroup (OXH_K1_WG_WAVES), alternating.
@@ -69,6 +70,13 @@ def main():
     lens = lens[: np.searchsorted(np.cumsum((lens + 255) // 256 * 256), total)]
     layouts["cdc_packed"] = (np.concatenate([[0], np.cumsum(lens)[:-1]]), lens)
     layouts["cdc_256"] = (np.concatenate([[0], np.cumsum((lens + 255) // 256 * 256)[:-1]]), lens)
+    # the same packed items, listed (not moved) in length order within each window of 64 consecutive
+    # items: a K1R wave's four rows then carry items of similar length
+    o_p, l_p = layouts["cdc_packed"]
+    nwin = len(l_p) // 64 * 64
+    order = np.argsort(l_p[:nwin].reshape(-1, 64), axis=1, kind="stable") + (np.arange(nwin // 64) * 64)[:, None]
+    order = np.concatenate([order.ravel(), np.arange(nwin, len(l_p))])
+    layouts["cdc_packed_w64sort"] = (o_p[order], l_p[order])
     lens = rng.integers(4096, 131072, 2 * total // (4096 + 131072))
     lens = lens[: np.searchsorted(np.cumsum((lens + 255) // 256 * 256), total)]
     layouts["cdc64_packed"] = (np.concatenate([[0], np.cumsum(lens)[:-1]]), lens)
