@@ -108,6 +108,9 @@ WaveKernel wave_kernel_for(int variant) {
         case 256: return oxh::xxh3_wave_kernel<DESC, 256>;
         case 260: return oxh::xxh3_wave_kernel<DESC, 260>;
         case 264: return oxh::xxh3_wave_kernel<DESC, 264>;
+        case 768: return oxh::xxh3_wave_kernel<DESC, 768>;
+        case 772: return oxh::xxh3_wave_kernel<DESC, 772>;
+        case 776: return oxh::xxh3_wave_kernel<DESC, 776>;
         default: return oxh::xxh3_wave_kernel<DESC, 0>;
     }
 }
@@ -139,14 +142,15 @@ int pick_variant(ItemShape shape) {
     return shape == ItemShape::Packed ? kVariantPacked : shape == ItemShape::Short ? kVariantShort : kVariantLong;
 }
 int pick_variant(bool short_items) { return pick_variant(short_items ? ItemShape::Short : ItemShape::Long); }
-// K1R variants (bit 8) hash four items per wave, one per 16-lane row
-uint64_t items_per_wave(int variant) { return (variant & 256) ? 4 : 1; }
+// K1R variants (bit 8) hash four items per wave, one per 16-lane row; K1H (bits 8 and 9) two, one per
+// pair of rows
+uint64_t items_per_wave(int variant) { return (variant & 256) ? ((variant & 512) ? 2 : 4) : 1; }
 // a variant wave_kernel_for instantiates, else 0 (its default kernel), so the launch geometry always
 // matches the kernel that runs
 int known_variant(int v) {
     switch (v) {
         case 1: case 2: case 4: case 8: case 12: case 40: case 64: case 72: case 74: case 104:
-        case 256: case 260: case 264: return v;
+        case 256: case 260: case 264: case 768: case 772: case 776: return v;
         default: return 0;
     }
 }

@@ -98,6 +98,7 @@ __device__ __forceinline__ void bcast_rows64(uint64_t x, uint64_t t[4], int lane
 //   bit 6     1 = stripe keys read from an LDS copy of the secret at each use (fewer VGPRs)
 //   bit 8     1 = K1R, one 16-lane row per item and four items per wave (rows_item below; bits 1-3
 //             as above, the others unused)
+//   bit 9     K1R only: 1 = K1H, two rows per item and two items per wave
 // Measured on MI355X (C2, tools/readbw.py, profiles/r01_readbw*.json): nt loads ~+11 % over
 // default-policy loads; 4 rounds in flight (2 waves/SIMD at 180 VGPRs) ~+4 % over 2 rounds (5 waves/SIMD).
 template <int V>
@@ -109,6 +110,7 @@ struct Cfg {
     static constexpr bool STAGGER = ((V >> 4) & 1) != 0;
     static constexpr bool BLOCKWISE = ((V >> 5) & 1) != 0;
     static constexpr bool ROWS = ((V >> 8) & 1) != 0;
+    static constexpr bool ROWS2 = ((V >> 9) & 1) != 0;
 };
 
 template <bool ALIGNED, bool NT = false>
@@ -496,25 +498,33 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
 // and 4 chain steps per round on every lane -- and is VALU-issue bound there (SQ_ACTIVE_INST_VALU at
 // the SIMDs' issue capacity, profiles/r04e_cdc_pmc.txt); here a 4 KiB iteration (one block of each
 // of 4 items) costs about a third of that.
-// The four items run in lockstep to the wave's longest one; a row whose item is done idles (its loads
+// RPI = 2 (Cfg bit 9, "K1H"): two rows (32 lanes) per item, two items per wave. Load j (0..1) reads
+// 512 contiguous bytes of the item (5 lines when unaligned, against 2 x 3 for two row loads); the lane
+// sums stripes {t/4, 8 + t/4} (t = lane % 32); the block sum takes one permlane16 swap more, and each
+// item's chain runs once per block on its 32 lanes.
+// The items of a wave run in lockstep to the longest one; a row whose item is done idles (its loads
 // go to kOOB and are dropped). All rows address their items through ONE buffer descriptor (it is
-// wave-uniform) over [lowest start, highest end) of the four; items further apart than that allows
-// (not the case in a chunk table) are hashed by one lane each (correct, slow: K1 is the shape for
-// such batches). Byte-shifted items load from the dword below their start and re-align in registers with
-// v_alignbyte_b32 (the shift is per lane, 0 for aligned items), as K1's BS path does.
+// wave-uniform) over [lowest start, highest end) of the wave's items; items further apart than that
+// allows (not the case in a chunk table) are hashed by one lane each (correct, slow: K1 is the shape
+// for such batches). Byte-shifted items load from the dword below their start and re-align in
+// registers (the shift is per lane, 0 for aligned items).
 template <bool DESC, int VARIANT>
 __device__ __forceinline__ void rows_item(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offsets,
                                           const uint64_t* __restrict__ lens, uint64_t n, uint64_t chunk,
                                           uint64_t total, uint64_t* __restrict__ out) {
     constexpr int D = Cfg<VARIANT>::DEPTH;
     constexpr bool NT = Cfg<VARIANT>::NT;
+    constexpr int RPI = Cfg<VARIANT>::ROWS2 ? 2 : 1;  // 16-lane rows per item
+    constexpr int LPI = 16 * RPI;                      // lanes per item
+    constexpr int IPW = 4 / RPI;                       // items per wave
+    constexpr int NL = 4 / RPI;                        // loads per 1 KiB block, 256 * RPI bytes each
     const int lane = threadIdx.x & 63;
-    const int q = (lane >> 2) & 3, k = lane & 3, tr = lane & 15;
-    const bool row_head = tr == 0, row_tail = tr == 15;
+    const int t = lane & (LPI - 1), k = lane & 3, st0 = t >> 2;  // the lane's stripe in load j: 4*RPI*j + st0
+    const bool head = t == 0;
     const uint64_t first =
-        ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * 4;
+        ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * IPW;
     if (first >= n) return;
-    const uint64_t item = first + (uint64_t)(lane >> 4);
+    const uint64_t item = first + (uint64_t)(lane / LPI);
     const bool valid = item < n;
     uint64_t off = 0, len = 0;
     if (valid) {
@@ -531,30 +541,30 @@ __device__ __forceinline__ void rows_item(const uint8_t* __restrict__ arena, con
     // loads start at the item's dword boundary, bs bytes before the item
     const uint32_t bs = (uint32_t)(start & 3);
     const uint64_t astart = start - bs;
-    // the four rows' long items under one descriptor: [lowest aligned start, highest end)
+    // the wave's long items under one descriptor: [lowest aligned start, highest end)
     uint64_t wlo = ~0ull, whi = 0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const uint64_t a = readlane64(lng ? astart : ~0ull, 16 * r);
-        const uint64_t e = readlane64(lng ? start + len : 0, 16 * r);
+    for (int r = 0; r < IPW; ++r) {
+        const uint64_t a = readlane64(lng ? astart : ~0ull, LPI * r);
+        const uint64_t e = readlane64(lng ? start + len : 0, LPI * r);
         wlo = a < wlo ? a : wlo;
         whi = e > whi ? e : whi;
     }
     if (whi != 0 && whi - wlo >= (1ull << 32) - (1ull << 20)) {
-        // items too far apart for one descriptor (not a chunk table): each row's first lane hashes
-        // its item alone -- correct for any layout, slow; K1 (one wave per item) is the path for that
-        if (valid && row_head) {
+        // items too far apart for one descriptor (not a chunk table): each item's first lane hashes
+        // it alone -- correct for any layout, slow; K1 (one wave per item) is the path for that
+        if (valid && head) {
             const U128 h = xxh3_lane_any(arena + off, len);
             out[2 * item] = h.lo;
             out[2 * item + 1] = h.hi;
         }
         return;
     }
-    uint64_t key0[4], key1[4];
+    uint64_t key0[NL], key1[NL];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        key0[j] = kSecW[4 * j + q + 2 * k];
-        key1[j] = kSecW[4 * j + q + 2 * k + 1];
+    for (int j = 0; j < NL; ++j) {
+        key0[j] = kSecW[4 * RPI * j + st0 + 2 * k];
+        key1[j] = kSecW[4 * RPI * j + st0 + 2 * k + 1];
     }
     const uint64_t sk0 = kSecW[16 + 2 * k], sk1 = kSecW[16 + 2 * k + 1];
     if (whi != 0) {
@@ -564,55 +574,68 @@ __device__ __forceinline__ void rows_item(const uint8_t* __restrict__ arena, con
         // blocks followed by a scramble (< 2^32: an item below 4 TiB) and stripes of block nb
         const uint32_t nb = act ? (uint32_t)((len - 1) >> 10) : 0;
         const uint32_t ns = act ? (uint32_t)(((len - 1) - ((uint64_t)nb << 10)) >> 6) : 0;
-        uint32_t B = 0;  // the pass's last iteration: its longest item's partial block
+        uint32_t B = 0;  // the wave's last iteration: its longest item's partial block
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)nb, 16 * r);
+        for (int r = 0; r < IPW; ++r) {
+            const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)nb, LPI * r);
             B = x > B ? x : B;
         }
         const bool shifted = act && bs != 0;
-        // pieces j < jpart of the partial block are live (stripe 4j+q < ns)
-        const uint32_t jpart = act ? (ns > (uint32_t)q ? (ns - (uint32_t)q + 3) >> 2 : 0u) : 0u;
+        // pieces j < jpart of the partial block are live (stripe 4*RPI*j + st0 < ns)
+        const uint32_t jpart = act && ns > (uint32_t)st0 ? (ns - (uint32_t)st0 + 4 * RPI - 1) / (4 * RPI) : 0u;
         uint64_t a0 = kInitW[2 * k], a1 = kInitW[2 * k + 1];
-        // pieces j < live_n(b) of iteration b are live: 4 in a full block, jpart in the partial one
-        auto live_n = [&](uint32_t b) -> uint32_t { return (act & (b < nb)) ? 4u : (b == nb) ? jpart : 0u; };
+        // pieces j < live_n(b) of iteration b are live: NL in a full block, jpart in the partial one
+        auto live_n = [&](uint32_t b) -> uint32_t { return (act & (b < nb)) ? (uint32_t)NL : (b == nb) ? jpart : 0u; };
         const __amdgpu_buffer_rsrc_t rsrc =
             __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), (short)0, (int)(uint32_t)span, kRsrcFlags);
-        // Byte-shifted rows load every piece 4 bytes late: the lane then holds dwords w1..w4 of the
+        // Byte-shifted items load every piece 4 bytes late: the lane then holds dwords w1..w4 of the
         // five its piece spans (w0 = the dword holding the piece's first byte) and takes w0 from the
-        // previous lane's w4 (DPP row_ror:1); the row's first lane takes it from the last lane of the
-        // previous load, and for load 0 from the previous iteration (`carry`; before the first, one
-        // dword load). No load ever reads past a live piece, and no extra loads are needed per
-        // iteration. v_perm_b32 then picks bytes bs..bs+3 of each dword pair; an aligned row loads on
-        // time and picks bytes 4..7 (the loaded dword itself).
+        // previous lane's w4 (DPP row_ror:1; a row's first lane from the previous row of the item
+        // through a permlane16 swap (RPI 2), or from the previous load, for load 0 from the previous
+        // iteration (`carry`; before the first, one dword load). No load reads past a live piece, and
+        // no extra loads are needed per iteration. v_perm_b32 then picks bytes bs..bs+3 of each dword
+        // pair; an aligned item loads on time and picks bytes 4..7 (the loaded dword itself).
         const uint32_t late = shifted ? 4u : 0u;
         const uint32_t psel = 0x03020100u + 0x01010101u * (shifted ? bs : 4u);
-        auto load_iter = [&](uint32_t b, uint4 (&dst)[4]) {
-            const uint32_t vo = vb + (b << 10) + (uint32_t)(q * 64 + k * 16) + late;
+        auto load_iter = [&](uint32_t b, uint4 (&dst)[NL]) {
+            const uint32_t vo = vb + (b << 10) + 16u * (uint32_t)t + late;
             const uint32_t jn = live_n(b);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) dst[j] = bload16<NT>(rsrc, (uint32_t)j < jn ? vo + (uint32_t)j * 256u : kOOB);
+            for (int j = 0; j < NL; ++j) dst[j] = bload16<NT>(rsrc, (uint32_t)j < jn ? vo + (uint32_t)(256 * RPI * j) : kOOB);
         };
-        uint32_t carry = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (shifted & row_head) ? vb : kOOB, 0, 0);
-        auto fold = [&](uint4 (&src)[4], uint32_t b) {
-            uint32_t pw[4];
+        uint32_t carry = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (shifted & head) ? vb : kOOB, 0, 0);
+        auto fold = [&](uint4 (&src)[NL], uint32_t b) {
+            uint32_t w0s[NL];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) pw[j] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)src[j].w, 0x121, 0xf, 0xf, false);
+            for (int j = 0; j < NL; ++j) {
+                const uint32_t pw = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)src[j].w, 0x121, 0xf, 0xf, false);
+                if constexpr (RPI == 1) {
+                    w0s[j] = head ? carry : pw;
+                    carry = pw;  // lane 0 of the row now holds the row's last w4
+                } else {
+                    // rows (0, 1) of the item: swap[0] gives row 1 row 0's values, swap[1] row 0 row 1's
+                    const auto sw = __builtin_amdgcn_permlane16_swap(pw, pw, false, false);
+                    w0s[j] = head ? carry : (t == 16 ? sw[0] : pw);
+                    carry = sw[1];  // lane 0 of the item now holds the item's last w4 of this load
+                }
+            }
             const uint32_t jn = live_n(b);
             uint64_t s0 = 0, s1 = 0;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t w0 = row_head ? (j == 0 ? carry : pw[j - 1]) : pw[j];
+            for (int j = 0; j < NL; ++j) {
                 const uint4 a = src[j];
-                const uint4 d = make_uint4(__builtin_amdgcn_perm(a.x, w0, psel), __builtin_amdgcn_perm(a.y, a.x, psel),
+                const uint4 d = make_uint4(__builtin_amdgcn_perm(a.x, w0s[j], psel), __builtin_amdgcn_perm(a.y, a.x, psel),
                                            __builtin_amdgcn_perm(a.z, a.y, psel), __builtin_amdgcn_perm(a.w, a.z, psel));
                 if ((uint32_t)j < jn) accum16(d, key0[j], key1[j], s0, s1);
             }
-            carry = pw[3];
             s0 += dpp64<DPP_ROW_ROR4>(s0);
             s1 += dpp64<DPP_ROW_ROR4>(s1);
             s0 += dpp64<DPP_ROW_ROR8>(s0);
             s1 += dpp64<DPP_ROW_ROR8>(s1);
+            if constexpr (RPI == 2) {
+                s0 = swap16_add(s0, s0);  // the item's two rows
+                s1 = swap16_add(s1, s1);
+            }
             const bool full = act & (b < nb), part = act & (b == nb);
             const uint64_t t0 = a0 + s0, t1 = a1 + s1;
             const uint64_t c0 = scramble1(t0, sk0), c1 = scramble1(t1, sk1);
@@ -622,7 +645,7 @@ __device__ __forceinline__ void rows_item(const uint8_t* __restrict__ arena, con
         // the last stripe (at len - 64, secret offset 121), fetched with the first iterations
         const uint4 last = bload16<false>(rsrc, act ? vb + bs + (uint32_t)len - 64 + 16 * (uint32_t)k : kOOB);
         {
-            uint4 ring[D][4];
+            uint4 ring[D][NL];
 #pragma unroll
             for (int d = 0; d < D; ++d) load_iter((uint32_t)d, ring[d]);
             // one loop to the end, the last group's folds guarded: with a separate tail after the loop
@@ -648,12 +671,12 @@ __device__ __forceinline__ void rows_item(const uint8_t* __restrict__ arena, con
         mhi += dpp64<DPP_QUAD_XOR1>(mhi);
         mlo += dpp64<DPP_QUAD_XOR2>(mlo);
         mhi += dpp64<DPP_QUAD_XOR2>(mhi);
-        if (act && row_head) {
+        if (act && head) {
             out[2 * item] = avalanche_xxh3(len * P64_1 + mlo);
             out[2 * item + 1] = avalanche_xxh3(~(len * P64_2) + mhi);
         }
     }
-    if (valid && !lng && row_head) {
+    if (valid && !lng && head) {
         const U128 h = xxh3_lane_short(arena + off, len);
         out[2 * item] = h.lo;
         out[2 * item + 1] = h.hi;
@@ -1021,6 +1044,12 @@ template __global__ void xxh3_wave_kernel<true, 260>(const uint8_t*, const uint6
 template __global__ void xxh3_wave_kernel<false, 260>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 template __global__ void xxh3_wave_kernel<true, 264>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 template __global__ void xxh3_wave_kernel<false, 264>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<true, 768>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<false, 768>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<true, 772>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<false, 772>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<true, 776>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<false, 776>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 template __global__ void xxh3_text_wave_kernel<0>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t*, uint64_t*);
 template __global__ void xxh3_text_wave_kernel<72>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t*, uint64_t*);
 template __global__ void xxh3_text_wave_kernel<8>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t*, uint64_t*);
