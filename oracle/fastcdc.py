@@ -11,8 +11,11 @@ named by its DECIMAL u128 string). The algorithm is in the un-vendored crate `fa
   byte of the normalised ranges), written differently from the C oracle's two-bytes-per-step loop,
   so the two cross-check each other on small inputs.
 * `chunks()` drives the C oracle (oracle/fastcdc_oracle.c) for larger inputs.
-Parity against a reference run is UNPINNED (no FastCDC fixtures exist in the reference; the crate
-cannot be built here). Only tests/ may import this module.
+Parity against a reference run is PARTLY PINNED: no FastCDC fixtures exist in the reference and the
+crate (fastcdc 3.2.1) is neither vendored nor buildable here, but two of the crate's own published
+tests are restated in tests/test_fastcdc.py -- `test_all_zeros` (10 chunks of 1 024 B, each cut with
+hash 14169102344523991076 = -GEAR[0] mod 2^64: pins GEAR[0], hence the MD5 rule, and the min/max
+walk) and `test_masks` (the MASKS entries level 1 picks). Only tests/ may import this module.
 """
 from __future__ import annotations
 

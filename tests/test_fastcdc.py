@@ -2,9 +2,11 @@
 
 Oracle: oracle/fastcdc_oracle.c (two-bytes-per-step loop, as the crate writes it) cross-checked
 against oracle/fastcdc.py's per-byte restatement; GEAR derived from the crate's documented MD5 rule.
-Parity against a reference run is unpinned (no fixtures exist; the crate is not vendored), so the
-bar is: GPU chunk table and digests bit-identical to the oracle on the same bytes, for every
-parameter class and the edge cases (empty, < min, odd tails, dense/pathological candidates).
+The crate is not vendored and no reference fixture exists; two of the crate's own published tests
+(fastcdc 3.2.1 `test_all_zeros`, `test_masks`) are restated below and pin GEAR[0] (hence the MD5
+rule), the mask selection and the min/max walk. Beyond them the bar is: GPU chunk table and digests
+bit-identical to the oracle on the same bytes, for every parameter class and the edge cases (empty,
+< min, odd tails, dense/pathological candidates).
 """
 import os
 
@@ -28,6 +30,30 @@ def test_gear_rule_matches_compiled_table(built_lib):
     from oxen_amd import dedup
 
     assert dedup.fastcdc_gear() == F.gear_table()
+
+
+def test_crate_all_zeros_known_answer():
+    """The crate's own known answer (fastcdc 3.2.1, src/v2020/mod.rs `test_all_zeros`, a published test
+    of the dependency that is not vendored here): 10 240 zero bytes at (64, 256, 1024) give 10 chunks of
+    1 024 B at multiples of 1 024, each returned with hash 14169102344523991076. For zeros the rolled
+    hash after 64+ steps is -GEAR[0] mod 2^64, so this pins GEAR[0] -- and with it the MD5 rule the
+    whole table is derived by -- and the min/max walk."""
+    chunks = F.chunks(np.zeros(10240, dtype=np.uint8), 64, 256, 1024)
+    assert chunks.tolist() == [[1024 * i, 1024] for i in range(10)]
+    gear = F.gear_table()
+    h = 0
+    for _ in range(1024 - 64):  # cut_gear rolls positions [min, max) of each chunk from hash 0
+        h = ((h << 1) + gear[0]) & F.M64
+    assert h == 14169102344523991076
+    assert F.chunks_py(bytes(10240), 64, 256, 1024) == [(1024 * i, 1024) for i in range(10)]
+
+
+def test_crate_mask_selection():
+    """fastcdc 3.2.1 `test_masks` (src/v2020/mod.rs): which MASKS entries level 1 picks for three
+    average sizes (mask_s = MASKS[bits + 1], mask_l = MASKS[bits - 1], bits = log2(avg) rounded)."""
+    assert F.masks(256, 1) == (F.MASKS[9], F.MASKS[7])
+    assert F.masks(16384, 1) == (F.MASKS[15], F.MASKS[13])
+    assert F.masks(4194304, 1) == (F.MASKS[23], F.MASKS[21])
 
 
 @pytest.mark.parametrize("level", [0, 1, 2, 3])
@@ -168,6 +194,20 @@ def test_fastcdc_constant_data(cuda, oracle_lib, byte, cdc_path):
     files = [np.full(s, byte, dtype=np.uint8) for s in (100, 5000, 1_500_001)]
     _check(cuda, oracle_lib, files, 64, 256, 1024)
     _check(cuda, oracle_lib, files, 4096, 8192, 16384)
+
+
+@pytest.mark.gpu
+def test_fastcdc_crate_all_zeros_on_device(cuda, cdc_path):
+    """The crate's `test_all_zeros` case through the device path: 10 chunks of 1 024 B."""
+    import torch
+
+    from oxen_amd.device import fastcdc_device, to_numpy_u64
+
+    arena = torch.zeros(10240, dtype=torch.uint8, device=cuda)
+    c_off, c_len, _, first = fastcdc_device(arena, [0], [10240], 64, 256, 1024, digests=False)
+    assert int(first[1]) == 10
+    assert to_numpy_u64(c_off).tolist() == [1024 * i for i in range(10)]
+    assert to_numpy_u64(c_len).tolist() == [1024] * 10
 
 
 @pytest.mark.gpu
