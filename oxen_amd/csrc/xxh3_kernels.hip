@@ -497,7 +497,7 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
 // items issues ~290 VALU instructions per 4 KiB round -- the reduce-scatter and broadcast across rows
 // and 4 chain steps per round on every lane -- and is VALU-issue bound there (SQ_ACTIVE_INST_VALU at
 // the SIMDs' issue capacity, profiles/r04e_cdc_pmc.txt); here a 4 KiB iteration (one block of each
-// of 4 items) costs about a third of that.
+// of 4 items) takes ~138 (the loop's .s), and packed items become bound by their access pattern.
 // RPI = 2 (Cfg bit 9, "K1H"): two rows (32 lanes) per item, two items per wave. Load j (0..1) reads
 // 512 contiguous bytes of the item (5 lines when unaligned, against 2 x 3 for two row loads); the lane
 // sums stripes {t/4, 8 + t/4} (t = lane % 32); the block sum takes one permlane16 swap more, and each
