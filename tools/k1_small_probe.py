@@ -11,7 +11,7 @@ Cases (~6.4 GB device-resident each, K1 = oxh_xxh3_128_batch_device, HIP events,
   cdc_256         the same lengths at 256-B alignment
   cdc_packed_w64sort  cdc_packed, listed in length order within windows of 64 items (K1R lockstep)
   cdc64_packed / cdc64_256   lengths uniform in [4 KiB, 128 KiB) (FastCDC at 64 KiB), likewise
-PROBE_CASES=a,b limits the run to those cases. PROBE_WG=1,4 repeats every case with that many waves per
+PROBE_BYTES sets the arena size (default 6.4 GB). PROBE_CASES=a,b limits the run to those cases. PROBE_WG=1,4 repeats every case with that many waves per
 K1 workgroup (OXH_K1_WG_WAVES), alternating.
 for each K1 variant given (default: 72 8).
 """
@@ -35,7 +35,7 @@ def main():
 
     variants = [int(v) for v in sys.argv[1:]] or [72, 8]
     dev = torch.device("cuda:0")
-    total = 6_400_000_000
+    total = int(os.environ.get("PROBE_BYTES", 6_400_000_000))
     arena = torch.empty(total + (1 << 20), dtype=torch.uint8, device=dev)
     fill_splitmix(arena, 5)
     rng = np.random.default_rng(0)
