@@ -20,5 +20,5 @@ fi
 wait $DEV
 D=$?
 echo "device_soak rc=$D engine_soak(1 MiB) rc=$E1 engine_soak(1 GiB) rc=$E2"
-tail -2 gpurun_out/${T}_device_soak.json gpurun_out/${T}_engine_soak_regrow_1mib.json gpurun_out/${T}_engine_soak_regrow_1gib.json
+for f in gpurun_out/${T}_device_soak.json gpurun_out/${T}_engine_soak_regrow_1mib.json gpurun_out/${T}_engine_soak_regrow_1gib.json; do tail -n 2 "$f"; done
 [ $D -eq 0 ] && [ $E1 -eq 0 ] && [ $E2 -eq 0 ]
