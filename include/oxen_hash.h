@@ -185,9 +185,11 @@ int oxh_clean_corrupted_versions(oxh_ctx* ctx, const char* versions_root, int dr
  * balanced by bytes when meta_sizes is given. Paths and outputs cross the process boundary through
  * one shared-memory region; calls on one pool serialise. Helpers exit on oxh_pool_destroy, or when
  * the creating process exits (whichever thread created the pool: a helper watches its socket and its
- * parent process, not the creating thread). A helper that dies, or that has not answered a call
- * within OXH_WAIT_LIMIT_S seconds (default 60), makes the call, and every later call, fail with
- * OXH_ERR_HIP. Creation fails with the first helper's error (e.g. OXH_ERR_NODEVICE without a GPU).
+ * parent process, not the creating thread). A helper that dies makes the call, and every later call,
+ * fail with OXH_ERR_HIP. A helper that is alive but has not answered within OXH_WAIT_LIMIT_S seconds
+ * (default 60) is only reported on stderr (the call keeps waiting: a large batch may take that long);
+ * OXH_POOL_CALL_LIMIT_S > 0 is the opt-in deadline after which the call, and every later call, fail
+ * with OXH_ERR_HIP (default 0 = no deadline). Creation fails with the first helper's error (e.g. OXH_ERR_NODEVICE without a GPU).
  * Replaces the reference's fan-out of 64-file batches over num_cpus*2 tasks of one process
  * (core/v_latest/add.rs:422-425) with a fan-out over processes and devices. */
 typedef struct oxh_pool oxh_pool;

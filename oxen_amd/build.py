@@ -83,17 +83,39 @@ def build_host(force: bool = False, verbose: bool = False) -> str:
     return HOST_LIB
 
 
+def compile_lib(out: str, defines: tuple[str, ...] = (), verbose: bool = False) -> str:
+    """hipcc every source to its own object in parallel (one hipcc per source), then link `out`."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    objdir = os.path.join(HERE, "build", os.path.basename(out).replace(".so", ""))
+    os.makedirs(objdir, exist_ok=True)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall"] + [f"-D{d}" for d in defines]
+
+    def one(src: str) -> str:
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        cmd = [hipcc()] + flags + ["-c", "-o", obj, src]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        return obj
+
+    jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", "0") or 0) or (os.cpu_count() or 4)))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(one, SOURCES))
+    tmp = out + ".tmp"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-Wl,--no-undefined", "-o", tmp] + objs
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, out)
+    return out
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         build_host(verbose=verbose)
         return LIB
-    tmp = LIB + ".tmp"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall", "-Wl,--no-undefined",
-           "-o", tmp] + SOURCES
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
+    compile_lib(LIB, verbose=verbose)
     build_host(force=True, verbose=verbose)
     return LIB
 

@@ -66,6 +66,7 @@ static constexpr uint64_t kCdcMasks[26] = {
 
 constexpr uint32_t kSecDefault = 512 * 1024;  // minimum section bytes (F1 wave / F2 lane unit)
 constexpr int kHashSpan = 47;          // positions after a chunk's start index with a truncated window
+constexpr uint64_t kXStaticLds = 256 * 8;  // the X kernels' static LDS (their gear table), beside the dynamic lists
 constexpr int kEntryShift = 47;        // candidate entry: group index (17 bits: units up to 2 MiB) << 47 | hash
 constexpr uint64_t kEntryHash = (1ull << kEntryShift) - 1;
 
@@ -1451,11 +1452,6 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     // (sec / 64 bytes), at most one per group; a denser unit keeps a truncated list and the walk
     // scans its bytes (C5 at 8 KiB: 2 expected per 8 KiB unit, 24 stored: P(overflow) ~ 1e-16).
     const double dens = std::min(1.0, 16.0 * std::ldexp(1.0, -__builtin_popcountll(prm.mask_s & prm.mask_l))) / 16.0;
-    prm.sec = oxh::kSecDefault;
-    if (const char* e = getenv("OXH_CDC_SECTION_BYTES")) {  // tests: many small sections per file
-        const uint64_t v = strtoull(e, nullptr, 10);
-        if (v >= 1024 && v % 1024 == 0 && v <= (1u << 30)) prm.sec = v;
-    }
     // sections of at least `max` bytes: a chunk never spans a whole section (F3's invariant)
     // Speculative walks meet the true walk after ~1.5 chunks (median) and within 6 chunks in 99 % of
     // random starts (measured with the oracle). Warm-up: 6 max-sized chunks, at least 128 KiB (r02
@@ -1473,48 +1469,65 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     }
     // The walk path (W + X, DESIGN §4 "F1 -> W"): chosen where it rolls fewer bytes than F1 -- small
     // chunks, where the skipped `min` bytes are a large share (61 % rolled at 8 KiB, 94 % at 64 KiB) --
-    // and where its layout rules hold: masks at bit 16 or above, a 128-B aligned arena, and every
-    // wave's 64 sections inside one 4 GiB window (checked below). OXH_CDC_WALK=0 / 1 forces it off / on.
+    // and where its layout rules hold: masks at bit 16 or above, a 128-B aligned arena, every wave's 64
+    // sections inside one 4 GiB window, and X's per-section lists within a workgroup's LDS (checked
+    // below; where one does not hold the call takes the scan). OXH_CDC_WALK=0 / 1 forces it off / on.
     const char* walk_env = getenv("OXH_CDC_WALK");
+    const bool walk_forced = walk_env && atoi(walk_env) != 0;
     bool walk = (((prm.mask_s | prm.mask_l) & 0xFFFFull) == 0) && (((uintptr_t)d_arena & 127) == 0) &&
-                (walk_env ? atoi(walk_env) != 0 : (avg_size <= 16384));
-    prm.warmup = std::max<uint64_t>(6 * (uint64_t)max_size, 128 * 1024);
-    if (walk) {
-        // one lane per section, one generation of 12-wave workgroups on every CU: sections as large
-        // as that allows (fewer sections = less warm-up and stitching), whole 8 KiB, at least 4 max
-        int dev = 0, cus = 256;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-        const uint64_t lanes = (uint64_t)cus * oxh::kScanWaves * 64;
-        const uint64_t want = (total_bytes + lanes - 1) / std::max<uint64_t>(lanes, 1);
-        if (!getenv("OXH_CDC_SECTION_BYTES")) prm.sec = std::max<uint64_t>({want, 4 * max_rounded, 64 * 1024});
-        // warm-up: a relaxed walk started anywhere lands on the true one within 14 / 37 / 67 KB in 50 /
-        // 90 / 99 % of starts at 8 KiB chunks (C restatement, 1 GiB); X re-walks the sections whose
-        // warm-up was too short, so it is kept short: two max-sized chunks
-        prm.warmup = 2 * (uint64_t)max_size;
-    }
-    if (prm.sec < max_rounded) prm.sec = max_rounded;
-    if (!walk && !getenv("OXH_CDC_SECTION_BYTES") && prm.sec < 8 * max_rounded) prm.sec = 8 * max_rounded;
-    prm.sec = (prm.sec + 8191) / 8192 * 8192;  // 64 F1 units of whole 128-byte rounds
-    // a candidate entry holds the group index in 17 bits: units of at most 2 MiB (sections of 128 MiB,
-    // 8 chunks of the crate's largest max); the test-only section override is clamped to that
-    prm.sec = std::min<uint64_t>(prm.sec, 128ull << 20);
-    if (prm.sec < max_rounded) return cdc_fail(OXH_ERR_INVALID, "section override below max_size");
-    prm.unit = prm.sec / 64;
-    if (const char* e = getenv("OXH_CDC_WARMUP_BYTES")) prm.warmup = strtoull(e, nullptr, 10);  // tests
-    prm.cap = (uint32_t)std::min<double>(prm.unit / 16, 8.0 * dens * prm.unit + 8);
-    if (const char* e = getenv("OXH_CDC_UNIT_CAP")) prm.cap = std::max(1, atoi(e));  // tests: force overflow
-    prm.speccap = (uint32_t)(prm.sec / min_size + 2 + (max_size + min_size - 1) / min_size);
-
+                (walk_env ? walk_forced : (avg_size <= 16384));
+    if (walk_forced && !walk) return cdc_fail(OXH_ERR_INVALID, "OXH_CDC_WALK=1: masks below bit 16 or an unaligned arena");
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    int max_lds = 0;
+    if (hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess) max_lds = 64 * 1024;
     std::vector<uint64_t> sec_base(n + 1);
-    sec_base[0] = 0;
-    for (uint64_t i = 0; i < n; ++i) sec_base[i + 1] = sec_base[i] + (lens[i] + prm.sec - 1) / prm.sec;
-    const uint64_t n_sec = sec_base[n];
-    if (walk) {
+    uint64_t n_sec = 0;
+    for (;;) {
+        prm.sec = oxh::kSecDefault;
+        if (const char* e = getenv("OXH_CDC_SECTION_BYTES")) {  // tests: many small sections per file
+            const uint64_t v = strtoull(e, nullptr, 10);
+            if (v >= 1024 && v % 1024 == 0 && v <= (1u << 30)) prm.sec = v;
+        }
+        prm.warmup = std::max<uint64_t>(6 * (uint64_t)max_size, 128 * 1024);
+        if (walk) {
+            // one lane per section, one generation of 12-wave workgroups on every CU: sections as large
+            // as that allows (fewer sections = less warm-up and stitching), whole 8 KiB, at least 4 max
+            int cus = 256;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+            const uint64_t lanes = (uint64_t)cus * oxh::kScanWaves * 64;
+            const uint64_t want = (total_bytes + lanes - 1) / std::max<uint64_t>(lanes, 1);
+            if (!getenv("OXH_CDC_SECTION_BYTES")) prm.sec = std::max<uint64_t>({want, 4 * max_rounded, 64 * 1024});
+            // warm-up: a relaxed walk started anywhere lands on the true one within 14 / 37 / 67 KB in 50 /
+            // 90 / 99 % of starts at 8 KiB chunks (C restatement, 1 GiB); X re-walks the sections whose
+            // warm-up was too short, so it is kept short: two max-sized chunks
+            prm.warmup = 2 * (uint64_t)max_size;
+        }
+        if (prm.sec < max_rounded) prm.sec = max_rounded;
+        if (!walk && !getenv("OXH_CDC_SECTION_BYTES") && prm.sec < 8 * max_rounded) prm.sec = 8 * max_rounded;
+        prm.sec = (prm.sec + 8191) / 8192 * 8192;  // 64 F1 units of whole 128-byte rounds
+        // a candidate entry holds the group index in 17 bits: units of at most 2 MiB (sections of 128 MiB,
+        // 8 chunks of the crate's largest max); the test-only section override is clamped to that
+        prm.sec = std::min<uint64_t>(prm.sec, 128ull << 20);
+        if (prm.sec < max_rounded) return cdc_fail(OXH_ERR_INVALID, "section override below max_size");
+        prm.unit = prm.sec / 64;
+        if (const char* e = getenv("OXH_CDC_WARMUP_BYTES")) prm.warmup = strtoull(e, nullptr, 10);  // tests
+        prm.cap = (uint32_t)std::min<double>(prm.unit / 16, 8.0 * dens * prm.unit + 8);
+        if (const char* e = getenv("OXH_CDC_UNIT_CAP")) prm.cap = std::max(1, atoi(e));  // tests: force overflow
+        prm.speccap = (uint32_t)(prm.sec / min_size + 2 + (max_size + min_size - 1) / min_size);
+
+        sec_base[0] = 0;
+        for (uint64_t i = 0; i < n; ++i) sec_base[i + 1] = sec_base[i] + (lens[i] + prm.sec - 1) / prm.sec;
+        n_sec = sec_base[n];
+        if (!walk) break;
+        // X keeps a section's start list and fix list in dynamic LDS beside its static gear table
+        std::string why;
+        if (2 * (uint64_t)prm.speccap * sizeof(uint32_t) + oxh::kXStaticLds > (uint64_t)max_lds)
+            why = "X's section lists do not fit the workgroup's LDS";
         // every wave's lanes must address their streams from one buffer resource: the lowest start
         // (warm-up included) to the highest byte a lane may read (its section end + two max chunks,
         // or its file end) within 4 GiB - 1 MiB
-        for (uint64_t w0s = 0, f = 0; w0s < n_sec && walk; w0s += 64) {
+        for (uint64_t w0s = 0, f = 0; w0s < n_sec && why.empty(); w0s += 64) {
             uint64_t lo = ~0ull, hi = 0;
             for (uint64_t sct = w0s; sct < std::min<uint64_t>(n_sec, w0s + 64); ++sct) {
                 while (sec_base[f + 1] <= sct) ++f;
@@ -1524,10 +1537,11 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
                 lo = std::min(lo, a);
                 hi = std::max(hi, b);
             }
-            if (hi - (lo & ~127ull) + 256 >= 0xFFFFFF00ull - (1ull << 20)) walk = false;
+            if (hi - (lo & ~127ull) + 256 >= 0xFFFFFF00ull - (1ull << 20)) why = "a wave's sections span 4 GiB";
         }
-        if (walk_env && atoi(walk_env) != 0 && !walk)
-            return cdc_fail(OXH_ERR_INVALID, "OXH_CDC_WALK=1: the arena layout does not allow the walk path");
+        if (why.empty()) break;
+        if (walk_forced) return cdc_fail(OXH_ERR_INVALID, "OXH_CDC_WALK=1: " + why);
+        walk = false;  // the scan, with its own section plan
     }
 
     // OXH_TRACE=1: host-side stage times of this call on stderr

@@ -92,25 +92,30 @@ int check_device(int device) {
 // ---------------------------------------------------------------- kernel launch helpers
 using WaveKernel = void (*)(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 
+// The shipped library instantiates the shapes the dispatch below picks (8, 72, 104, 264) and the
+// 4-round ring (0) as the fallback for any other forced variant. The experiments that lost their A/Bs
+//  are compiled only into the probe build (tools/build_probe_lib.sh, -DOXH_PROBE_VARIANTS).
 template <bool DESC>
 WaveKernel wave_kernel_for(int variant) {
     switch (variant) {
+        case 8: return oxh::xxh3_wave_kernel<DESC, 8>;
+        case 72: return oxh::xxh3_wave_kernel<DESC, 72>;
+        case 104: return oxh::xxh3_wave_kernel<DESC, 104>;
+        case 264: return oxh::xxh3_wave_kernel<DESC, 264>;
+#ifdef OXH_PROBE_VARIANTS
         case 1: return oxh::xxh3_wave_kernel<DESC, 1>;
         case 2: return oxh::xxh3_wave_kernel<DESC, 2>;
         case 4: return oxh::xxh3_wave_kernel<DESC, 4>;
-        case 8: return oxh::xxh3_wave_kernel<DESC, 8>;
         case 12: return oxh::xxh3_wave_kernel<DESC, 12>;
         case 64: return oxh::xxh3_wave_kernel<DESC, 64>;
-        case 72: return oxh::xxh3_wave_kernel<DESC, 72>;
         case 74: return oxh::xxh3_wave_kernel<DESC, 74>;
         case 40: return oxh::xxh3_wave_kernel<DESC, 40>;
-        case 104: return oxh::xxh3_wave_kernel<DESC, 104>;
         case 256: return oxh::xxh3_wave_kernel<DESC, 256>;
         case 260: return oxh::xxh3_wave_kernel<DESC, 260>;
-        case 264: return oxh::xxh3_wave_kernel<DESC, 264>;
         case 768: return oxh::xxh3_wave_kernel<DESC, 768>;
         case 772: return oxh::xxh3_wave_kernel<DESC, 772>;
         case 776: return oxh::xxh3_wave_kernel<DESC, 776>;
+#endif
         default: return oxh::xxh3_wave_kernel<DESC, 0>;
     }
 }
@@ -149,8 +154,11 @@ uint64_t items_per_wave(int variant) { return (variant & 256) ? ((variant & 512)
 // matches the kernel that runs
 int known_variant(int v) {
     switch (v) {
-        case 1: case 2: case 4: case 8: case 12: case 40: case 64: case 72: case 74: case 104:
-        case 256: case 260: case 264: case 768: case 772: case 776: return v;
+        case 8: case 72: case 104: case 264: return v;
+#ifdef OXH_PROBE_VARIANTS
+        case 1: case 2: case 4: case 12: case 40: case 64: case 74:
+        case 256: case 260: case 768: case 772: case 776: return v;
+#endif
         default: return 0;
     }
 }
@@ -180,19 +188,10 @@ int launch_text(const uint8_t* arena, const uint64_t* offs, const uint64_t* lens
     const uint64_t blocks = (n + 3) / 4;
     // K1T keeps the 2-round ring with the keys in LDS at every item size: the counting needs the
     // registers (tools/k1t_probe.py: 6.41 TB/s on C2 and 5.55 on ragged items, against 5.42 / 4.40
-    // with variant 8 and 4.32 / 2.56 with the 4-round ring)
+    // with variant 8 and 4.32 / 2.56 with the 4-round ring); only that shape ships
     (void)short_items;
-    const int forced = g_variant.load();
-    const int v = forced ? forced : kVariantShort;
-    if (v == kVariantShort)
-        hipLaunchKernelGGL(oxh::xxh3_text_wave_kernel<kVariantShort>, dim3((unsigned)blocks), dim3(256), 0, st, arena, offs, lens,
-                           n, out, counts);
-    else if (v == kVariantLong)
-        hipLaunchKernelGGL(oxh::xxh3_text_wave_kernel<kVariantLong>, dim3((unsigned)blocks), dim3(256), 0, st, arena, offs, lens,
-                           n, out, counts);
-    else
-        hipLaunchKernelGGL(oxh::xxh3_text_wave_kernel<0>, dim3((unsigned)blocks), dim3(256), 0, st, arena, offs, lens, n, out,
-                           counts);
+    hipLaunchKernelGGL(oxh::xxh3_text_wave_kernel<kVariantShort>, dim3((unsigned)blocks), dim3(256), 0, st, arena, offs, lens,
+                       n, out, counts);
     HIP_TRY(hipGetLastError());
     return OXH_OK;
 }
@@ -2033,7 +2032,7 @@ int refresh_file(FileStream& fs, FileRequest* r, uint64_t i) {
         const int rc = oversize_item(c, tmp.data(), L, r->out + 2 * i, r->counts ? r->counts + 2 * i : nullptr,
                                      r->utf8 ? &u8 : nullptr);
         if (rc == OXH_ERR_NOMEM) {
-            item_failed(r, i, OXH_ERR_NOMEM, ENOMEM);  // this file's failure, not the run's
+            item_failed(r, i, OXH_ERR_NOMEM, 0);  // this file's failure, not the run's; os_error 0 (no open / read failed), as large_items reports it
         } else if (rc) {
             return rc;
         } else {

@@ -175,19 +175,54 @@ _IO_ERROR_KINDS = {
 }
 
 
+# Other_Grapheme_Extend code points outside categories Mn / Me (DerivedCoreProperties: Grapheme_Extend =
+# Mn + Me + Other_Grapheme_Extend); the Cf ones among them are escaped as non-printable anyway
+_OTHER_GRAPHEME_EXTEND = frozenset([0x09BE, 0x09D7, 0x0B3E, 0x0B57, 0x0BBE, 0x0BD7, 0x0CC2, 0x0CD5, 0x0CD6, 0x0D3E,
+                                    0x0D57, 0x0DCF, 0x0DDF, 0x1B35, 0x200C, 0x302E, 0x302F, 0xFF9E, 0xFF9F, 0x1133E,
+                                    0x11357, 0x114B0, 0x114BD, 0x115AF, 0x11930, 0x1D165, 0x1D16E, 0x1D16F, 0x1D170,
+                                    0x1D171, 0x1D172])
+
+
+def _rust_escape_char(ch: str, escape_single_quote: bool) -> str:
+    """char::escape_debug_ext (Rust core): the named escapes, then \\u{..} for grapheme-extended and
+    non-printable chars. core::unicode::printable marks as non-printable every code point of general
+    category Cc, Cf, Cs, Co, Cn, Zl, Zp or Zs except the space (its generator, printable.py); the
+    categories come from Python's unicodedata, whose Unicode version may trail Rust's for recently
+    assigned code points ("Error texts")."""
+    import unicodedata
+
+    esc = {"\0": "\\0", "\t": "\\t", "\r": "\\r", "\n": "\\n", "\\": "\\\\", '"': '\\"'}
+    if ch in esc:
+        return esc[ch]
+    if ch == "'" and escape_single_quote:
+        return "\\'"
+    o = ord(ch)
+    cat = unicodedata.category(ch)
+    if cat in ("Mn", "Me") or o in _OTHER_GRAPHEME_EXTEND:
+        return "\\u{%x}" % o
+    if cat in ("Cc", "Cf", "Cs", "Co", "Cn", "Zl", "Zp", "Zs") and ch != " ":
+        return "\\u{%x}" % o
+    return ch
+
+
 def rust_str_debug(text: str) -> str:
-    """`{:?}` of a Rust str / Path: double quotes; backslash, double quote, newline, carriage return,
-    tab and NUL escaped, other control characters as \\u{..}."""
-    esc = {'"': '\\"', "\\": "\\\\", "\n": "\\n", "\r": "\\r", "\t": "\\t", "\0": "\\0"}
+    """`{:?}` of a Rust str (e.g. io::Error's message): double quotes; the escapes of char::escape_debug
+    except that a single quote stays as it is."""
+    return '"' + "".join(_rust_escape_char(ch, False) for ch in text) + '"'
+
+
+def rust_path_debug(path) -> str:
+    """`{:?}` of a Rust Path on Unix (OsStr -> the byte string's Utf8Chunks Debug, core/src/str/lossy.rs):
+    the valid UTF-8 runs escaped by char::escape_debug (a single quote too), every byte of an invalid
+    sequence as \\xNN (upper-case hex)."""
+    raw = os.fsencode(path)
     out = ['"']
-    for ch in text:
+    for ch in raw.decode("utf-8", errors="surrogateescape"):
         o = ord(ch)
-        if ch in esc:
-            out.append(esc[ch])
-        elif o < 0x20 or o == 0x7F or 0xD800 <= o <= 0xDFFF:
-            out.append("\\u{%x}" % o)
+        if 0xDC80 <= o <= 0xDCFF:  # a byte that is not part of valid UTF-8
+            out.append("\\x%02X" % (o - 0xDC00))
         else:
-            out.append(ch)
+            out.append(_rust_escape_char(ch, True))
     out.append('"')
     return "".join(out)
 
@@ -209,7 +244,7 @@ def file_error(path, status: int, os_error: int, size_hint: Optional[int] = None
     (status OXH_ERR_OPEN; hasher.rs:141-145, or :151-154 for the streamed branch a size >= 1e9 picks),
     or the read did (OXH_ERR_IO; :135-139 / :161-165)."""
     if status == _capi.OXH_ERR_OPEN:
-        p = rust_str_debug(os.fsdecode(path) if isinstance(path, (bytes, os.PathLike)) else str(path))
+        p = rust_path_debug(path)
         err = rust_io_error_debug(os_error)
         if size_hint is not None and size_hint >= LARGE_FILE_BYTES:
             return OxenError(f"Could not open file {p} due to {err}", _capi.OXH_ERR_OPEN)
@@ -488,8 +523,9 @@ def u128_hash_file_contents(path) -> int:
     """hasher.rs:102-112 (stats the file itself; a missing file is an error)."""
     try:
         size = os.stat(path).st_size
-    except OSError:
-        raise OxenError(f"Could not get metadata for {str(path)!r}", _capi.OXH_ERR_IO) from None
+    except OSError as e:  # util::fs::metadata -> OxenError::file_metadata_error (util/fs.rs:593-601, error.rs:1176-1182)
+        raise OxenError(f"Could not get file metadata: {rust_path_debug(path)} error {rust_io_error_debug(e.errno or 0)}",
+                        _capi.OXH_ERR_IO) from None
     return _hash_one_file(path, size)
 
 

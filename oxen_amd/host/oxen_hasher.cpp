@@ -116,29 +116,103 @@ std::string hash_buffer(const void* data, size_t len) { return format_hex(hash_b
 
 std::string hash_str(std::string_view s) { return hash_buffer(s.data(), s.size()); }
 
-// `{:?}` of a Rust str / Path: double quotes, \\ \" \n \r \t \0 escaped, other control characters as \u{..}
-std::string rust_str_debug(const std::string& s) {
+namespace {
+// core::unicode::printable marks as non-printable every code point of general category Cc, Cf, Cs, Co,
+// Cn, Zl, Zp or Zs except the space; Grapheme_Extend chars are escaped too. This table holds the
+// controls, format chars, separators, surrogates, private use and noncharacters, and the combining
+// blocks most file names meet; marks of other scripts and unassigned code points are not in it
+// ("Error texts").
+bool needs_unicode_escape(uint32_t c) {
+    static const uint32_t ranges[][2] = {
+        {0x0000, 0x001F}, {0x007F, 0x00A0}, {0x00AD, 0x00AD}, {0x0300, 0x036F}, {0x0483, 0x0489}, {0x0591, 0x05BD},
+        {0x0600, 0x0605}, {0x0610, 0x061A}, {0x061C, 0x061C}, {0x064B, 0x065F}, {0x06DD, 0x06DD}, {0x070F, 0x070F},
+        {0x1680, 0x1680}, {0x180E, 0x180E}, {0x1AB0, 0x1AFF}, {0x1DC0, 0x1DFF}, {0x2000, 0x200F}, {0x2028, 0x202F},
+        {0x205F, 0x2064}, {0x2066, 0x206F}, {0x20D0, 0x20F0}, {0x3000, 0x3000}, {0x302E, 0x302F}, {0x3099, 0x309A},
+        {0xD800, 0xF8FF}, {0xFE00, 0xFE0F}, {0xFE20, 0xFE2F}, {0xFEFF, 0xFEFF}, {0xFF9E, 0xFF9F}, {0xFFF0, 0xFFFB},
+        {0xFFFE, 0xFFFF}, {0x1D165, 0x1D169}, {0x1D16D, 0x1D182}, {0xE0000, 0xE0FFF}, {0xF0000, 0x10FFFF},
+    };
+    for (const auto& r : ranges)
+        if (c >= r[0] && c <= r[1]) return true;
+    return false;
+}
+
+// char::escape_debug_ext of one code point, appended to o
+void escape_char(std::string& o, uint32_t c, const char* utf8, size_t n, bool escape_single_quote) {
+    switch (c) {
+        case '"': o += "\\\""; return;
+        case '\\': o += "\\\\"; return;
+        case '\n': o += "\\n"; return;
+        case '\r': o += "\\r"; return;
+        case '\t': o += "\\t"; return;
+        case '\0': o += "\\0"; return;
+        case '\'':
+            o += escape_single_quote ? "\\'" : "'";
+            return;
+        default:
+            break;
+    }
+    if (needs_unicode_escape(c)) {
+        char b[16];
+        snprintf(b, sizeof b, "\\u{%x}", c);
+        o += b;
+    } else {
+        o.append(utf8, n);
+    }
+}
+
+// length of the valid UTF-8 sequence at s[i] (core::str::from_utf8's rules), 0 if it is not one
+size_t utf8_seq(const std::string& s, size_t i, uint32_t& cp) {
+    const unsigned char b0 = (unsigned char)s[i];
+    auto cont = [&](size_t k) { return i + k < s.size() && ((unsigned char)s[i + k] & 0xC0) == 0x80; };
+    if (b0 < 0x80) {
+        cp = b0;
+        return 1;
+    }
+    if (b0 >= 0xC2 && b0 <= 0xDF && cont(1)) {
+        cp = ((b0 & 0x1Fu) << 6) | ((unsigned char)s[i + 1] & 0x3Fu);
+        return 2;
+    }
+    if (b0 >= 0xE0 && b0 <= 0xEF && cont(1) && cont(2)) {
+        const unsigned char b1 = (unsigned char)s[i + 1];
+        if ((b0 == 0xE0 && b1 < 0xA0) || (b0 == 0xED && b1 > 0x9F)) return 0;  // overlong / surrogate
+        cp = ((b0 & 0x0Fu) << 12) | ((b1 & 0x3Fu) << 6) | ((unsigned char)s[i + 2] & 0x3Fu);
+        return 3;
+    }
+    if (b0 >= 0xF0 && b0 <= 0xF4 && cont(1) && cont(2) && cont(3)) {
+        const unsigned char b1 = (unsigned char)s[i + 1];
+        if ((b0 == 0xF0 && b1 < 0x90) || (b0 == 0xF4 && b1 > 0x8F)) return 0;  // overlong / above U+10FFFF
+        cp = ((b0 & 0x07u) << 18) | ((b1 & 0x3Fu) << 12) | (((unsigned char)s[i + 2] & 0x3Fu) << 6) |
+             ((unsigned char)s[i + 3] & 0x3Fu);
+        return 4;
+    }
+    return 0;
+}
+
+std::string rust_debug(const std::string& s, bool path) {
     std::string o = "\"";
-    for (unsigned char ch : s) {
-        switch (ch) {
-            case '"': o += "\\\""; break;
-            case '\\': o += "\\\\"; break;
-            case '\n': o += "\\n"; break;
-            case '\r': o += "\\r"; break;
-            case '\t': o += "\\t"; break;
-            case '\0': o += "\\0"; break;
-            default:
-                if (ch < 0x20 || ch == 0x7F) {
-                    char b[16];
-                    snprintf(b, sizeof b, "\\u{%x}", ch);
-                    o += b;
-                } else {
-                    o += (char)ch;
-                }
+    for (size_t i = 0; i < s.size();) {
+        uint32_t cp = 0;
+        const size_t n = utf8_seq(s, i, cp);
+        if (n == 0) {  // a byte outside valid UTF-8: \xNN in a Path (str values are valid UTF-8 by type)
+            char b[8];
+            snprintf(b, sizeof b, "\\x%02X", (unsigned char)s[i]);
+            o += b;
+            ++i;
+            continue;
         }
+        escape_char(o, cp, s.data() + i, n, path);
+        i += n;
     }
     return o + "\"";
 }
+}  // namespace
+
+// `{:?}` of a Rust str: double quotes, char::escape_debug's escapes except the single quote
+std::string rust_str_debug(const std::string& s) { return rust_debug(s, false); }
+
+// `{:?}` of a Rust Path on Unix (OsStr Debug -> Utf8Chunks Debug, core/src/str/lossy.rs): valid UTF-8 runs
+// escaped by char::escape_debug (the single quote too), each byte of an invalid sequence as \xNN
+std::string rust_path_debug(const std::string& path) { return rust_debug(path, true); }
 
 // `{:?}` of std::io::Error::from_raw_os_error(e): Os { code, kind, message }, the kind from Rust std's
 // decode_error_kind (sys/pal/unix)
@@ -172,7 +246,7 @@ std::string rust_io_error_debug(int e) {
 
 std::string file_error_text(const std::string& path, int status, int os_error, uint64_t size_hint) {
     if (status == OXH_ERR_OPEN) {
-        const std::string p = rust_str_debug(path), err = rust_io_error_debug(os_error);
+        const std::string p = rust_path_debug(path), err = rust_io_error_debug(os_error);
         if (size_hint >= kLargeFileBytes) return "Could not open file " + p + " due to " + err;  // hasher.rs:151-154
         return "util::hasher::hash_file_contents Could not open file " + p + " " + err;       // hasher.rs:141-145
     }
@@ -262,8 +336,12 @@ u128 get_hash_given_metadata(const std::string& path, const struct stat& metadat
 
 u128 u128_hash_file_contents(const std::string& path) {
     struct stat sb;
-    if (stat(path.c_str(), &sb) != 0)  // util::fs::metadata(path)? (hasher.rs:105)
-        throw OxenError::basic_str("Could not get metadata for \"" + path + "\"", OXH_ERR_IO);
+    // util::fs::metadata(path)? (hasher.rs:105) -> OxenError::file_metadata_error (util/fs.rs:593-601,
+    // error.rs:1176-1182)
+    if (stat(path.c_str(), &sb) != 0)
+        throw OxenError::basic_str("Could not get file metadata: " + rust_path_debug(path) + " error " +
+                                       rust_io_error_debug(errno),
+                                   OXH_ERR_IO);
     return hash_one_file(path, (uint64_t)sb.st_size);
 }
 

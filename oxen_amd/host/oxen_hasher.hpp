@@ -100,6 +100,7 @@ constexpr uint64_t kLargeFileBytes = 1000000000ull;
 std::string file_error_text(const std::string& path, int status, int os_error, uint64_t size_hint);
 // Rust `{:?}` of a str / Path, and of std::io::Error::from_raw_os_error(e)
 std::string rust_str_debug(const std::string& s);
+std::string rust_path_debug(const std::string& path);
 std::string rust_io_error_debug(int e);
 std::vector<FileHash> hash_files(const std::vector<std::string>& paths, oxh_ctx* ctx = nullptr);
 

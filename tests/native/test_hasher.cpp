@@ -179,10 +179,19 @@ static void known_answers(const std::string& golden) {
 
 static void file_errors(const std::string& golden) {
     const std::string missing = golden + "/no-such-file";
-    CHECK(throws_oxen([&] { hasher::hash_file_contents(missing); }, "Could not get metadata"));
     struct stat sb {};
     // hasher.rs:141-145: File::open's io::Error in its Debug form (the errno crosses the ABI)
     const std::string enoent = "Os { code: 2, kind: NotFound, message: \"No such file or directory\" }";
+    // hasher.rs:117 -> util::fs::metadata (fs.rs:593-601) -> OxenError::file_metadata_error (error.rs:1176-1182)
+    CHECK(throws_oxen([&] { hasher::hash_file_contents(missing); },
+                      "Could not get file metadata: \"" + missing + "\" error " + enoent));
+    const std::string notdir = golden + "/data_test/text/hello.txt/x";  // ENOTDIR: root cannot bypass it
+    CHECK(throws_oxen([&] { hasher::u128_hash_file_contents(notdir); },
+                      "Could not get file metadata: \"" + notdir +
+                          "\" error Os { code: 20, kind: NotADirectory, message: \"Not a directory\" }"));
+    CHECK(throws_oxen([&] { hasher::get_hash_given_metadata(notdir, sb); },
+                      "util::hasher::hash_file_contents Could not open file \"" + notdir +
+                          "\" Os { code: 20, kind: NotADirectory, message: \"Not a directory\" }"));
     CHECK(throws_oxen([&] { hasher::get_hash_given_metadata(missing, sb); },
                       "util::hasher::hash_file_contents Could not open file \"" + missing + "\" " + enoent));
     struct stat big {};
@@ -191,6 +200,10 @@ static void file_errors(const std::string& golden) {
                       "Could not open file \"" + missing + "\" due to " + enoent));
     CHECK(throws_oxen([&] { hasher::get_hash_given_metadata(golden, sb); }, "Could not read file for hashing"));
     CHECK(hasher::rust_str_debug("a\"b\\c\nd\x01") == "\"a\\\"b\\\\c\\nd\\u{1}\"");
+    // Path Debug: a single quote escaped, bytes outside UTF-8 as \xNN, zero-width space and combining
+    // acute as \u{..}; str Debug keeps the single quote
+    CHECK(hasher::rust_path_debug("a'b\xff\xfe\xe2\x80\x8bx\xcc\x81\xc3\xa9") == "\"a\\'b\\xFF\\xFE\\u{200b}x\\u{301}\xc3\xa9\"");
+    CHECK(hasher::rust_str_debug("it's") == "\"it's\"");
     CHECK(hasher::rust_io_error_debug(40) == "Os { code: 40, kind: FilesystemLoop, message: \"Too many levels of symbolic links\" }");
     CHECK(hasher::rust_io_error_debug(24) == "Os { code: 24, kind: Uncategorized, message: \"Too many open files\" }");
     std::vector<int> sleeps;

@@ -360,3 +360,22 @@ def test_fastcdc_walk_truncated_window_cuts(cuda, oracle_lib, monkeypatch):
     assert np.array_equal(to_numpy_u64(c_off), want[:, 0]) and np.array_equal(to_numpy_u64(c_len), want[:, 1])
     short = int(((want[:-1, 1] >= 4096) & (want[:-1, 1] < 4096 + 47)).sum())
     assert short > 50, short  # chunks cut inside the truncated window: the case X exists for
+
+
+@pytest.mark.gpu
+def test_fastcdc_walk_lists_beyond_lds_take_the_scan(cuda, oracle_lib, monkeypatch):
+    """X keeps a section's start list in dynamic LDS (2 x speccap u32). With 128 MiB sections at
+    min 4 KiB that is 256 KiB, above a workgroup's 160 KiB: the call must take the scan instead of
+    failing its X launch, and with the walk forced (OXH_CDC_WALK=1) fail with a message that says why."""
+    from oxen_amd import _capi
+    from oxen_amd.device import fastcdc_device
+
+    monkeypatch.setenv("OXH_CDC_SECTION_BYTES", str(128 << 20))
+    rng = np.random.default_rng(160)
+    files = [rng.integers(0, 256, s, dtype=np.uint8) for s in (3_000_001, 70_000, 0)]
+    assert _check(cuda, oracle_lib, files, 4096, 8192, 16384) > 0
+    monkeypatch.setenv("OXH_CDC_WALK", "1")
+    import torch
+
+    with pytest.raises(_capi.OxenError, match="OXH_CDC_WALK=1: X's section lists do not fit"):
+        fastcdc_device(torch.from_numpy(files[0]).to(cuda), [0], [len(files[0])], 4096, 8192, 16384)

@@ -18,6 +18,7 @@ pytestmark = pytest.mark.gpu
 
 ENOENT_DEBUG = 'Os { code: 2, kind: NotFound, message: "No such file or directory" }'
 ELOOP_DEBUG = 'Os { code: 40, kind: FilesystemLoop, message: "Too many levels of symbolic links" }'
+ENOTDIR_DEBUG = 'Os { code: 20, kind: NotADirectory, message: "Not a directory" }'
 
 
 @pytest.fixture
@@ -36,12 +37,14 @@ def test_status_and_errno_per_item(cuda, tree):
 
     paths = [str(tree / n) for n in ["ok.txt", "missing", "dangling", "loop_a", "adir"]]
     paths.append(str(tree / ("x" * 300)))  # a component above NAME_MAX
+    paths.append(str(tree / "ok.txt" / "x"))  # a file used as a directory
     d, sizes, st, oserr = hasher.hash_files_with_errors_128bit(paths)
-    assert st == [0, _capi.OXH_ERR_OPEN, _capi.OXH_ERR_OPEN, _capi.OXH_ERR_OPEN, _capi.OXH_ERR_IO, _capi.OXH_ERR_OPEN]
-    assert oserr == [0, errno.ENOENT, errno.ENOENT, errno.ELOOP, errno.EISDIR, errno.ENAMETOOLONG]
+    assert st == [0, _capi.OXH_ERR_OPEN, _capi.OXH_ERR_OPEN, _capi.OXH_ERR_OPEN, _capi.OXH_ERR_IO, _capi.OXH_ERR_OPEN,
+                  _capi.OXH_ERR_OPEN]
+    assert oserr == [0, errno.ENOENT, errno.ENOENT, errno.ELOOP, errno.EISDIR, errno.ENAMETOOLONG, errno.ENOTDIR]
     assert d[0] == hasher.hash_buffer_128bit(b"hello") and all(x is None for x in d[1:])
     # the same through every file entry point that reports errno
-    _, _, st2, oserr2 = hasher.hash_files_with_errors_128bit(paths, [5, 0, 0, 0, 4096, 0])
+    _, _, st2, oserr2 = hasher.hash_files_with_errors_128bit(paths, [5, 0, 0, 0, 4096, 0, 0])
     assert (st2, oserr2) == (st, oserr)
     ds, _, st3 = hasher.hash_files_128bit(paths)
     assert st3 == st and ds[0] == d[0]
@@ -71,9 +74,29 @@ def test_reference_messages(cuda, tree):
     with pytest.raises(_capi.OxenError) as e:
         hasher.hash_file_contents(str(tree / "adir"))
     assert str(e.value) == "Could not read file for hashing" and e.value.code == _capi.OXH_ERR_IO
-    # u128_hash_file_contents stats first (util::fs::metadata(path)?, hasher.rs:105)
-    with pytest.raises(_capi.OxenError, match="Could not get metadata"):
+    # u128_hash_file_contents stats first (util::fs::metadata(path)?, hasher.rs:105): util/fs.rs:593-601 ->
+    # OxenError::file_metadata_error (error.rs:1176-1182)
+    with pytest.raises(_capi.OxenError) as e:
         hasher.u128_hash_file_contents(missing)
+    assert str(e.value) == f'Could not get file metadata: "{missing}" error {ENOENT_DEBUG}'
+    with pytest.raises(_capi.OxenError) as e:
+        hasher.hash_file_contents(missing)
+    assert str(e.value) == f'Could not get file metadata: "{missing}" error {ENOENT_DEBUG}'
+    # ENOTDIR (a file used as a directory): an open failure that root cannot bypass, on the GPU box too
+    notdir = str(tree / "ok.txt" / "x")
+    with pytest.raises(_capi.OxenError) as e:
+        hasher.u128_hash_file_contents(notdir)
+    assert str(e.value) == f'Could not get file metadata: "{notdir}" error {ENOTDIR_DEBUG}'
+    with pytest.raises(_capi.OxenError) as e:
+        hasher.get_hash_given_metadata(notdir, st)
+    assert str(e.value) == f'util::hasher::hash_file_contents Could not open file "{notdir}" {ENOTDIR_DEBUG}'
+    assert e.value.code == _capi.OXH_ERR_OPEN
+    # a name with a single quote, bytes outside UTF-8 and a zero-width space: Path's Debug form
+    odd_b = os.fsencode(str(tree)) + b"/it's\xff\xfe" + "\u200b".encode()
+    with pytest.raises(_capi.OxenError) as e:
+        hasher.get_hash_given_metadata(odd_b, st)
+    assert str(e.value) == (f'util::hasher::hash_file_contents Could not open file "{tree}/it\\\'s\\xFF\\xFE\\u{{200b}}" '
+                            f"{ENOENT_DEBUG}")
     # a path with a quote and a newline: Rust's Debug escapes them
     odd = tree / 'we"ird\nname'
     with pytest.raises(_capi.OxenError) as e:

@@ -39,9 +39,10 @@ def _mismatch(got, want, lens):
     return [int(lens[i]) for i in bad[:20]]
 
 
-# K1 variants (xxh3_kernels.hip Cfg; 0 is the shipped path); 256 / 260 / 264 are K1R (a row per item),
-# 768 / 772 / 776 K1H (two rows per item)
-VARIANTS = [0, 1, 2, 4, 8, 12, 40, 64, 72, 74, 104, 256, 260, 264, 768, 772, 776]
+# The K1 variants the shipped library instantiates (xxh3_kernels.hip Cfg): the shapes the dispatch picks
+# (8 long items, 72 short, 104 block-wise packed, 264 K1R: a row per item) and the 4-round ring 0, which
+# also runs for any other forced variant. The experiments are in the probe build (tools/build_probe_lib.py).
+VARIANTS = [0, 8, 72, 104, 264]
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2, 3])
@@ -65,7 +66,7 @@ def test_every_length_unaligned(cuda, golden, mode, variant):
 
 
 @pytest.mark.parametrize("wg_waves", ["1", "2"])
-@pytest.mark.parametrize("variant", [0, 8, 72, 104, 264, 776])
+@pytest.mark.parametrize("variant", VARIANTS)
 def test_every_length_workgroup_width(cuda, golden, variant, wg_waves, monkeypatch):
     """K1 launched with 1 or 2 items (waves) per workgroup instead of 4 (OXH_K1_WG_WAVES): the item
     index comes from blockDim, so every item is still hashed exactly once; the ragged golden batch."""
@@ -184,7 +185,7 @@ def test_c2_full_size_sampled(cuda, oracle_lib):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("variant", [0, 264, 776, 392])
+@pytest.mark.parametrize("variant", [0, 264, 392])
 def test_chunk_digests(cuda, oracle_lib, variant):
     """Fixed-size chunk digests (no descriptor table), with the default K1, with K1R forced, and with a
     variant number that no kernel has (392: the default kernel runs, with its own launch geometry)."""
@@ -386,10 +387,10 @@ def _text_counts(b: bytes):
     return 1 + b.count(b"\n"), sum(1 for x in b if (x & 0xC0) != 0x80)
 
 
-@pytest.mark.parametrize("variant", [0, 8, 72, 4])
+@pytest.mark.parametrize("variant", [0, 8])
 def test_text_counts_fused_every_length(cuda, oracle_lib, variant):
-    """K1T: digests identical to K1 and text counts exact for every length class, aligned and not,
-    for the default dispatch and every K1T instantiation (<8>, <72>, <0> via a forced variant)."""
+    """K1T: digests identical to K1 and text counts exact for every length class, aligned and not.
+    Only K1T<72> ships; a forced K1 variant (8) must not change which K1T runs."""
     import torch
 
     from oxen_amd import _capi
@@ -975,7 +976,7 @@ def test_files_modified_metadata_hash_step(oracle_lib, tmp_path, cuda):
                                                                     file_metadata=meta)
 
 
-@pytest.mark.parametrize("variant", [0, 264, 260, 256, 776, 768])
+@pytest.mark.parametrize("variant", [0, 264, 1])
 def test_k1r_lockstep_rows(cuda, oracle_lib, variant):
     """K1R runs a wave's four items in lockstep to the longest: MiB items next to tiny ones, short-path
     items (<= 240 B) in the same wave, every byte shift, a batch size that leaves the last wave with 1-3
@@ -1007,7 +1008,7 @@ def test_k1r_lockstep_rows(cuda, oracle_lib, variant):
     assert not len(bad), [(int(i), int(lens[i]), int(offs[i]) % 4) for i in bad[:10]]
 
 
-@pytest.mark.parametrize("variant", [264, 260, 776])
+@pytest.mark.parametrize("variant", [264])
 def test_k1r_items_far_apart(cuda, oracle_lib, variant):
     """K1R with a wave's items more than 4 GiB apart (one descriptor cannot span them): each row's item
     is hashed alone, still bit-exact."""

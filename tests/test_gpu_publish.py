@@ -101,6 +101,9 @@ def test_big_file_allocation_failure_is_per_file(cuda, oracle_lib, tmp_path, mon
         monkeypatch.setenv("OXH_BIG_PIECE_MIB", str(1 << 19))
         d, sz, st = hasher.hash_files_128bit(paths, c)
         assert st == [0, _capi.OXH_ERR_NOMEM] and d == [oracle.xxh3_128_int(small), None]
+        # os_error is the errno of a failed open or read only: 0 for an allocation failure (include/oxen_hash.h)
+        d, sz, st, oserr = hasher.hash_files_with_errors_128bit(paths, None, c)
+        assert st == [0, _capi.OXH_ERR_NOMEM] and oserr == [0, 0]
         d, sz, st, stored = hasher.add_files(paths, root, c)
         assert st == [0, _capi.OXH_ERR_NOMEM] and stored == [True, False]
         assert not any(".oxentmp." in f for f in _tree(root))

@@ -165,3 +165,17 @@ def test_bench_reference_add_c1(oracle_lib):
 
     r = bench.cpu_oxen_add_c1(threads=2, reps=1)
     assert r["ok"] and r["files"] == 1001 and r["ms"] > 0
+
+
+def test_rust_debug_forms():
+    """Rust's `{:?}` of a Path (OsStr on Unix: Utf8Chunks Debug) and of a str, as hasher.rs's and
+    util::fs::metadata's error texts carry them (error.rs:1176-1182): a Path escapes the single quote and
+    writes bytes outside UTF-8 as \\xNN; both escape non-printable and grapheme-extended chars as \\u{..}."""
+    from oxen_amd import hasher
+
+    assert hasher.rust_path_debug("/tmp/a") == '"/tmp/a"'
+    assert hasher.rust_path_debug(b"it's\xff\xfe") == '"it\\\'s\\xFF\\xFE"'
+    assert hasher.rust_path_debug("a​b c x́é漢\U0001f402") == '"a\\u{200b}b\\u{a0}c x\\u{301}é漢\U0001f402"'
+    assert hasher.rust_path_debug('q"\\\n\r\t\0\x01\x7f') == '"q\\"\\\\\\n\\r\\t\\0\\u{1}\\u{7f}"'
+    assert hasher.rust_str_debug("it's") == '"it\'s"'
+    assert hasher.rust_io_error_debug(20) == 'Os { code: 20, kind: NotADirectory, message: "Not a directory" }'
