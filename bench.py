@@ -283,7 +283,14 @@ def main() -> None:
     # N > 1 over RCCL: each step's digest gather runs on the collective's stream while the next step
     # hashes into the other of two digest tables (shard.PipelinedGather: the gather of step k overlaps
     # the hash of k+1; a table is rewritten only after the gather that read it has finished)
-    pipe = PipelinedGather(n_items, world, dev) if multi and args.backend == "nccl" else None
+    # The gather is the C ABI's oxh_gather_digests (comm.py / csrc/comm.cpp: RCCL all-gather over xGMI),
+    # the call a Rust host links; rank 0's communicator id travels over the process group.
+    comm = None
+    if multi and args.backend == "nccl":
+        from oxen_amd.comm import comm_from_process_group
+
+        comm = comm_from_process_group(rank, world, dev.index)
+    pipe = PipelinedGather(n_items, world, dev, comm=comm) if comm is not None else None
 
     def step():
         if pipe is not None:
@@ -399,7 +406,9 @@ def main() -> None:
             "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (splitmix64 byte stream, seed %d+rank), device-resident in HBM" % args.seed,
             "config": {"workload": desc, "items_per_gpu": n_items, "item_bytes": item_len,
-                       "bytes_per_gpu": bytes_per_rank, "parallelism": f"files sharded x{world}, RCCL all-gather of digests" if multi else "single GPU",
+                       "bytes_per_gpu": bytes_per_rank, "parallelism": (f"files sharded x{world}, one RCCL all-gather of the digests per step "
+                                               f"({'oxh_gather_digests' if comm is not None else 'torch gloo rehearsal'})")
+                       if multi else "single GPU",
                        "kernel_variant": args.variant or "auto (8: 2-round ring, items > 16 KiB)"},
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -407,6 +416,8 @@ def main() -> None:
         print(json.dumps(result), flush=True)
     if multi:
         dist.barrier()
+        if comm is not None:
+            comm.close()
         dist.destroy_process_group()
 
 

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define OXH_ABI_VERSION 3
+#define OXH_ABI_VERSION 4
 
 /* status codes (also used per item in status[]) */
 #define OXH_OK 0
@@ -288,6 +288,28 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
                        uint32_t min_size, uint32_t avg_size, uint32_t max_size, uint32_t level,
                        uint64_t* d_chunk_offsets, uint64_t* d_chunk_lens, uint64_t* d_digests, uint64_t capacity,
                        uint64_t* first_chunk, void* stream);
+/* FastCDC from host memory to host memory: the block-level dedup chunker as the reference runs it --
+ * fs::read(input_file), v2020 chunking, xxh3_128 per chunk (fastcdchunker.rs:75-98) -- over n files
+ * (oxh_fastcdc_files: paths; each opened and read whole, its size from fstat) or n host buffers
+ * (oxh_fastcdc_host). The bytes stream through a bounded pipeline: parallel reads into a pinned
+ * bounce ring, H2D on a side stream into one of two device pieces of OXH_CDC_PIECE_MIB (default 1 GiB),
+ * chunked by oxh_fastcdc_device while the next piece is read. A file larger than what is left of a
+ * piece is chunked in segments; a chunk is kept only once `max_size` bytes after its start are known
+ * and the next segment is chunked from the first one that was not (a cut depends only on its start
+ * and the max bytes after it), so every boundary is the one the crate finds in the whole file.
+ * Output, in host memory: chunk k = bytes [chunk_offsets[k], + chunk_lens[k]) of its file (the
+ * crate's Chunk.offset / length), digests[2k..2k+1] its XXH3-128 (lo, hi; NULL = boundaries only);
+ * file i's chunks are first_chunk[i] .. first_chunk[i+1]-1 (n+1 entries). A file that cannot be
+ * opened (status OXH_ERR_OPEN) or read (OXH_ERR_IO, e.g. EISDIR, or the file ended early: os_error 0)
+ * has no chunks; the others are unaffected. sizes / status / os_error may be NULL. More chunks than
+ * `capacity` fail the call with OXH_ERR_INVALID (the text holds the count needed); the
+ * oxh_fastcdc_max_chunks bound of the sizes always suffices. Parameter ranges as oxh_fastcdc_device. */
+int oxh_fastcdc_files(oxh_ctx* ctx, const char* const* paths, uint64_t n, uint32_t min_size, uint32_t avg_size,
+                      uint32_t max_size, uint32_t level, uint64_t* chunk_offsets, uint64_t* chunk_lens, uint64_t* digests,
+                      uint64_t capacity, uint64_t* first_chunk, uint64_t* sizes, int32_t* status, int32_t* os_error);
+int oxh_fastcdc_host(oxh_ctx* ctx, const uint8_t* const* bufs, const uint64_t* lens, uint64_t n, uint32_t min_size,
+                     uint32_t avg_size, uint32_t max_size, uint32_t level, uint64_t* chunk_offsets, uint64_t* chunk_lens,
+                     uint64_t* digests, uint64_t capacity, uint64_t* first_chunk);
 /* Upper bound on the chunk count of files of these lengths (every chunk but a file's last is >= min). */
 uint64_t oxh_fastcdc_max_chunks(const uint64_t* lens, uint64_t n, uint32_t min_size);
 /* The compiled-in GEAR table (256 u64) and the (mask_s, mask_l) pair for an average size and
@@ -305,6 +327,30 @@ int oxh_combined_hash_device(const uint64_t* d_content, const uint64_t* d_metada
  * streams[offsets[i] .. offsets[i] + lens[i]). Blocks until `out` (2n u64) is filled. */
 int oxh_hash_streams(oxh_ctx* ctx, const uint8_t* streams, const uint64_t* offsets,
                      const uint64_t* lens, uint64_t n, uint64_t* out);
+
+/* ---------------------------------------------------------------- multi-GPU: the digest gather
+ * files shard across the GPUs of a node as contiguous byte-balanced ranges, one process
+ * per GPU and no data-path collective; the one exchange is the 16-B-per-file digest table, gathered over
+ * xGMI with RCCL. This replaces the reference's in-process fan-out of 64-file batches
+ * (core/v_latest/add.rs:422-425) when the shards are device-resident on several GPUs.
+ * RCCL is loaded at run time (librccl.so.1; $OXH_RCCL_LIB overrides); without it the calls fail with
+ * OXH_ERR_NODEVICE.
+ * One rank calls oxh_comm_unique_id and hands the OXH_COMM_ID_BYTES bytes to every rank out of band
+ * (as ncclGetUniqueId); each rank then calls oxh_comm_create with its rank and GPU (it blocks until all
+ * nranks have). oxh_gather_digests: counts[q] (host, nranks entries, the same on every rank) = rank q's
+ * item count; rank q's d_local holds its 2 * counts[q] u64 digests (lo, hi); d_full (2 * sum(counts) u64,
+ * device) receives every rank's table in rank order -- on every rank when root < 0 (all-gather), else on
+ * rank `root` only (d_full may be NULL on the others). Equal counts take one ncclAllGather / ncclGather,
+ * ragged ones a group of point-to-point transfers. Enqueued on `stream` (hipStream_t, NULL = the null
+ * stream); returns without waiting. A communicator is used by one thread at a time. */
+#define OXH_COMM_ID_BYTES 128
+typedef struct oxh_comm oxh_comm;
+int oxh_comm_unique_id(uint8_t* id);
+int oxh_comm_create(const uint8_t* id, int rank, int nranks, int device, oxh_comm** out);
+int oxh_comm_info(oxh_comm* comm, int* rank, int* nranks, int* device);
+int oxh_gather_digests(oxh_comm* comm, const uint64_t* d_local, const uint64_t* counts, uint64_t* d_full, int root,
+                       void* stream);
+int oxh_comm_destroy(oxh_comm* comm);
 
 /* ---------------------------------------------------------------- formatting (host only) */
 /* MerkleHash Display (merkle_hash.rs:73-77): format!("{:x}") -- lowercase, NOT zero-padded.

@@ -31,6 +31,7 @@ OXH_MODE_LANE = 2
 OXH_MODE_WAVE_SHORT = 3
 OXH_MODE_WAVE_PACKED = 4
 OXH_MAX_STAGING_BYTES = 2147483392  # 2 GiB - 256 (include/oxen_hash.h)
+OXH_COMM_ID_BYTES = 128
 
 _u64 = ctypes.c_uint64
 _u32 = ctypes.c_uint32
@@ -86,8 +87,17 @@ SIGNATURES = {
     "oxh_xxh3_stream_destroy": (_int, [_vp]),
     "oxh_fastcdc_device": (_int, [_vp, _u64p, _u64p, _u64, _u32, _u32, _u32, _u32, _vp, _vp, _vp, _u64, _u64p, _vp]),
     "oxh_fastcdc_max_chunks": (_u64, [_u64p, _u64, _u32]),
+    "oxh_fastcdc_files": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64, _u32, _u32, _u32, _u32, _u64p, _u64p, _u64p,
+                                 _u64, _u64p, _u64p, _i32p, _i32p]),
+    "oxh_fastcdc_host": (_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64p, _u64, _u32, _u32, _u32, _u32, _u64p, _u64p,
+                                _u64p, _u64, _u64p]),
     "oxh_fastcdc_gear": (_int, [_u64p]),
     "oxh_fastcdc_masks": (_int, [_u32, _u32, _u64p, _u64p]),
+    "oxh_comm_unique_id": (_int, [ctypes.c_char_p]),
+    "oxh_comm_create": (_int, [ctypes.c_char_p, _int, _int, _int, ctypes.POINTER(_vp)]),
+    "oxh_comm_info": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int), ctypes.POINTER(_int)]),
+    "oxh_gather_digests": (_int, [_vp, _vp, _u64p, _vp, _int, _vp]),
+    "oxh_comm_destroy": (_int, [_vp]),
 }
 
 _lib = None

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "liboxen_hash.so")
 SOURCES = [os.path.join(CSRC, "xxh3_kernels.hip"), os.path.join(CSRC, "oxen_hash_capi.hip"), os.path.join(CSRC, "fastcdc.hip"),
-           os.path.join(CSRC, "reader_pool.cpp")]
+           os.path.join(CSRC, "reader_pool.cpp"), os.path.join(CSRC, "comm.cpp"), os.path.join(CSRC, "fastcdc_host.cpp")]
 DEPS = SOURCES + [os.path.join(CSRC, "xxh3_device.hpp"), os.path.join(CSRC, "fastcdc_gear.h"), os.path.join(CSRC, "pool.hpp"), os.path.join(CSRC, "scratch.hpp"),
                   os.path.join(CSRC, "reader_pool.hpp"), os.path.join(ROOT, "include", "oxen_hash.h")]
 HELPER_SRC = os.path.join(CSRC, "hash_helper.cpp")

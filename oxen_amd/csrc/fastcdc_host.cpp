@@ -1,0 +1,626 @@
+// oxen_amd/csrc/fastcdc_host.cpp -- FastCDC chunking that starts and ends in host memory
+// (include/oxen_hash.h: oxh_fastcdc_files, oxh_fastcdc_host).
+//
+// The reference chunker reads a whole file into memory (`fs::read(input_file)`,
+// experiments/block-level-dedup/src/chunker/fastcdchunker.rs:75), runs fastcdc v2020 over it (:83-88)
+// and hashes every chunk with xxh3_128 (:95-98). Here the bytes go through a bounded pipeline instead:
+//
+//   readers (pool threads, pread / memcpy)  ->  pinned bounce ring (4 x 64 MiB)  --H2D, copy stream-->
+//   device piece buffer b (2 x 1 GiB)  --oxh_fastcdc_device on the compute stream: W + X (or F1-F3),
+//   then K1R over the chunks-->  chunk table + digests  --D2H-->  the caller's arrays
+//
+// Files are taken in order and packed into pieces; a file larger than what is left of a piece is
+// cut into segments. A chunk's cut depends only on its start and on the `max` bytes after it
+// (cut_gear scans at most `max` bytes, and the hash restarts at every chunk start), so a chunk of a
+// segment that starts at s with s + max <= segment end is exactly the crate's chunk; the first chunk
+// that is not is the CARRY, the exact start the file's next segment is chunked from. The next segment
+// is read from `max` bytes before the previous segment's end (the carry always lies in that tail), so
+// its bytes can be uploaded before the previous segment is chunked; the device call then starts the
+// segment's chunking at the carry. Two piece buffers let round r+1's reads and copies run while
+// round r is chunked on a worker thread.
+#include <hip/hip_runtime_api.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/oxen_hash.h"
+#include "pool.hpp"
+
+namespace oxh {
+int set_error(int code, const std::string& msg);            // oxen_hash_capi.hip
+int ctx_device(oxh_ctx* c);                                 // oxen_hash_capi.hip
+std::mutex& ctx_call_mutex(oxh_ctx* c);                     // ... serialises a context's non-engine calls
+void*& ctx_cdc_state(oxh_ctx* c, void (*deleter)(void*));   // ... a slot the context frees on destroy
+int default_reader_threads();                               // ... OXH_NUM_THREADS / the CPU quota, <= 16
+}  // namespace oxh
+
+namespace {
+
+constexpr uint64_t kCdcBounce = 64ull << 20;  // one pinned bounce buffer
+constexpr int kCdcNBounce = 4;                // the ring: reads of the next windows run while earlier H2Ds drain
+constexpr uint64_t kCdcPart = 4ull << 20;     // one reader task
+constexpr uint64_t kCdcAlign = 256;           // segment placement in a piece
+constexpr uint64_t kProbeWindow = 256;        // files opened (and stat'ed) ahead of the planner
+
+inline uint64_t align_up(uint64_t x) { return (x + kCdcAlign - 1) & ~(kCdcAlign - 1); }
+
+// Per-context state, created on first use and kept: the two device piece buffers, the pinned ring,
+// the chunk-table buffers, streams and a reader pool of its own (the context's engine keeps its
+// pools busy independently).
+struct CdcHost {
+    int device = 0;
+    hipStream_t copy = nullptr, comp = nullptr;
+    uint64_t piece = 0;
+    uint8_t* d_piece[2] = {};
+    hipEvent_t ev_copied[2] = {};
+    uint8_t* h_bounce[kCdcNBounce] = {};
+    hipEvent_t ev_bounce[kCdcNBounce] = {};
+    bool bounce_used[kCdcNBounce] = {};
+    uint64_t tab_cap = 0;  // entries of the chunk-table buffers below
+    uint64_t *d_off = nullptr, *d_len = nullptr, *d_dig = nullptr;
+    uint64_t *h_off = nullptr, *h_len = nullptr, *h_dig = nullptr;
+    oxh::Pool* pool = nullptr;
+
+    ~CdcHost() {
+        (void)hipSetDevice(device);
+        if (copy) (void)hipStreamSynchronize(copy);
+        if (comp) (void)hipStreamSynchronize(comp);
+        for (auto* p : d_piece)
+            if (p) (void)hipFree(p);
+        for (auto e : ev_copied)
+            if (e) (void)hipEventDestroy(e);
+        for (int i = 0; i < kCdcNBounce; ++i) {
+            if (h_bounce[i]) (void)hipHostFree(h_bounce[i]);
+            if (ev_bounce[i]) (void)hipEventDestroy(ev_bounce[i]);
+        }
+        free_tables();
+        if (copy) (void)hipStreamDestroy(copy);
+        if (comp) (void)hipStreamDestroy(comp);
+        delete pool;
+    }
+    void free_tables() {
+        for (auto* p : {d_off, d_len, d_dig})
+            if (p) (void)hipFree(p);
+        for (auto* p : {h_off, h_len, h_dig})
+            if (p) (void)hipHostFree(p);
+        d_off = d_len = d_dig = h_off = h_len = h_dig = nullptr;
+        tab_cap = 0;
+    }
+    // chunk-table buffers of at least `need` entries
+    int tables(uint64_t need) {
+        if (need <= tab_cap) return OXH_OK;
+        free_tables();
+        const uint64_t cap = std::max<uint64_t>(need + need / 4, 1 << 16);
+        bool ok = hipMalloc(&d_off, cap * 8) == hipSuccess && hipMalloc(&d_len, cap * 8) == hipSuccess &&
+                  hipMalloc(&d_dig, cap * 16) == hipSuccess &&
+                  hipHostMalloc(&h_off, cap * 8, hipHostMallocDefault) == hipSuccess &&
+                  hipHostMalloc(&h_len, cap * 8, hipHostMallocDefault) == hipSuccess &&
+                  hipHostMalloc(&h_dig, cap * 16, hipHostMallocDefault) == hipSuccess;
+        if (!ok) {
+            (void)hipGetLastError();
+            free_tables();
+            return oxh::set_error(OXH_ERR_NOMEM, "FastCDC chunk-table buffers");
+        }
+        tab_cap = cap;
+        return OXH_OK;
+    }
+};
+
+void free_cdc_host(void* p) { delete static_cast<CdcHost*>(p); }
+
+// the context's CdcHost with pieces of `piece` bytes (re-made if the size changed)
+int cdc_host(oxh_ctx* ctx, uint64_t piece, CdcHost** out) {
+    void*& slot = oxh::ctx_cdc_state(ctx, free_cdc_host);
+    CdcHost* h = static_cast<CdcHost*>(slot);
+    if (h && h->piece == piece) {
+        *out = h;
+        return OXH_OK;
+    }
+    delete h;
+    slot = nullptr;
+    h = new CdcHost;
+    h->device = oxh::ctx_device(ctx);
+    h->piece = piece;
+    auto bad = [&](int code, const char* what) {
+        (void)hipGetLastError();
+        delete h;
+        return oxh::set_error(code, std::string("FastCDC host pipeline: ") + what);
+    };
+    if (hipStreamCreateWithFlags(&h->copy, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&h->comp, hipStreamNonBlocking) != hipSuccess)
+        return bad(OXH_ERR_HIP, "streams");
+    for (int b = 0; b < 2; ++b) {
+        if (hipMalloc(&h->d_piece[b], piece + 4096) != hipSuccess) return bad(OXH_ERR_NOMEM, "device piece buffers");
+        if (hipEventCreateWithFlags(&h->ev_copied[b], hipEventDisableTiming) != hipSuccess) return bad(OXH_ERR_HIP, "events");
+    }
+    for (int i = 0; i < kCdcNBounce; ++i) {
+        if (hipHostMalloc(&h->h_bounce[i], kCdcBounce, hipHostMallocDefault) != hipSuccess)
+            return bad(OXH_ERR_NOMEM, "pinned bounce buffers");
+        if (hipEventCreateWithFlags(&h->ev_bounce[i], hipEventDisableTiming) != hipSuccess) return bad(OXH_ERR_HIP, "events");
+    }
+    h->pool = new oxh::Pool(oxh::default_reader_threads());
+    slot = h;
+    *out = h;
+    return OXH_OK;
+}
+
+// Where item i's bytes come from.
+struct CdcSource {
+    virtual ~CdcSource() = default;
+    // OXH_OK with its size, or the item's status (OXH_ERR_OPEN / OXH_ERR_IO) and errno
+    virtual int open(uint64_t i, uint64_t& size, int& oserr) = 0;
+    // [off, off + n) into dst; false with errno (0: the file ended early); called from many threads
+    virtual bool read(uint64_t i, uint64_t off, uint64_t n, uint8_t* dst, int& oserr) = 0;
+    virtual void close(uint64_t) {}
+};
+
+// fs::read(input_file) (fastcdchunker.rs:75): File::open, then the whole file. A directory opens and
+// fails its read with EISDIR, as read_to_end does; the size is the open file's fstat.
+struct FileSrc final : CdcSource {
+    const char* const* paths;
+    std::vector<int> fds;
+    FileSrc(const char* const* p, uint64_t n) : paths(p), fds(n, -1) {}
+    ~FileSrc() override {
+        for (int fd : fds)
+            if (fd >= 0) ::close(fd);
+    }
+    int open(uint64_t i, uint64_t& size, int& oserr) override {
+        size = 0;
+        const int fd = ::open(paths[i], O_RDONLY | O_CLOEXEC);
+        if (fd < 0) {
+            oserr = errno;
+            return OXH_ERR_OPEN;
+        }
+        struct stat sb;
+        if (fstat(fd, &sb) != 0) {
+            oserr = errno;
+            ::close(fd);
+            return OXH_ERR_IO;
+        }
+        if (S_ISDIR(sb.st_mode)) {
+            oserr = EISDIR;
+            ::close(fd);
+            return OXH_ERR_IO;
+        }
+        fds[i] = fd;
+        size = (uint64_t)sb.st_size;
+        return OXH_OK;
+    }
+    bool read(uint64_t i, uint64_t off, uint64_t n, uint8_t* dst, int& oserr) override {
+        for (uint64_t got = 0; got < n;) {
+            const ssize_t k = pread(fds[i], dst + got, n - got, (off_t)(off + got));
+            if (k < 0 && errno == EINTR) continue;
+            if (k < 0) oserr = errno;
+            if (k <= 0) return false;
+            got += (uint64_t)k;
+        }
+        return true;
+    }
+    void close(uint64_t i) override {
+        if (fds[i] >= 0) ::close(fds[i]);
+        fds[i] = -1;
+    }
+};
+
+struct MemSrc final : CdcSource {
+    const uint8_t* const* bufs;
+    const uint64_t* lens;
+    MemSrc(const uint8_t* const* b, const uint64_t* l) : bufs(b), lens(l) {}
+    int open(uint64_t i, uint64_t& size, int&) override {
+        size = lens[i];
+        return OXH_OK;
+    }
+    bool read(uint64_t i, uint64_t off, uint64_t n, uint8_t* dst, int&) override {
+        memcpy(dst, bufs[i] + off, n);
+        return true;
+    }
+};
+
+struct FileState {
+    uint64_t size = 0;
+    std::atomic<int> status{OXH_OK}, oserr{0};
+    bool probed = false;
+    uint64_t carry = 0;      // the exact chunk start the next segment is chunked from (stitcher)
+    uint64_t next_lo = 0;    // where the next segment's read starts (planner)
+    uint64_t first = 0;      // output index of the file's first chunk (stitcher)
+    int segs_left = 0;       // segments planned but not yet read (planner / reader; closes the fd)
+};
+
+struct Seg {
+    uint64_t file, lo, hi, poff;  // file bytes [lo, hi) at piece offset poff
+    bool first, last;             // the file's first / last segment
+};
+
+struct Round {
+    int b = 0;
+    std::vector<Seg> segs;
+    bool io_done = false;
+};
+
+struct Call {
+    CdcHost* h;
+    CdcSource* src;
+    uint64_t n;
+    uint32_t mn, av, mx, lv;
+    uint64_t* c_off;
+    uint64_t* c_len;
+    uint64_t* dig;
+    uint64_t capacity;
+    uint64_t* first_chunk;
+    std::vector<FileState> files;
+    uint64_t total = 0;  // chunks emitted (written while < capacity)
+    std::atomic<int> rc{OXH_OK};
+    std::string err;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<Round> ready;   // rounds whose bytes are on the device, for the chunking thread
+    bool planner_done = false;
+    bool buf_busy[2] = {false, false};
+    double t_read = 0, t_chunk = 0, t_wait = 0;
+
+    void fail(int code, const std::string& m) {
+        int z = OXH_OK;
+        if (rc.compare_exchange_strong(z, code)) {
+            std::lock_guard<std::mutex> g(mu);
+            err = m;
+        }
+        cv.notify_all();
+    }
+};
+
+double now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+
+// Stitch one round's chunk table into the caller's arrays (round order = file order = output order).
+void stitch(Call& C, const Round& R, const std::vector<uint64_t>& first, const std::vector<uint64_t>& item_off) {
+    CdcHost& h = *C.h;
+    for (size_t j = 0; j < R.segs.size(); ++j) {
+        const Seg& s = R.segs[j];
+        FileState& F = C.files[s.file];
+        if (s.first) F.first = C.total;
+        if (F.status.load() != OXH_OK) {  // a read of this file failed (this round or before): drop its chunks
+            C.total = F.first;
+            if (s.last) C.first_chunk[s.file + 1] = C.total;
+            continue;
+        }
+        const uint64_t a = first[j], e = first[j + 1];
+        const uint64_t start = s.first ? s.lo : F.carry;
+        bool carried = false;
+        for (uint64_t k = a; k < e; ++k) {
+            const uint64_t pos = start + (h.h_off[k] - item_off[j]);  // the chunk's offset in its file
+            if (!s.last && pos + C.mx > s.hi) {  // not certain before the file's next bytes: chunk it again
+                F.carry = pos;
+                carried = true;
+                break;
+            }
+            if (C.total < C.capacity) {
+                C.c_off[C.total] = pos;
+                C.c_len[C.total] = h.h_len[k];
+                if (C.dig) {
+                    C.dig[2 * C.total] = h.h_dig[2 * k];
+                    C.dig[2 * C.total + 1] = h.h_dig[2 * k + 1];
+                }
+            }
+            ++C.total;
+        }
+        if (!s.last && !carried) F.carry = s.hi;  // every chunk final: the next one starts at the segment end
+        if (s.last) C.first_chunk[s.file + 1] = C.total;
+    }
+}
+
+// The chunking thread: rounds in order; each waits for its copies, is chunked on the device, its table
+// comes back, and its piece buffer is handed back to the planner.
+void chunk_rounds(Call& C) {
+    CdcHost& h = *C.h;
+    (void)hipSetDevice(h.device);
+    std::vector<uint64_t> offs, lens, first, item_off;
+    for (;;) {
+        Round R;
+        {
+            std::unique_lock<std::mutex> lk(C.mu);
+            const double t0 = now();
+            C.cv.wait(lk, [&] { return !C.ready.empty() || C.planner_done || C.rc.load() != OXH_OK; });
+            C.t_wait += now() - t0;
+            if (C.rc.load() != OXH_OK) return;
+            if (C.ready.empty()) return;  // planner done, nothing left
+            R = std::move(C.ready.front());
+            C.ready.pop_front();
+        }
+        const double t0 = now();
+        const size_t m = R.segs.size();
+        offs.assign(m, 0), lens.assign(m, 0), item_off.assign(m, 0), first.assign(m + 1, 0);
+        for (size_t j = 0; j < m; ++j) {
+            const Seg& s = R.segs[j];
+            const FileState& F = C.files[s.file];
+            if (F.status.load() != OXH_OK) continue;  // an empty item keeps the indices
+            const uint64_t start = s.first ? s.lo : F.carry;
+            if (start < s.lo || start > s.hi) {
+                C.fail(OXH_ERR_HIP, "FastCDC host pipeline: carry outside its segment");
+                return;
+            }
+            offs[j] = item_off[j] = s.poff + (start - s.lo);
+            lens[j] = s.hi - start;
+        }
+        const uint64_t need = oxh_fastcdc_max_chunks(lens.data(), m, C.mn) + 1;
+        int rc = h.tables(need);
+        if (rc == OXH_OK && hipStreamWaitEvent(h.comp, h.ev_copied[R.b], 0) != hipSuccess) rc = oxh::set_error(OXH_ERR_HIP, "wait copies");
+        if (rc == OXH_OK)
+            rc = oxh_fastcdc_device(h.d_piece[R.b], offs.data(), lens.data(), m, C.mn, C.av, C.mx, C.lv, h.d_off, h.d_len,
+                                    C.dig ? h.d_dig : nullptr, h.tab_cap, first.data(), h.comp);
+        const uint64_t tot = first[m];
+        if (rc == OXH_OK && tot) {
+            if (hipMemcpyAsync(h.h_off, h.d_off, tot * 8, hipMemcpyDeviceToHost, h.comp) != hipSuccess ||
+                hipMemcpyAsync(h.h_len, h.d_len, tot * 8, hipMemcpyDeviceToHost, h.comp) != hipSuccess ||
+                (C.dig && hipMemcpyAsync(h.h_dig, h.d_dig, tot * 16, hipMemcpyDeviceToHost, h.comp) != hipSuccess))
+                rc = oxh::set_error(OXH_ERR_HIP, "chunk table D2H");
+        }
+        if (rc == OXH_OK && hipStreamSynchronize(h.comp) != hipSuccess) rc = oxh::set_error(OXH_ERR_HIP, "chunking stream");
+        if (rc != OXH_OK) {
+            C.fail(rc, oxh_last_error());
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(C.mu);
+            C.buf_busy[R.b] = false;  // the piece buffer may take the next round's bytes
+        }
+        C.cv.notify_all();
+        stitch(C, R, first, item_off);
+        C.t_chunk += now() - t0;
+    }
+}
+
+// Read one round's segments into the piece buffer through the bounce ring (windows of kCdcBounce of
+// the piece, read by the pool in kCdcPart tasks, each window's H2D once its reads are done; up to
+// kCdcNBounce - 1 windows reading while the oldest one's copy is issued).
+int upload_round(Call& C, const Round& R) {
+    CdcHost& h = *C.h;
+    struct Part {
+        uint64_t file, off, n, boff;
+    };
+    struct Window {
+        int bb = 0;
+        uint64_t base = 0, used = 0;
+        std::vector<Part> parts;
+        std::function<void(int)> fn;
+        oxh::Pool::Group grp;
+    };
+    std::vector<std::unique_ptr<Window>> wins;
+    for (const Seg& s : R.segs) {
+        if (C.files[s.file].status.load() != OXH_OK) continue;
+        for (uint64_t o = s.lo; o < s.hi;) {
+            const uint64_t p = s.poff + (o - s.lo), w = p / kCdcBounce;
+            const uint64_t n = std::min({s.hi - o, kCdcPart, (w + 1) * kCdcBounce - p});
+            while (wins.size() <= w) {
+                wins.emplace_back(new Window);
+                wins.back()->base = (uint64_t)(wins.size() - 1) * kCdcBounce;
+            }
+            Window& W = *wins[w];
+            W.parts.push_back({s.file, o, n, p - W.base});
+            W.used = std::max(W.used, p - W.base + n);
+            o += n;
+        }
+    }
+    std::deque<Window*> inflight;
+    uint64_t next_bb = 0;
+    auto finish = [&](Window& W) -> int {
+        W.grp.wait();
+        if (W.used == 0) return OXH_OK;
+        if (hipMemcpyAsync(h.d_piece[R.b] + W.base, h.h_bounce[W.bb], W.used, hipMemcpyHostToDevice, h.copy) != hipSuccess ||
+            hipEventRecord(h.ev_bounce[W.bb], h.copy) != hipSuccess)
+            return oxh::set_error(OXH_ERR_HIP, "piece H2D");
+        h.bounce_used[W.bb] = true;
+        return OXH_OK;
+    };
+    int rc = OXH_OK;
+    for (auto& wp : wins) {
+        Window& W = *wp;
+        if (W.parts.empty()) continue;
+        W.bb = (int)(next_bb++ % kCdcNBounce);
+        if (h.bounce_used[W.bb] && hipEventSynchronize(h.ev_bounce[W.bb]) != hipSuccess) {
+            rc = oxh::set_error(OXH_ERR_HIP, "bounce buffer wait");
+            break;
+        }
+        h.bounce_used[W.bb] = false;
+        uint8_t* dst = h.h_bounce[W.bb];
+        W.fn = [&C, &W, dst](int t) {
+            const Part& P = W.parts[(size_t)t];
+            FileState& F = C.files[P.file];
+            if (F.status.load(std::memory_order_relaxed) != OXH_OK) return;
+            int e = 0;
+            if (!C.src->read(P.file, P.off, P.n, dst + P.boff, e)) {
+                int z = OXH_OK;
+                if (F.status.compare_exchange_strong(z, OXH_ERR_IO)) F.oserr.store(e);
+            }
+        };
+        h.pool->start((int)W.parts.size(), W.fn, W.grp);
+        inflight.push_back(&W);
+        if ((int)inflight.size() >= kCdcNBounce - 1) {
+            rc = finish(*inflight.front());
+            inflight.pop_front();
+            if (rc) break;
+        }
+    }
+    while (!inflight.empty()) {  // (after an error too: no task may outlive its window)
+        const int r2 = finish(*inflight.front());
+        inflight.pop_front();
+        if (rc == OXH_OK) rc = r2;
+    }
+    if (rc == OXH_OK && hipEventRecord(h.ev_copied[R.b], h.copy) != hipSuccess) rc = oxh::set_error(OXH_ERR_HIP, "copy event");
+    return rc;
+}
+
+int run(oxh_ctx* ctx, CdcSource& src, uint64_t n, uint32_t mn, uint32_t av, uint32_t mx, uint32_t lv, uint64_t* c_off,
+        uint64_t* c_len, uint64_t* dig, uint64_t capacity, uint64_t* first_chunk, uint64_t* sizes, int32_t* status,
+        int32_t* os_error) {
+    if (!ctx) return oxh::set_error(OXH_ERR_INVALID, "null context");
+    if (!first_chunk) return oxh::set_error(OXH_ERR_INVALID, "null first_chunk");
+    if (capacity && (!c_off || !c_len)) return oxh::set_error(OXH_ERR_INVALID, "null chunk table");
+    // the crate's asserts (v2020::FastCDC::with_level), checked before any I/O
+    uint64_t ms = 0, ml = 0;
+    if (mn < 64 || mn > 1048576) return oxh::set_error(OXH_ERR_INVALID, "min_size must be in [64, 1048576]");
+    if (mx < 1024 || mx > 16777216) return oxh::set_error(OXH_ERR_INVALID, "max_size must be in [1024, 16777216]");
+    if (int rc = oxh_fastcdc_masks(av, lv, &ms, &ml)) return rc;
+    std::lock_guard<std::mutex> call_lock(oxh::ctx_call_mutex(ctx));
+    (void)hipSetDevice(oxh::ctx_device(ctx));
+    // pieces of OXH_CDC_PIECE_MIB (default 1 GiB); a segment is at least 16 MiB and 4 max chunks
+    const char* pe = getenv("OXH_CDC_PIECE_MIB");
+    const uint64_t min_seg = std::max<uint64_t>(16ull << 20, 4ull * mx + kCdcAlign);
+    uint64_t piece = (pe && atoll(pe) > 0 ? (uint64_t)atoll(pe) : 1024ull) << 20;
+    piece = std::min<uint64_t>(std::max<uint64_t>(piece, 2 * min_seg), 3ull << 30);
+    piece = (piece + kCdcBounce - 1) / kCdcBounce * kCdcBounce;
+    CdcHost* h = nullptr;
+    if (int rc = cdc_host(ctx, piece, &h)) return rc;
+
+    Call C;
+    C.h = h, C.src = &src, C.n = n, C.mn = mn, C.av = av, C.mx = mx, C.lv = lv;
+    C.c_off = c_off, C.c_len = c_len, C.dig = dig, C.capacity = capacity, C.first_chunk = first_chunk;
+    C.files = std::vector<FileState>(n);
+    first_chunk[0] = 0;
+    static const bool trace = getenv("OXH_TRACE") != nullptr;
+    const double t_start = now();
+    std::thread chunker(chunk_rounds, std::ref(C));
+
+    // probe (open + fstat) the files [lo, hi) in parallel
+    uint64_t probed = 0;
+    auto probe_to = [&](uint64_t hi) {
+        hi = std::min(hi, n);
+        if (hi <= probed) return;
+        const uint64_t lo = probed;
+        h->pool->parallel_for((int)(hi - lo), [&](int t) {
+            FileState& F = C.files[lo + (uint64_t)t];
+            int e = 0;
+            const int st = src.open(lo + (uint64_t)t, F.size, e);
+            F.status.store(st);
+            F.oserr.store(e);
+            F.probed = true;
+        });
+        probed = hi;
+    };
+
+    int rc = OXH_OK;
+    uint64_t cur = 0;  // the planner's file
+    int round_no = 0;
+    while (cur < n && C.rc.load() == OXH_OK) {
+        Round R;
+        R.b = round_no & 1;
+        // plan: files in order into this piece; a file that does not fit whole takes the rest of the
+        // piece (if at least min_seg) and continues in the next round from `max` before its end
+        uint64_t off = 0;
+        while (cur < n) {
+            if (cur >= probed) probe_to(cur + kProbeWindow);
+            FileState& F = C.files[cur];
+            if (F.status.load() != OXH_OK || F.size == 0) {  // no (more) chunks: an error, or an empty file
+                // (a file whose read failed in an earlier round keeps its first output index: the
+                // stitcher drops what it emitted for it)
+                R.segs.push_back({cur, 0, 0, 0, F.next_lo == 0, true});
+                ++cur;
+                continue;
+            }
+            const uint64_t lo = F.next_lo, left = F.size - lo;
+            const uint64_t at = align_up(off);
+            const uint64_t room = at < piece ? piece - at : 0;
+            if (left <= room) {
+                R.segs.push_back({cur, lo, F.size, at, lo == 0, true});
+                ++F.segs_left;
+                off = at + left;
+                ++cur;
+                continue;
+            }
+            if (room >= min_seg) {
+                R.segs.push_back({cur, lo, lo + room, at, lo == 0, false});
+                ++F.segs_left;
+                F.next_lo = lo + room - mx;  // the carry lies in (end - max, end]
+            }
+            break;
+        }
+        // the piece buffer: free once the chunking thread is done with round - 2
+        {
+            std::unique_lock<std::mutex> lk(C.mu);
+            const double t0 = now();
+            C.cv.wait(lk, [&] { return !C.buf_busy[R.b] || C.rc.load() != OXH_OK; });
+            C.t_wait += now() - t0;
+            if (C.rc.load() != OXH_OK) break;
+            C.buf_busy[R.b] = true;
+        }
+        const double t0 = now();
+        rc = upload_round(C, R);
+        C.t_read += now() - t0;
+        for (const Seg& s : R.segs)  // a file's descriptor closes after its last segment's reads
+            if (s.hi > s.lo && --C.files[s.file].segs_left == 0 && s.last) src.close(s.file);
+        if (rc) {
+            C.fail(rc, oxh_last_error());
+            break;
+        }
+        {
+            std::lock_guard<std::mutex> g(C.mu);
+            C.ready.push_back(std::move(R));
+        }
+        C.cv.notify_all();
+        ++round_no;
+    }
+    {
+        std::lock_guard<std::mutex> g(C.mu);
+        C.planner_done = true;
+    }
+    C.cv.notify_all();
+    chunker.join();
+    (void)hipStreamSynchronize(h->copy);
+    for (uint64_t i = 0; i < n; ++i) src.close(i);
+    if (C.rc.load() != OXH_OK) return oxh::set_error(C.rc.load(), "FastCDC host pipeline: " + C.err);
+    for (uint64_t i = 0; i < n; ++i) {
+        const FileState& F = C.files[i];
+        const bool ok = F.status.load() == OXH_OK;
+        if (sizes) sizes[i] = F.size;  // fstat's size (0 when the open failed)
+        if (status) status[i] = F.status.load();
+        if (os_error) os_error[i] = ok ? 0 : F.oserr.load();
+    }
+    if (trace)
+        fprintf(stderr, "[oxh] fastcdc_host: %llu items, %d rounds of %llu MiB, %llu chunks: total %.1f ms, reads+H2D %.1f, "
+                "chunking+D2H+stitch %.1f, waits %.1f\n", (unsigned long long)n, round_no, (unsigned long long)(piece >> 20),
+                (unsigned long long)C.total, 1e3 * (now() - t_start), 1e3 * C.t_read, 1e3 * C.t_chunk, 1e3 * C.t_wait);
+    if (C.total > capacity)
+        return oxh::set_error(OXH_ERR_INVALID, "chunk capacity too small: need " + std::to_string(C.total) + " entries");
+    return OXH_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int oxh_fastcdc_files(oxh_ctx* ctx, const char* const* paths, uint64_t n, uint32_t min_size, uint32_t avg_size,
+                      uint32_t max_size, uint32_t level, uint64_t* chunk_offsets, uint64_t* chunk_lens, uint64_t* digests,
+                      uint64_t capacity, uint64_t* first_chunk, uint64_t* sizes, int32_t* status, int32_t* os_error) {
+    if (n && !paths) return oxh::set_error(OXH_ERR_INVALID, "null paths");
+    for (uint64_t i = 0; i < n; ++i)
+        if (!paths[i]) return oxh::set_error(OXH_ERR_INVALID, "null path");
+    FileSrc src(paths, n);
+    return run(ctx, src, n, min_size, avg_size, max_size, level, chunk_offsets, chunk_lens, digests, capacity, first_chunk,
+               sizes, status, os_error);
+}
+
+int oxh_fastcdc_host(oxh_ctx* ctx, const uint8_t* const* bufs, const uint64_t* lens, uint64_t n, uint32_t min_size,
+                     uint32_t avg_size, uint32_t max_size, uint32_t level, uint64_t* chunk_offsets, uint64_t* chunk_lens,
+                     uint64_t* digests, uint64_t capacity, uint64_t* first_chunk) {
+    if (n && (!bufs || !lens)) return oxh::set_error(OXH_ERR_INVALID, "null buffers");
+    for (uint64_t i = 0; i < n; ++i)
+        if (lens[i] && !bufs[i]) return oxh::set_error(OXH_ERR_INVALID, "null buffer");
+    MemSrc src(bufs, lens);
+    return run(ctx, src, n, min_size, avg_size, max_size, level, chunk_offsets, chunk_lens, digests, capacity, first_chunk,
+               nullptr, nullptr, nullptr);
+}
+
+}  // extern "C"

@@ -246,9 +246,10 @@ int default_threads() {
 }  // namespace
 
 namespace oxh {
-// for the other translation units of the library (fastcdc.hip)
+// for the other translation units of the library (fastcdc.hip, fastcdc_host.cpp, comm.cpp)
 int set_error(int code, const std::string& msg) { return fail(code, msg); }
 int cpu_quota() { return usable_cpus(); }
+int default_reader_threads() { return default_threads(); }
 }  // namespace oxh
 
 // ---------------------------------------------------------------- context
@@ -291,6 +292,8 @@ struct oxh_ctx {
     oxh::Pool* wpool = nullptr;  // consumers of hashed bytes (fused publish), created on first use
     oxh::Pool* rpool = nullptr;  // streaming-pipeline file readers (stream_files)
     std::mutex mu;
+    void* cdc = nullptr;                 // FastCDC host pipeline (fastcdc_host.cpp), created on first use
+    void (*cdc_free)(void*) = nullptr;
 };
 
 namespace {
@@ -1064,6 +1067,8 @@ int oxh_ctx_destroy(oxh_ctx* c) {
         c->engine.join();
     }
     (void)hipSetDevice(c->device);
+    if (c->cdc && c->cdc_free) c->cdc_free(c->cdc);
+    c->cdc = nullptr;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     for (int s = 0; s < NSLOT; ++s) {
@@ -1100,6 +1105,18 @@ int oxh_ctx_destroy(oxh_ctx* c) {
 }
 
 void* oxh_ctx_stream(oxh_ctx* c) { return c ? (void*)c->stream : nullptr; }
+}  // extern "C"
+
+namespace oxh {
+int ctx_device(oxh_ctx* c) { return c->device; }
+std::mutex& ctx_call_mutex(oxh_ctx* c) { return c->mu; }
+void*& ctx_cdc_state(oxh_ctx* c, void (*deleter)(void*)) {
+    c->cdc_free = deleter;
+    return c->cdc;
+}
+}  // namespace oxh
+
+extern "C" {
 
 int oxh_xxh3_128_batch_device(const void* d_arena, const uint64_t* d_offsets, const uint64_t* d_lens, uint64_t n,
                               uint64_t* d_out, int mode, void* stream) {

@@ -16,6 +16,7 @@ u64, chunks: Vec<String>}` (:11-16, :110-121). Boundaries and digests both come 
 """
 from __future__ import annotations
 
+import ctypes
 import os
 import struct
 from typing import Optional
@@ -122,6 +123,96 @@ def decode_archive_metadata(buf: bytes) -> tuple[int, list[dict]]:
     return chunk, entries
 
 
+class FastCdcTable:
+    """A chunk table in host memory: chunk k = bytes [offsets[k], offsets[k] + lens[k]) of its file,
+    digests[k] = (lo, hi) of its XXH3-128 (None when not asked for); file i's chunks are rows
+    first[i] .. first[i+1]-1. sizes / status / os_error per file (oxh_fastcdc_files)."""
+
+    def __init__(self, offsets, lens, digests, first, sizes=None, status=None, os_error=None):
+        self.offsets, self.lens, self.digests, self.first = offsets, lens, digests, first
+        self.sizes, self.status, self.os_error = sizes, status, os_error
+
+    def file(self, i: int):
+        a, b = int(self.first[i]), int(self.first[i + 1])
+        return self.offsets[a:b], self.lens[a:b], (self.digests[a:b] if self.digests is not None else None)
+
+
+def _need_from_error(e: _capi.OxenError) -> Optional[int]:
+    import re
+
+    m = re.search(r"need (\d+) entries", str(e))
+    return int(m.group(1)) if m and e.code == _capi.OXH_ERR_INVALID else None
+
+
+def fastcdc_files(paths, min_size: int, avg_size: int, max_size: int, level: int = 1, digests: bool = True,
+                  ctx: Optional[_capi.Context] = None) -> FastCdcTable:
+    """oxh_fastcdc_files: FastCDC v2020 boundaries and XXH3-128 chunk digests of files on disk, read by
+    the library (fastcdchunker.rs:75-98: fs::read, v2020 chunking, xxh3_128 per chunk), results in
+    host memory. A file that cannot be opened / read has no chunks and its status / errno set."""
+    from .hasher import _PathTable, default_context
+
+    ctx = ctx or default_context()
+    n = len(paths)
+    sizes_hint = np.zeros(n, dtype=np.uint64)
+    for i, p in enumerate(paths):
+        try:
+            sizes_hint[i] = os.stat(p).st_size
+        except OSError:
+            pass
+    L = _capi.lib()
+    cap = max(1, int(L.oxh_fastcdc_max_chunks(sizes_hint.ctypes.data_as(_capi._u64p), n, max(1, int(min_size)))))
+    table = _PathTable(paths) if n else None
+    for _ in range(3):  # a file that grew since the stat above needs a larger table: retry with the count
+        off = np.zeros(cap, dtype=np.uint64)
+        ln = np.zeros(cap, dtype=np.uint64)
+        dig = np.zeros((cap, 2), dtype=np.uint64) if digests else None
+        first = np.zeros(n + 1, dtype=np.uint64)
+        sizes = np.zeros(n, dtype=np.uint64)
+        status = np.zeros(n, dtype=np.int32)
+        oserr = np.zeros(n, dtype=np.int32)
+        rc = L.oxh_fastcdc_files(ctx.handle, table.arg if table else None, n, int(min_size), int(avg_size), int(max_size),
+                                 int(level), off.ctypes.data_as(_capi._u64p), ln.ctypes.data_as(_capi._u64p),
+                                 dig.ctypes.data_as(_capi._u64p) if dig is not None else None, cap,
+                                 first.ctypes.data_as(_capi._u64p), sizes.ctypes.data_as(_capi._u64p),
+                                 status.ctypes.data_as(_capi._i32p), oserr.ctypes.data_as(_capi._i32p))
+        try:
+            _capi.check(rc, "oxh_fastcdc_files")
+        except _capi.OxenError as e:
+            need = _need_from_error(e)
+            if need is None:
+                raise
+            cap = need
+            continue
+        total = int(first[n])
+        return FastCdcTable(off[:total], ln[:total], dig[:total] if dig is not None else None, first, sizes, status, oserr)
+    raise _capi.OxenError("oxh_fastcdc_files: the files keep growing", _capi.OXH_ERR_INVALID)
+
+
+def fastcdc_host(buffers, min_size: int, avg_size: int, max_size: int, level: int = 1, digests: bool = True,
+                 ctx: Optional[_capi.Context] = None) -> FastCdcTable:
+    """oxh_fastcdc_host: the same over host buffers (bytes / numpy uint8 arrays)."""
+    from .hasher import default_context
+
+    ctx = ctx or default_context()
+    arrs = [np.frombuffer(b, dtype=np.uint8) if isinstance(b, (bytes, bytearray, memoryview)) else np.ascontiguousarray(b, dtype=np.uint8)
+            for b in buffers]
+    n = len(arrs)
+    lens_in = np.array([a.size for a in arrs], dtype=np.uint64)
+    ptrs = (ctypes.c_char_p * max(n, 1))(*[ctypes.cast(a.ctypes.data, ctypes.c_char_p) if a.size else None for a in arrs])
+    L = _capi.lib()
+    cap = max(1, int(L.oxh_fastcdc_max_chunks(lens_in.ctypes.data_as(_capi._u64p), n, max(1, int(min_size)))))
+    off = np.zeros(cap, dtype=np.uint64)
+    ln = np.zeros(cap, dtype=np.uint64)
+    dig = np.zeros((cap, 2), dtype=np.uint64) if digests else None
+    first = np.zeros(n + 1, dtype=np.uint64)
+    _capi.check(L.oxh_fastcdc_host(ctx.handle, ptrs, lens_in.ctypes.data_as(_capi._u64p), n, int(min_size), int(avg_size),
+                                   int(max_size), int(level), off.ctypes.data_as(_capi._u64p), ln.ctypes.data_as(_capi._u64p),
+                                   dig.ctypes.data_as(_capi._u64p) if dig is not None else None, cap,
+                                   first.ctypes.data_as(_capi._u64p)), "oxh_fastcdc_host")
+    total = int(first[n])
+    return FastCdcTable(off[:total], ln[:total], dig[:total] if dig is not None else None, first)
+
+
 class FastCDChunker:
     """fastcdchunker.rs:30-66 + the Chunker trait (chunker.rs): name / pack / unpack / get_chunk_hashes."""
 
@@ -144,20 +235,31 @@ class FastCDChunker:
                                               self.max_chunk_size)
         return to_numpy_u64(c_off), to_numpy_u64(c_len), to_numpy_u64(dig).reshape(-1, 2)
 
-    def pack(self, input_file: str, output_dir: str) -> str:
+    def pack(self, input_file: str, output_dir: str, ctx: Optional[_capi.Context] = None) -> str:
+        """fastcdchunker.rs:72-122. The library reads the file (oxh_fastcdc_files: its bytes stream to
+        the device once; boundaries and chunk digests come back to host memory); the chunk files are
+        then written from a read-only map of the input, as the reference writes its slices."""
+        import errno as _errno
+        import mmap
+
         os.makedirs(output_dir, exist_ok=True)
-        with open(input_file, "rb") as fh:
-            content = fh.read()
-        size = os.stat(input_file).st_size
-        host = torch.frombuffer(bytearray(content), dtype=torch.uint8) if content else torch.empty(0, dtype=torch.uint8)
-        dev = host.to(self.device)
-        offs, lens, digs = self.chunk_buffer(dev)
+        tab = fastcdc_files([input_file], self.min_chunk_size, self.avg_chunk_size, self.max_chunk_size, ctx=ctx)
+        if int(tab.status[0]) != _capi.OXH_OK:  # fs::read(input_file)? (:75): the io::Error
+            e = int(tab.os_error[0]) or _errno.EIO
+            raise OSError(e, os.strerror(e), input_file)
+        size = os.stat(input_file).st_size  # input_file.metadata()?.len() (:77-78)
         names = []
-        for o, l, (lo, hi) in zip(offs, lens, digs):
-            name = chunk_name(lo, hi)
-            names.append(name)
-            with open(os.path.join(output_dir, name), "wb") as out:
-                out.write(content[int(o):int(o) + int(l)])
+        with open(input_file, "rb") as fh:
+            content = mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_READ) if size else b""
+            try:
+                for o, l, (lo, hi) in zip(tab.offsets, tab.lens, tab.digests):
+                    name = chunk_name(lo, hi)
+                    names.append(name)
+                    with open(os.path.join(output_dir, name), "wb") as out:
+                        out.write(content[int(o):int(o) + int(l)])
+            finally:
+                if size:
+                    content.close()
         base = os.path.basename(os.path.normpath(input_file)) or "unknown_file"
         with open(os.path.join(output_dir, METADATA_FILE_NAME), "wb") as meta:
             meta.write(encode_metadata(base, size, names))

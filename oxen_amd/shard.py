@@ -1,6 +1,7 @@
 """Multi-GPU sharding of the hashing stage: one process per GPU, files split into contiguous
 byte-balanced ranges (no data-path collective), and ONE collective at the end -- an all-gather of
-the 16-B-per-file digest table (RCCL over xGMI with the "nccl" backend; gloo in CPU tests).
+the 16-B-per-file digest table: on GPUs the C ABI's oxh_gather_digests (RCCL over xGMI, comm.py),
+in CPU tests torch.distributed over gloo.
 """
 from __future__ import annotations
 
@@ -44,14 +45,22 @@ def gather_digest_table(local: torch.Tensor, counts: Sequence[int], group=None) 
 class PipelinedGather:
     """Double-buffered digest tables whose all-gather overlaps the next batch's hashing (bench.py's
     N > 1 step): fill(b) hands out local table b; gather(b) starts its all-gather asynchronously; a
-    table is handed out again only after the gather that read it has completed (work.wait(), which on
-    RCCL makes the current stream wait, on gloo blocks). Every rank must hold the same count n."""
+    table is handed out again only after the gather that read it has completed. Every rank must hold
+    the same count n.
 
-    def __init__(self, n: int, world: int, device, group=None, buffers: int = 2):
+    With `comm` (a comm.DigestComm) the gather is the C ABI's oxh_gather_digests (RCCL all-gather over
+    xGMI, what a Rust host links) on a side stream of its own, ordered against the hashing stream with
+    HIP events; without one it is torch.distributed's all_gather_into_tensor (the gloo rehearsal and
+    CPU tests)."""
+
+    def __init__(self, n: int, world: int, device, group=None, buffers: int = 2, comm=None):
         self.local = [torch.empty((n, 2), dtype=torch.int64, device=device) for _ in range(buffers)]
         self.full = [torch.empty((n * world, 2), dtype=torch.int64, device=device) for _ in range(buffers)]
         self.pending = [None] * buffers
         self.group = group
+        self.comm = comm
+        self.counts = [n] * world
+        self.side = torch.cuda.Stream(device) if comm is not None else None
         self.k = 0
 
     def next_local(self) -> tuple[int, torch.Tensor]:
@@ -59,17 +68,31 @@ class PipelinedGather:
         b = self.k % len(self.local)
         self.k += 1
         if self.pending[b] is not None:
-            self.pending[b].wait()
+            if self.comm is not None:  # the hashing stream waits for that gather's event
+                torch.cuda.current_stream(self.local[b].device).wait_event(self.pending[b])
+            else:
+                self.pending[b].wait()
             self.pending[b] = None
         return b, self.local[b]
 
     def gather(self, b: int) -> torch.Tensor:
         """Start the all-gather of local table b; returns the full table it will fill."""
-        self.pending[b] = dist.all_gather_into_tensor(self.full[b], self.local[b], group=self.group, async_op=True)
+        if self.comm is not None:
+            cur = torch.cuda.current_stream(self.local[b].device)
+            self.side.wait_stream(cur)  # the hash that filled table b comes first
+            self.comm.gather(self.local[b], self.counts, self.full[b], root=-1, stream=self.side)
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+            self.pending[b] = ev
+        else:
+            self.pending[b] = dist.all_gather_into_tensor(self.full[b], self.local[b], group=self.group, async_op=True)
         return self.full[b]
 
     def drain(self) -> None:
         for i, w in enumerate(self.pending):
             if w is not None:
-                w.wait()
+                if self.comm is not None:
+                    torch.cuda.current_stream(self.local[i].device).wait_event(w)
+                else:
+                    w.wait()
                 self.pending[i] = None

@@ -64,25 +64,26 @@ def _free_port():
 
 @pytest.mark.gpu
 def test_pipelined_gather_rccl_in_process(cuda, oracle_lib):
-    """The RCCL leg of C4 in the GPU suite: an in-process "nccl" group of world size 1, bench.py's
-    pipelined step (K1 into one of two digest tables while the previous table's all-gather runs on
-    RCCL's stream) for several steps; every gathered table equals the local K1 digests, which equal
-    the oracle on a sample."""
+    """The RCCL leg of C4 in the GPU suite, through the C ABI (oxh_comm_* / oxh_gather_digests, what
+    bench.py's N > 1 step and a Rust host call): a communicator of one rank, bench.py's pipelined step
+    (K1 into one of two digest tables while the previous table's all-gather runs on a side stream) for
+    several steps; every gathered table equals the local K1 digests, which equal the oracle on a sample.
+    Then the rooted gather (root 0) and the argument checks."""
     import torch
-    import torch.distributed as dist
 
+    from oxen_amd import _capi
+    from oxen_amd.comm import DigestComm
     from oxen_amd.device import DeviceArena, to_numpy_u64
     from oxen_amd.shard import PipelinedGather
 
-    dist.init_process_group("nccl", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{_free_port()}",
-                            device_id=cuda)
-    try:
+    with DigestComm(DigestComm.unique_id(), 0, 1, cuda.index or 0) as comm:
+        assert comm.info() == (0, 1, cuda.index or 0)
         rng = np.random.default_rng(11)
         lens = rng.integers(0, 300_000, 3000).astype(np.uint64)
         da = DeviceArena.splitmix(lens, seed=19, device=cuda)
         ref = torch.empty((len(lens), 2), dtype=torch.int64, device=cuda)
         da.hash(ref)
-        pipe = PipelinedGather(len(lens), 1, cuda)
+        pipe = PipelinedGather(len(lens), 1, cuda, comm=comm)
         fulls = []
         for _ in range(6):
             b, local = pipe.next_local()
@@ -98,5 +99,12 @@ def test_pipelined_gather_rccl_in_process(cuda, oracle_lib):
         idx = rng.choice(len(lens), 200, replace=False)
         got = oracle_lib.batch(host, da.offsets_host[idx], da.lens_host[idx])
         assert np.array_equal(got, want[idx])
-    finally:
-        dist.destroy_process_group()
+        # rooted (ncclGather) and empty tables
+        full = torch.zeros_like(ref)
+        comm.gather(ref, [len(lens)], full, root=0)
+        torch.cuda.synchronize()
+        assert torch.equal(full, ref)
+        comm.gather(ref[:0], [0], torch.empty((0, 2), dtype=torch.int64, device=cuda), root=-1)
+        with pytest.raises(_capi.OxenError) as e:
+            comm.gather(ref, [len(lens)], full, root=1)
+        assert e.value.code == _capi.OXH_ERR_INVALID

@@ -33,7 +33,7 @@ def test_built_for_gfx950(built_lib):
 
 def test_abi_version_and_format(built_lib):
     L = _capi.lib()
-    assert L.oxh_abi_version() == 3
+    assert L.oxh_abi_version() == 4
     buf = ctypes.create_string_buffer(40)
     # unpadded lowercase hex (merkle_hash.rs:73-77)
     n = L.oxh_format_hex(0x688558138047f8a, 0x2da4b9c5a75caad3 >> 4, buf)
@@ -85,3 +85,23 @@ def test_python_constants_match_the_header():
     assert not mismatched, mismatched
     modes = {k for k in defines if k.startswith("OXH_MODE_")}
     assert modes <= set(bound), modes - set(bound)
+
+
+def test_comm_argument_checks_without_device(built_lib):
+    """The digest-gather ABI (oxh_comm_*): argument errors are OXH_ERR_INVALID before any device or
+    RCCL work; without a GPU, creating a communicator fails with OXH_ERR_NODEVICE (no CPU fallback)."""
+    import torch
+
+    L = _capi.lib()
+    assert L.oxh_comm_unique_id(None) == _capi.OXH_ERR_INVALID
+    h = ctypes.c_void_p()
+    uid = b"\0" * _capi.OXH_COMM_ID_BYTES
+    assert L.oxh_comm_create(None, 0, 1, 0, ctypes.byref(h)) == _capi.OXH_ERR_INVALID
+    assert L.oxh_comm_create(uid, 1, 1, 0, ctypes.byref(h)) == _capi.OXH_ERR_INVALID
+    assert L.oxh_comm_create(uid, 0, 0, 0, ctypes.byref(h)) == _capi.OXH_ERR_INVALID
+    assert L.oxh_gather_digests(None, None, None, None, -1, None) == _capi.OXH_ERR_INVALID
+    assert L.oxh_comm_info(None, None, None, None) == _capi.OXH_ERR_INVALID
+    assert L.oxh_comm_destroy(None) == _capi.OXH_OK
+    if not torch.cuda.is_available():
+        assert L.oxh_comm_create(uid, 0, 1, 0, ctypes.byref(h)) == _capi.OXH_ERR_NODEVICE
+        assert not h.value

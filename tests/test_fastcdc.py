@@ -379,3 +379,106 @@ def test_fastcdc_walk_lists_beyond_lds_take_the_scan(cuda, oracle_lib, monkeypat
 
     with pytest.raises(_capi.OxenError, match="OXH_CDC_WALK=1: X's section lists do not fit"):
         fastcdc_device(torch.from_numpy(files[0]).to(cuda), [0], [len(files[0])], 4096, 8192, 16384)
+
+
+# ------------------------------------------------------------------------------ host-memory entry points
+def _check_table(oracle_lib, tab, datas, mn, av, mx, level=1):
+    """A FastCdcTable (dedup.fastcdc_files / fastcdc_host) against the oracle, file by file."""
+    assert len(tab.first) == len(datas) + 1 and int(tab.first[0]) == 0
+    for i, d in enumerate(datas):
+        off, ln, dig = tab.file(i)
+        want = F.chunks(d, mn, av, mx, level) if d is not None else np.zeros((0, 2), np.uint64)
+        assert len(off) == len(want), (i, len(off), len(want))
+        assert np.array_equal(off, want[:, 0]) and np.array_equal(ln, want[:, 1]), i
+        if d is not None and len(want):
+            assert np.array_equal(dig, oracle_lib.batch(d, want[:, 0], want[:, 1], threads=8)), i
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("piece_mib", [None, "32"], ids=["1GiB-pieces", "32MiB-pieces"])
+@pytest.mark.parametrize("cfg", [CONFIGS[0], CONFIGS[1], CONFIGS[3], CONFIGS[4]], ids=lambda c: "-".join(map(str, c)))
+def test_fastcdc_files_ragged(cuda, oracle_lib, tmp_path, monkeypatch, cfg, piece_mib):
+    """oxh_fastcdc_files (the reference's fs::read -> chunk -> xxh3 per chunk, fastcdchunker.rs:75-98,
+    starting and ending in host memory): empty, 1 B, < min, == min, odd tails, files that cross the
+    piece boundary and (with 32 MiB pieces) files cut into many segments whose carries must land on
+    the crate's boundaries. Every boundary and digest equals the oracle's."""
+    from oxen_amd import dedup
+
+    if piece_mib:
+        monkeypatch.setenv("OXH_CDC_PIECE_MIB", piece_mib)
+    mn, av, mx = cfg
+    rng = np.random.default_rng(sum(cfg) + (7 if piece_mib else 0))
+    sizes = [0, 1, mn - 1, mn, mn + 1, mx + 7, 262_145, 3_000_001, 70_000_003, 5_555, 41_000_000, 17]
+    datas, paths = [], []
+    for i, s in enumerate(sizes):
+        d = rng.integers(0, 256, s, dtype=np.uint8)
+        if i == 9:
+            d[:] = 0  # constant data: every position matches or none does
+        p = tmp_path / f"f{i}"
+        p.write_bytes(d.tobytes())
+        datas.append(d)
+        paths.append(str(p))
+    tab = dedup.fastcdc_files(paths, mn, av, mx)
+    assert list(tab.status) == [0] * len(sizes) and list(tab.sizes) == sizes
+    _check_table(oracle_lib, tab, datas, mn, av, mx)
+    # the same bytes from host buffers
+    _check_table(oracle_lib, dedup.fastcdc_host(datas, mn, av, mx), datas, mn, av, mx)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("avg", [8192, 65536])
+def test_fastcdc_files_2_5_gib_default_pieces(cuda, oracle_lib, tmp_path, avg):
+    """A 2.5 GiB file through the default 1 GiB pieces (two piece boundaries inside the file, each
+    chunked again from its carry), between two small files: the whole file checked, every boundary
+    and every digest, against the oracle."""
+    from oxen_amd import dedup
+    from oxen_amd.workloads import splitmix_bytes
+
+    big = splitmix_bytes(2525, 0, (5 << 29) + 12_345)
+    small = [np.frombuffer(b"hello world" * 1000, dtype=np.uint8), splitmix_bytes(7, 3, 9_999)]
+    datas = [small[0], big, small[1]]
+    paths = []
+    for i, d in enumerate(datas):
+        p = tmp_path / f"g{i}"
+        d.tofile(str(p))
+        paths.append(str(p))
+    tab = dedup.fastcdc_files(paths, 4096, avg, 2 * avg)
+    assert list(tab.status) == [0, 0, 0]
+    _check_table(oracle_lib, tab, datas, 4096, avg, 2 * avg)
+
+
+@pytest.mark.gpu
+def test_fastcdc_files_errors_are_per_file(cuda, oracle_lib, tmp_path):
+    """A missing path (File::open fails: OXH_ERR_OPEN, ENOENT), a directory (opens, read fails:
+    OXH_ERR_IO, EISDIR), a file used as a directory (ENOTDIR) have no chunks; the files around them are
+    chunked exactly. A table too small fails the call and names the count needed."""
+    import errno
+
+    from oxen_amd import _capi, dedup
+
+    rng = np.random.default_rng(3)
+    a = rng.integers(0, 256, 300_000, dtype=np.uint8)
+    b = rng.integers(0, 256, 50_000, dtype=np.uint8)
+    (tmp_path / "a").write_bytes(a.tobytes())
+    (tmp_path / "b").write_bytes(b.tobytes())
+    (tmp_path / "d").mkdir()
+    paths = [str(tmp_path / "a"), str(tmp_path / "missing"), str(tmp_path / "d"), str(tmp_path / "a" / "x"), str(tmp_path / "b")]
+    tab = dedup.fastcdc_files(paths, 4096, 8192, 16384)
+    assert list(tab.status) == [0, _capi.OXH_ERR_OPEN, _capi.OXH_ERR_IO, _capi.OXH_ERR_OPEN, 0]
+    assert list(tab.os_error) == [0, errno.ENOENT, errno.EISDIR, errno.ENOTDIR, 0]
+    _check_table(oracle_lib, tab, [a, None, None, None, b], 4096, 8192, 16384)
+    # capacity: the library counts on and reports what it needed
+    from oxen_amd.hasher import _PathTable, default_context
+
+    ctx = default_context()
+    t = _PathTable(paths)
+    off = np.zeros(2, dtype=np.uint64)
+    first = np.zeros(len(paths) + 1, dtype=np.uint64)
+    rc = _capi.lib().oxh_fastcdc_files(ctx.handle, t.arg, len(paths), 4096, 8192, 16384, 1, off.ctypes.data_as(_capi._u64p),
+                                       off.ctypes.data_as(_capi._u64p), None, 2, first.ctypes.data_as(_capi._u64p),
+                                       None, None, None)
+    assert rc == _capi.OXH_ERR_INVALID
+    assert f"need {len(tab.offsets)} entries" in _capi.lib().oxh_last_error().decode()
+    # the reference's pack() returns fs::read's io::Error
+    with pytest.raises(FileNotFoundError):
+        dedup.FastCDChunker(8192, 1).pack(str(tmp_path / "missing"), str(tmp_path / "out"))

@@ -16,6 +16,7 @@ INTEGRATION = os.path.join(ROOT, "INTEGRATION.md")
 C_BASE = {
     "int": "c_int", "int32_t": "i32", "uint32_t": "u32", "uint64_t": "u64", "uint8_t": "u8", "char": "c_char",
     "void": "c_void", "oxh_ctx": "OxhCtx", "oxh_pool": "OxhPool", "oxh_xxh3_stream": "OxhStream",
+    "oxh_comm": "OxhComm",
 }
 
 
