@@ -22,6 +22,7 @@ from __future__ import annotations
 import ctypes
 import hashlib
 import math
+import os
 
 import numpy as np
 
@@ -108,3 +109,38 @@ def chunks(data, min_size: int, avg: int, max_size: int, level: int = 1) -> np.n
                            _GEAR.ctypes.data_as(u64p), offs.ctypes.data_as(u64p), lens.ctypes.data_as(u64p), cap)
     assert n <= cap
     return np.stack([offs[:n], lens[:n]], axis=1)
+
+
+def files(paths, min_size: int, avg: int, max_size: int, level: int = 1, threads: int = 1, mmap_files: bool = False):
+    """C oracle over files (oxo_fastcdc_files): the reference's per-file read -> v2020 chunking ->
+    xxh3_128 per chunk, `threads` files at a time. Returns (counts (n,), fingerprints (n, 2), status (n,)),
+    a file's fingerprint being XXH3-128 of its (offset, length, lo, hi) u64 records (record_fingerprint)."""
+    global _GEAR
+    if _GEAR is None:
+        _GEAR = np.array(gear_table(), dtype=np.uint64)
+    L = _lib()
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    L.oxo_fastcdc_files.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                    ctypes.c_uint32, ctypes.c_uint32, u64p, ctypes.c_int, ctypes.c_int, u64p, u64p,
+                                    ctypes.POINTER(ctypes.c_int32)]
+    L.oxo_fastcdc_files.restype = None
+    n = len(paths)
+    arr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
+    counts = np.zeros(n, dtype=np.uint64)
+    fp = np.zeros((n, 2), dtype=np.uint64)
+    status = np.zeros(n, dtype=np.int32)
+    L.oxo_fastcdc_files(arr, n, min_size, avg, max_size, level, _GEAR.ctypes.data_as(u64p), 1 if mmap_files else 0,
+                        int(threads), counts.ctypes.data_as(u64p), fp.ctypes.data_as(u64p),
+                        status.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    return counts, fp, status
+
+
+def record_fingerprint(offsets, lens, digests) -> tuple[int, int]:
+    """XXH3-128 (lo, hi) of a chunk table's (offset, length, lo, hi) u64 LE records -- what
+    oxo_fastcdc_files reports per file -- for comparing a GPU table against the C oracle at full size."""
+    from . import oracle as _o
+
+    rec = np.empty((len(offsets), 4), dtype=np.uint64)
+    rec[:, 0], rec[:, 1] = offsets, lens
+    rec[:, 2:] = np.asarray(digests, dtype=np.uint64).reshape(-1, 2)
+    return _o.xxh3_128(rec.tobytes())

@@ -22,6 +22,7 @@
  * product's compiled-in copy. Parity against a reference run is UNPINNED: the reference's tests
  * hold no FastCDC fixtures and the crate cannot be built here (no cargo, no network).
  */
+#define _GNU_SOURCE
 #include <stdint.h>
 #include <string.h>
 
@@ -104,4 +105,108 @@ u64 oxo_fastcdc(const u8* src, u64 len, u32 min, u32 avg, u32 max, u32 level, co
         processed += cut;
     }
     return n;
+}
+
+/* ---- files: the reference's pack() loop minus the chunk-file writes, one thread per file ----
+ * fastcdchunker.rs:75-98 per file: fs::read(input_file) (mode 0: read() of the whole file into a
+ * malloc'd buffer, as fs::read does; mode 1: a read-only mmap, for sets whose whole-file buffers would
+ * not fit in host memory beside the page cache), v2020 chunking, xxh3_128 of every chunk. Files are
+ * taken by `nthreads` threads from a shared counter (the reference's pack is single-threaded per file;
+ * the files of a set are independent). Per file: the chunk count and fp = XXH3-128 of its records
+ * (offset, length, digest lo, digest hi as u64 LE per chunk) -- the GPU table is fingerprinted the
+ * same way by the caller -- and status 0 / 1 open / 2 read / 3 memory. */
+#include <fcntl.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+void oxo_xxh3_128(const void* data, uint64_t len, uint64_t out[2]);
+
+typedef struct {
+    const char* const* paths;
+    u64 n;
+    u32 min, avg, max, level;
+    const u64* gear;
+    int mode;
+    u64* counts;
+    u64* fp;
+    int32_t* status;
+    u64 next;  /* shared file counter (atomic) */
+} cdc_files_job;
+
+static int cdc_one_file(cdc_files_job* j, u64 i) {
+    const int fd = open(j->paths[i], O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return 1;
+    struct stat sb;
+    if (fstat(fd, &sb) != 0) { close(fd); return 2; }
+    const u64 sz = (u64)sb.st_size;
+    u8* buf = NULL;
+    int mapped = 0;
+    if (sz && j->mode == 1) {
+        void* m = mmap(NULL, sz, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (m == MAP_FAILED) { close(fd); return 3; }
+        buf = (u8*)m;
+        mapped = 1;
+    } else {
+        buf = (u8*)malloc(sz ? sz : 1);
+        if (!buf) { close(fd); return 3; }
+        u64 got = 0;
+        while (got < sz) {
+            const ssize_t r = read(fd, buf + got, sz - got);
+            if (r <= 0) { free(buf); close(fd); return 2; }
+            got += (u64)r;
+        }
+    }
+    close(fd);
+    u64 m[2];
+    oxo_fastcdc_masks(j->avg, j->level, m);
+    const u64 cap = sz / (j->min ? j->min : 1) + 2;
+    u64* rec = (u64*)malloc(cap * 4 * sizeof(u64));
+    if (!rec) { if (mapped) munmap(buf, sz); else free(buf); return 3; }
+    u64 processed = 0, k = 0;
+    while (processed < sz) {
+        const u64 cut = cut_gear(buf + processed, sz - processed, j->min, j->avg, j->max, m[0], m[1], j->gear);
+        if (cut == 0 || k >= cap) break;
+        u64 d[2];
+        oxo_xxh3_128(buf + processed, cut, d);
+        rec[4 * k] = processed;
+        rec[4 * k + 1] = cut;
+        rec[4 * k + 2] = d[0];
+        rec[4 * k + 3] = d[1];
+        ++k;
+        processed += cut;
+    }
+    j->counts[i] = k;
+    oxo_xxh3_128(rec, k * 4 * sizeof(u64), j->fp + 2 * i);
+    free(rec);
+    if (mapped) munmap(buf, sz); else free(buf);
+    return 0;
+}
+
+static void* cdc_files_worker(void* arg) {
+    cdc_files_job* j = (cdc_files_job*)arg;
+    for (;;) {
+        const u64 i = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
+        if (i >= j->n) break;
+        j->counts[i] = 0;
+        j->fp[2 * i] = j->fp[2 * i + 1] = 0;
+        j->status[i] = cdc_one_file(j, i);
+    }
+    return NULL;
+}
+
+void oxo_fastcdc_files(const char* const* paths, u64 n, u32 min, u32 avg, u32 max, u32 level, const u64* gear,
+                       int mode, int nthreads, u64* counts, u64* fp, int32_t* status) {
+    cdc_files_job j;
+    memset(&j, 0, sizeof j);
+    j.paths = paths, j.n = n, j.min = min, j.avg = avg, j.max = max, j.level = level, j.gear = gear, j.mode = mode;
+    j.counts = counts, j.fp = fp, j.status = status;
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    for (int t = 1; t < nthreads; ++t) pthread_create(&th[t], NULL, cdc_files_worker, &j);
+    cdc_files_worker(&j);
+    for (int t = 1; t < nthreads; ++t) pthread_join(th[t], NULL);
 }

@@ -482,3 +482,26 @@ def test_fastcdc_files_errors_are_per_file(cuda, oracle_lib, tmp_path):
     # the reference's pack() returns fs::read's io::Error
     with pytest.raises(FileNotFoundError):
         dedup.FastCDChunker(8192, 1).pack(str(tmp_path / "missing"), str(tmp_path / "out"))
+
+
+def test_oracle_files_driver_matches_buffers(oracle_lib, tmp_path):
+    """oxo_fastcdc_files (the CPU baseline of tools/bench_fastcdc_e2e.py: per file read or mmap -> v2020
+    -> xxh3_128 per chunk, files over threads) reports for every file the chunk count and the
+    fingerprint of exactly the table F.chunks + the per-chunk oracle give; errors per file."""
+    rng = np.random.default_rng(12)
+    datas, paths = [], []
+    for i, s in enumerate([0, 1, 4095, 4097, 300_001, 2_000_000]):
+        d = rng.integers(0, 256, s, dtype=np.uint8)
+        p = tmp_path / f"o{i}"
+        p.write_bytes(d.tobytes())
+        datas.append(d)
+        paths.append(str(p))
+    paths.append(str(tmp_path / "missing"))
+    for mm in (False, True):
+        counts, fp, st = F.files(paths, 4096, 8192, 16384, threads=3, mmap_files=mm)
+        assert list(st) == [0] * len(datas) + [1]
+        for i, d in enumerate(datas):
+            want = F.chunks(d, 4096, 8192, 16384)
+            dig = oracle_lib.batch(d, want[:, 0], want[:, 1]) if len(want) else np.zeros((0, 2), np.uint64)
+            assert int(counts[i]) == len(want)
+            assert (int(fp[i, 0]), int(fp[i, 1])) == F.record_fingerprint(want[:, 0], want[:, 1], dig)

@@ -1,0 +1,28 @@
+#!/bin/bash
+# r05 GPU steps: STEPS picks them (comma list). Each step has its own time limit; a test failure is
+# reported and the script goes on, a timeout / abort / signal stops it (nothing more on the GPU).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+T=${TAG:-r05a}
+step() {  # name, limit, command...
+  local name=$1 lim=$2
+  shift 2
+  case ",${STEPS:-all}," in *",$name,"*|*",all,"*) ;; *) return 0;; esac
+  echo "== $name $(date +%T)"
+  timeout -k 10 "$lim" "$@" > "gpurun_out/${T}_$name.out" 2> "gpurun_out/${T}_$name.err"
+  local rc=$?
+  tail -c 1500 "gpurun_out/${T}_$name.out"; echo
+  if [ $rc -ne 0 ]; then
+    echo "$name rc=$rc"; tail -20 "gpurun_out/${T}_$name.err"
+    if [ $rc -ge 124 ]; then exit $rc; fi
+  fi
+}
+step box 30 bash -c 'nproc; free -g; df -h /tmp /dev/shm .; cat /sys/fs/cgroup/memory.max /sys/fs/cgroup/cpu.max 2>/dev/null; ulimit -n'
+step newtests 900 python -u -m pytest tests/test_fastcdc.py tests/test_bench_launch.py tests/test_gpu_file_errors.py -m gpu -q --timeout 300 --timeout-method thread -k "files or host or lds or gather or reference_messages or status_and_errno"
+step pytest 1200 python -u -m pytest tests -m gpu -q --maxfail=20 --timeout 300 --timeout-method thread
+step bench 240 python bench.py --gpus 1 --steps 20 --warmup 5
+step bench_dist 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --dist --steps 20 --warmup 5 --no-cpu-baseline
+step c5e2e_small 600 python tools/bench_fastcdc_e2e.py --dir /tmp/oxh_c5s --files 16 --gib 1 --chunk 8192 --reps 3 --cold
+echo "== done $(date +%T)"
