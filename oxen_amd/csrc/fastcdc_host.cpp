@@ -51,8 +51,17 @@ int default_reader_threads();                               // ... OXH_NUM_THREA
 
 namespace {
 
-constexpr uint64_t kCdcBounce = 64ull << 20;  // one pinned bounce buffer
-constexpr int kCdcNBounce = 4;                // the ring: reads of the next windows run while earlier H2Ds drain
+constexpr uint64_t kCdcBounce = 64ull << 20;  // one pinned bounce buffer (a window of the piece)
+constexpr int kCdcMaxBounce = 16;
+// the ring: reads of the next windows run while earlier H2Ds drain (OXH_CDC_NBOUNCE, 2..16, default 4)
+int cdc_nbounce() {
+    static const int v = [] {
+        const char* e = getenv("OXH_CDC_NBOUNCE");
+        const int k = e ? atoi(e) : 4;
+        return std::max(2, std::min(k, kCdcMaxBounce));
+    }();
+    return v;
+}
 constexpr uint64_t kCdcPart = 4ull << 20;     // one reader task
 constexpr uint64_t kCdcAlign = 256;           // segment placement in a piece
 constexpr uint64_t kProbeWindow = 256;        // files opened (and stat'ed) ahead of the planner
@@ -68,9 +77,10 @@ struct CdcHost {
     uint64_t piece = 0;
     uint8_t* d_piece[2] = {};
     hipEvent_t ev_copied[2] = {};
-    uint8_t* h_bounce[kCdcNBounce] = {};
-    hipEvent_t ev_bounce[kCdcNBounce] = {};
-    bool bounce_used[kCdcNBounce] = {};
+    int nbounce = 0;
+    uint8_t* h_bounce[kCdcMaxBounce] = {};
+    hipEvent_t ev_bounce[kCdcMaxBounce] = {};
+    bool bounce_used[kCdcMaxBounce] = {};
     uint64_t tab_cap = 0;  // entries of the chunk-table buffers below
     uint64_t *d_off = nullptr, *d_len = nullptr, *d_dig = nullptr;
     uint64_t *h_off = nullptr, *h_len = nullptr, *h_dig = nullptr;
@@ -84,7 +94,7 @@ struct CdcHost {
             if (p) (void)hipFree(p);
         for (auto e : ev_copied)
             if (e) (void)hipEventDestroy(e);
-        for (int i = 0; i < kCdcNBounce; ++i) {
+        for (int i = 0; i < kCdcMaxBounce; ++i) {
             if (h_bounce[i]) (void)hipHostFree(h_bounce[i]);
             if (ev_bounce[i]) (void)hipEventDestroy(ev_bounce[i]);
         }
@@ -127,7 +137,7 @@ void free_cdc_host(void* p) { delete static_cast<CdcHost*>(p); }
 int cdc_host(oxh_ctx* ctx, uint64_t piece, CdcHost** out) {
     void*& slot = oxh::ctx_cdc_state(ctx, free_cdc_host);
     CdcHost* h = static_cast<CdcHost*>(slot);
-    if (h && h->piece == piece) {
+    if (h && h->piece == piece && h->nbounce == cdc_nbounce()) {
         *out = h;
         return OXH_OK;
     }
@@ -148,7 +158,8 @@ int cdc_host(oxh_ctx* ctx, uint64_t piece, CdcHost** out) {
         if (hipMalloc(&h->d_piece[b], piece + 4096) != hipSuccess) return bad(OXH_ERR_NOMEM, "device piece buffers");
         if (hipEventCreateWithFlags(&h->ev_copied[b], hipEventDisableTiming) != hipSuccess) return bad(OXH_ERR_HIP, "events");
     }
-    for (int i = 0; i < kCdcNBounce; ++i) {
+    h->nbounce = cdc_nbounce();
+    for (int i = 0; i < h->nbounce; ++i) {
         if (hipHostMalloc(&h->h_bounce[i], kCdcBounce, hipHostMallocDefault) != hipSuccess)
             return bad(OXH_ERR_NOMEM, "pinned bounce buffers");
         if (hipEventCreateWithFlags(&h->ev_bounce[i], hipEventDisableTiming) != hipSuccess) return bad(OXH_ERR_HIP, "events");
@@ -271,7 +282,7 @@ struct Call {
     std::deque<Round> ready;   // rounds whose bytes are on the device, for the chunking thread
     bool planner_done = false;
     bool buf_busy[2] = {false, false};
-    double t_read = 0, t_chunk = 0, t_wait = 0;
+    double t_read = 0, t_chunk = 0, t_wait = 0, t_read_wait = 0, t_h2d_wait = 0;
 
     void fail(int code, const std::string& m) {
         int z = OXH_OK;
@@ -417,7 +428,9 @@ int upload_round(Call& C, const Round& R) {
     std::deque<Window*> inflight;
     uint64_t next_bb = 0;
     auto finish = [&](Window& W) -> int {
+        const double tw = now();
         W.grp.wait();
+        C.t_read_wait += now() - tw;
         if (W.used == 0) return OXH_OK;
         if (hipMemcpyAsync(h.d_piece[R.b] + W.base, h.h_bounce[W.bb], W.used, hipMemcpyHostToDevice, h.copy) != hipSuccess ||
             hipEventRecord(h.ev_bounce[W.bb], h.copy) != hipSuccess)
@@ -429,11 +442,13 @@ int upload_round(Call& C, const Round& R) {
     for (auto& wp : wins) {
         Window& W = *wp;
         if (W.parts.empty()) continue;
-        W.bb = (int)(next_bb++ % kCdcNBounce);
+        W.bb = (int)(next_bb++ % (uint64_t)h.nbounce);
+        const double tw = now();
         if (h.bounce_used[W.bb] && hipEventSynchronize(h.ev_bounce[W.bb]) != hipSuccess) {
             rc = oxh::set_error(OXH_ERR_HIP, "bounce buffer wait");
             break;
         }
+        C.t_h2d_wait += now() - tw;
         h.bounce_used[W.bb] = false;
         uint8_t* dst = h.h_bounce[W.bb];
         W.fn = [&C, &W, dst](int t) {
@@ -448,7 +463,7 @@ int upload_round(Call& C, const Round& R) {
         };
         h.pool->start((int)W.parts.size(), W.fn, W.grp);
         inflight.push_back(&W);
-        if ((int)inflight.size() >= kCdcNBounce - 1) {
+        if ((int)inflight.size() >= h.nbounce - 1) {
             rc = finish(*inflight.front());
             inflight.pop_front();
             if (rc) break;
@@ -590,8 +605,10 @@ int run(oxh_ctx* ctx, CdcSource& src, uint64_t n, uint32_t mn, uint32_t av, uint
     }
     if (trace)
         fprintf(stderr, "[oxh] fastcdc_host: %llu items, %d rounds of %llu MiB, %llu chunks: total %.1f ms, reads+H2D %.1f, "
-                "chunking+D2H+stitch %.1f, waits %.1f\n", (unsigned long long)n, round_no, (unsigned long long)(piece >> 20),
-                (unsigned long long)C.total, 1e3 * (now() - t_start), 1e3 * C.t_read, 1e3 * C.t_chunk, 1e3 * C.t_wait);
+                "chunking+D2H+stitch %.1f, waits %.1f (of them: reads %.1f, bounce H2D %.1f), %d bounce x %llu MiB, %d readers\n",
+                (unsigned long long)n, round_no, (unsigned long long)(piece >> 20), (unsigned long long)C.total,
+                1e3 * (now() - t_start), 1e3 * C.t_read, 1e3 * C.t_chunk, 1e3 * C.t_wait, 1e3 * C.t_read_wait,
+                1e3 * C.t_h2d_wait, h->nbounce, (unsigned long long)(kCdcBounce >> 20), h->pool->size());
     if (C.total > capacity)
         return oxh::set_error(OXH_ERR_INVALID, "chunk capacity too small: need " + std::to_string(C.total) + " entries");
     return OXH_OK;

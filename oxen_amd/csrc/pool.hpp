@@ -8,6 +8,7 @@
 
 #include <atomic>
 #include <condition_variable>
+#include <deque>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -127,8 +128,8 @@ class Pool {
                 std::unique_lock<std::mutex> lk(mu_);
                 cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
                 if (stop_ && q_.empty()) return;
-                job = std::move(q_.back());
-                q_.pop_back();
+                job = std::move(q_.front());  // first in, first out: a caller waiting on its oldest
+                q_.pop_front();               // group (the bounce windows) gets it done first
                 ++busy_;
             }
             job();
@@ -140,7 +141,7 @@ class Pool {
         }
     }
     std::vector<std::thread> th_;
-    std::vector<std::function<void()>> q_;
+    std::deque<std::function<void()>> q_;
     std::mutex mu_;
     std::condition_variable cv_, idle_cv_;
     int busy_ = 0;

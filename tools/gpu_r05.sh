@@ -25,4 +25,11 @@ step pytest 1200 python -u -m pytest tests -m gpu -q --maxfail=20 --timeout 300 
 step bench 240 python bench.py --gpus 1 --steps 20 --warmup 5
 step bench_dist 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --dist --steps 20 --warmup 5 --no-cpu-baseline
 step c5e2e_small 600 python tools/bench_fastcdc_e2e.py --dir /tmp/oxh_c5s --files 16 --gib 1 --chunk 8192 --reps 3 --cold
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step e2e_nb4 600 env OXH_TRACE=1 OXH_CDC_NBOUNCE=4 python tools/bench_fastcdc_e2e.py --dir /tmp/oxh_c5s --files 16 --gib 1 --chunk 8192 --reps 3 --keep
+step e2e_nb8 600 env OXH_TRACE=1 OXH_CDC_NBOUNCE=8 python tools/bench_fastcdc_e2e.py --dir /tmp/oxh_c5s --files 16 --gib 1 --chunk 8192 --reps 3
+step e2e_shm_8k 900 env OXH_TRACE=1 OXH_CDC_NBOUNCE=${NB:-8} python tools/bench_fastcdc_e2e.py --dir /dev/shm/oxh_c5 --files 16 --gib 8 --chunk 8192 --reps 3 --keep
+step e2e_shm_64k 900 env OXH_TRACE=1 OXH_CDC_NBOUNCE=${NB:-8} python tools/bench_fastcdc_e2e.py --dir /dev/shm/oxh_c5 --files 16 --gib 8 --chunk 65536 --reps 3
+step e2e_disk_8k 900 env OXH_TRACE=1 OXH_CDC_NBOUNCE=${NB:-8} python tools/bench_fastcdc_e2e.py --dir /tmp/oxh_c5d --files 8 --gib 8 --chunk 8192 --reps 2 --cold
+rm -rf /dev/shm/oxh_c5 /tmp/oxh_c5s /tmp/oxh_c5d
 echo "== done $(date +%T)"
