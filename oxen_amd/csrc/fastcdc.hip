@@ -46,12 +46,15 @@
 #include "../../include/oxen_hash.h"
 #include "fastcdc_gear.h"
 #include "scratch.hpp"
+#include "xxh3_device.hpp"
 
 namespace oxh {
 
 int set_error(int code, const std::string& msg);  // oxen_hash_capi.hip: oxh_last_error() text
 int k1_packed(const void* d_arena, const uint64_t* d_offsets, const uint64_t* d_lens, uint64_t n, uint64_t* d_out,
               uint64_t mean_len, hipStream_t st);  // oxen_hash_capi.hip
+__global__ void xxh3_rows_fold_kernel(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t*,
+                                      const uint64_t*, const uint8_t*);  // xxh3_kernels.hip (K1F)
 
 // fastcdc::v2020::MASKS, indexed by the number of one bits (entries 0..4 are padding)
 static constexpr uint64_t kCdcMasks[26] = {
@@ -762,8 +765,11 @@ __global__ __launch_bounds__(1024) void cdc_prefix_kernel(CdcStitch s, uint64_t 
 }
 
 // F3d: the chunk table. One lane per chunk start, grouped by section (a wave per section).
+// c_flag (W2's fold, may be NULL): 1 for a chunk of a section whose list is W's own (its block sums in
+// geo.sums are the chunk's), 0 for the sections X re-walked.
 __global__ __launch_bounds__(256) void cdc_emit_kernel(CdcFiles f, CdcParams prm, CdcStitch s, uint64_t n_sec,
-                                                       uint64_t* __restrict__ c_off, uint64_t* __restrict__ c_len) {
+                                                       uint64_t* __restrict__ c_off, uint64_t* __restrict__ c_len,
+                                                       uint8_t* __restrict__ c_flag) {
     const uint64_t sec = (uint64_t)blockIdx.x * 4 + (uint64_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (sec >= n_sec) return;
     const int lane = threadIdx.x & 63;
@@ -774,11 +780,13 @@ __global__ __launch_bounds__(256) void cdc_emit_kernel(CdcFiles f, CdcParams prm
     const uint32_t* src = s.status[sec] == kFixed ? s.fix + sec * prm.speccap : f.spec + sec * prm.speccap + s.k0[sec];
     const uint64_t base = s.out_base[sec];
     const uint64_t ex = s.exit[sec];
+    const uint8_t own = s.status[sec] == kFixed ? 0 : 1;
     for (uint32_t k = lane; k < cnt; k += 64) {
         const uint64_t a = sec_start + src[k];
         const uint64_t b = k + 1 < cnt ? sec_start + src[k + 1] : ex;
         c_off[base + k] = foff + a;
         c_len[base + k] = b - a;
+        if (c_flag) c_flag[base + k] = own;
     }
 }
 
@@ -839,6 +847,7 @@ constexpr uint32_t kNoCut = 0xFFFFFFFFu;
 
 struct WalkGeom {
     uint64_t arena_bytes;  // the arena holds file bytes up to here (the DMA range stops at it, 16-B rounded)
+    uint64_t* sums;        // FOLD: XXH3 block sums, 8 u64 per 1 KiB of arena (block at arena offset A -> A >> 10)
 };
 
 // The chunk that starts at m-space position cs: its test window [lo, tL), the mask switch tS and the
@@ -887,7 +896,22 @@ __device__ __forceinline__ void walk_begin_chunk(WalkLane& L, const CdcParams& p
 // LATE: the next round's DMA goes out after this round is rolled, when each lane's next line is known
 // (no stale round after a cut, but the DMA's latency is left to the other waves of the SIMD to hide);
 // otherwise it goes out before the roll, for the line after the current one.
-template <int WAVES, bool LATE>
+//
+// FOLD (W2, min = 4 KiB, DESIGN §4 "W2"): the walk also folds XXH3's stripe accumulation into the bytes
+// it streams. XXH3-128's long path sums 64-B stripes into 8 accumulators per 1 KiB block and scrambles
+// them between blocks; a block's sum (acc[i] += lo32(w ^ key) * hi32(w ^ key), acc[i ^ 1] += w over its
+// 128 words) does not depend on the accumulators, so W can produce the sums of a chunk's blocks 4..
+// (the bytes after its `min` = 4 blocks, the only ones W reads) and a second pass (K1F) adds blocks 0-3,
+// the partial last block and the last stripe from the bytes and runs each chunk's chain over the stored
+// sums. For that, a lane's lines are chunk-relative: line k of a chunk starting at cs is fetched from
+// (cs + min + 128 k) & ~3 (dword aligned; W proper fetches 128-B aligned lines), so every 8 lines are one
+// block, word q of a line is bytes [cs + min + 128 k + 8 q, + 8) at line byte (cs & 3) + 8 q, realigned
+// with v_alignbyte, and its key is secret word 2 (k % 8) + (q >> 3) + (q & 7) (taken from the lanes that
+// hold the secret, by ds_bpermute: W's LDS is full). Word 15 needs the next line's first dword, so it is
+// folded at the start of the next round. A block's sum goes to geo.sums once its last word is folded;
+// blocks of chunks that start before the lane's section (warm-up) are not stored, and K1F uses a chunk's
+// sums only where the stitch kept W's list (X marks fixed sections).
+template <int WAVES, bool LATE, bool FOLD = false>
 __global__ __launch_bounds__(64 * WAVES) void cdc_walk_scan_kernel(CdcFiles f, CdcParams prm, uint64_t n_sec, WalkGeom geo) {
     __shared__ __attribute__((aligned(16))) uint64_t lds[256 * 32 + WAVES * 1024];
     for (int i = threadIdx.x; i < 256 * 32; i += blockDim.x) lds[i] = kGear[i >> 5] << 16;
@@ -936,7 +960,8 @@ __global__ __launch_bounds__(64 * WAVES) void cdc_walk_scan_kernel(CdcFiles f, C
     uint32_t* __restrict__ out = f.spec + secq * prm.speccap;
     if (live) walk_begin_chunk(L, prm, out);
     const uint32_t a0 = (uint32_t)(prm.min & ~1ull);
-    uint32_t NL = L.done ? kWalkOob : ((L.cs + a0) & ~127u);  // next line to fetch
+    constexpr uint32_t kLineMask = FOLD ? ~3u : ~127u;  // FOLD: chunk-relative, dword-aligned lines
+    uint32_t NL = L.done ? kWalkOob : ((L.cs + a0) & kLineMask);  // next line to fetch
     const uint64_t ms64 = prm.mask_s << 16, ml64 = prm.mask_l << 16;
     const uint32_t ms = (uint32_t)(ms64 >> 32), ml = (uint32_t)(ml64 >> 32), mc = ms & ml;  // host: all bits >= 16
     const uint32_t copy_off = (uint32_t)(lane & 31) * 8;
@@ -945,20 +970,16 @@ __global__ __launch_bounds__(64 * WAVES) void cdc_walk_scan_kernel(CdcFiles f, C
         const uint32_t a = __builtin_amdgcn_perm(word, copy_off, 0x0c0c0000u | ((4u + (uint32_t)j) << 8));
         return *(const uint64_t*)(tab + a);
     };
-    // DMA k, lane 8m + j: piece (j - rot(r)) & 7 of the line of lane r = 8k + m
+    // DMA k, lane 8m + j: piece (j - rot(r)) & 7 of the line of lane r = 8k + m; rot(r) = (r >> 1) & 7 =
+    // (4 (k & 1) + (m >> 1)) & 7, so the offset takes two values (odd and even k)
     const int dm = lane >> 3, dj = lane & 7;
-    uint32_t poff[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const uint32_t r = 8 * k + dm;
-        poff[k] = 16 * ((uint32_t)(dj - (int)((r >> 1) & 7)) & 7);
-    }
+    const uint32_t poff0 = 16 * ((uint32_t)(dj - (dm >> 1)) & 7), poff1 = 16 * ((uint32_t)(dj - ((4 + (dm >> 1)) & 7)) & 7);
     auto dma = [&](uint32_t line) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const uint32_t src = (uint32_t)__builtin_amdgcn_ds_bpermute((8 * k + dm) * 4, (int)line);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)(slot + 64 * k), 16,
-                                                     src + poff[k], 0, 0, kScanDmaAux);
+                                                     src + ((k & 1) ? poff1 : poff0), 0, 0, kScanDmaAux);
         }
     };
     uint32_t RL = NL;  // the line the DMA in flight fetches for this lane
@@ -967,19 +988,91 @@ __global__ __launch_bounds__(64 * WAVES) void cdc_walk_scan_kernel(CdcFiles f, C
     dma(RL);
     const int rot = (lane >> 1) & 7;
     uint64_t h = 0;
+    // FOLD state: the chunk's block accumulators, its line count, byte shift, the previous line's last
+    // two dwords and its word 15's key (that word is folded next round), whether the chunk's first valid
+    // round is still to come (xfresh: the accumulators restart there), and the secret word this lane
+    // holds for the others' ds_bpermute. The fold itself runs on every round with the whole wave active
+    // (ds_bpermute reads nothing from inactive lanes): what a stale round (the one in flight at a cut)
+    // adds is wiped when the next chunk's first valid round restarts the accumulators.
+    uint64_t xa[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t xk = 0, xbs = 0, lag0 = 0, lag1 = 0, klag_lo = 0, klag_hi = 0;
+    bool xlag = false, xfresh = true;
+    const uint64_t sec_w = kSecW[lane < 24 ? lane : 0];
+    const uint32_t sec_lo = (uint32_t)sec_w, sec_hi = (uint32_t)(sec_w >> 32);
+    const uint64_t mbase = base - (uint64_t)f.arena;  // arena offset of m-space 0
+    auto fold_word = [&](uint32_t lo, uint32_t hi, uint32_t klo, uint32_t khi, int i) {
+        xa[i] += (uint64_t)(lo ^ klo) * (uint64_t)(hi ^ khi);
+        xa[i ^ 1] += ((uint64_t)hi << 32) | lo;
+    };
+    // the sum of the chunk's block 4 + (xk - 1) / 8 is complete: store it (recorded chunks only), restart
+    auto fold_store = [&]() {
+        if (L.cs >= L.mS) {
+            const uint64_t blk = (mbase + (uint64_t)L.cs + (uint64_t)a0 + 1024ull * ((xk - 1) >> 3)) >> 10;
+            uint4* dst = reinterpret_cast<uint4*>(geo.sums + 8 * blk);
+            dst[0] = make_uint4((uint32_t)xa[0], (uint32_t)(xa[0] >> 32), (uint32_t)xa[1], (uint32_t)(xa[1] >> 32));
+            dst[1] = make_uint4((uint32_t)xa[2], (uint32_t)(xa[2] >> 32), (uint32_t)xa[3], (uint32_t)(xa[3] >> 32));
+            dst[2] = make_uint4((uint32_t)xa[4], (uint32_t)(xa[4] >> 32), (uint32_t)xa[5], (uint32_t)(xa[5] >> 32));
+            dst[3] = make_uint4((uint32_t)xa[6], (uint32_t)(xa[6] >> 32), (uint32_t)xa[7], (uint32_t)(xa[7] >> 32));
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) xa[i] = 0;
+    };
+    auto fold_reset = [&]() { xk = 0, xlag = false, xfresh = true, xbs = L.cs & 3u; };
+    if constexpr (FOLD) fold_reset();
 #pragma unroll 1
     for (;;) {
         if (__builtin_amdgcn_ballot_w64(!L.done) == 0) break;
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this round's DMA has landed
         uint32_t wv[32];
+        // (FOLD: the 8 slot addresses are recomputed every round rather than held in registers)
+        int rr = rot;
+        if constexpr (FOLD) asm volatile("" : "+v"(rr));
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-            const uint4 v = slot[lane * 8 + ((q + rot) & 7)];
+            const uint4 v = slot[lane * 8 + ((q + rr) & 7)];
             wv[4 * q] = v.x, wv[4 * q + 1] = v.y, wv[4 * q + 2] = v.z, wv[4 * q + 3] = v.w;
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the slot is free for the next DMA
         const uint32_t CL = RL;
         const bool CV = RV && !L.done;
+        if constexpr (FOLD) {
+            // a valid round (CV; not the stale one after a cut) is line xk of the chunk at L.cs: keys
+            // 2 (xk % 8) + 0..8 (words q < 8 take key q, words q >= 8 key q - 7), whole wave active
+            const uint32_t kb = (xk & 7u) * 8u;  // bpermute byte address of key 2 (xk % 8)
+            auto key = [&](int j, uint32_t& lo, uint32_t& hi) {
+                lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(kb + 4u * (uint32_t)j), (int)sec_lo);
+                hi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(kb + 4u * (uint32_t)j), (int)sec_hi);
+            };
+            // word 15 of the previous line; its block may then be complete
+            fold_word(__builtin_amdgcn_alignbyte(lag1, lag0, xbs), __builtin_amdgcn_alignbyte(wv[0], lag1, xbs), klag_lo,
+                      klag_hi, 7);
+            if (CV && xlag && ((xk - 1) & 7u) == 7u) fold_store();
+            if (CV && xfresh) {  // the chunk's first valid round: the accumulators start here
+#pragma unroll
+                for (int i = 0; i < 8; ++i) xa[i] = 0;
+                xfresh = false;
+            }
+            // key j serves word j (j < 8) and word j + 7 (1 <= j <= 7); key 8 is word 15's, next round.
+            // One key in flight ahead of its use keeps the registers down (W2 sits at 3 waves per SIMD).
+            auto word = [&](int q, uint32_t klo, uint32_t khi) {
+                fold_word(__builtin_amdgcn_alignbyte(wv[2 * q + 1], wv[2 * q], xbs),
+                          __builtin_amdgcn_alignbyte(wv[2 * q + 2], wv[2 * q + 1], xbs), klo, khi, q & 7);
+            };
+            uint32_t kl, kh, nkl, nkh;
+            key(0, kl, kh);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                key(j + 1, nkl, nkh);
+                word(j, kl, kh);
+                if (j >= 1) word(j + 7, kl, kh);
+                kl = nkl, kh = nkh;
+            }
+            if (CV) {
+                lag0 = wv[30], lag1 = wv[31], klag_lo = kl, klag_hi = kh;
+                xlag = true;
+                ++xk;
+            }
+        }
         if constexpr (!LATE) {
             RL = L.done ? kWalkOob : NL;
             RV = !L.done;
@@ -993,7 +1086,7 @@ __global__ __launch_bounds__(64 * WAVES) void cdc_walk_scan_kernel(CdcFiles f, C
         else if (CL >= L.tS) m = ml;
         else m = mc;
         bool cut_now = false;
-        constexpr int P = 3;
+        constexpr int P = FOLD ? 2 : 3;
         uint64_t G[P + 1][4];
 #pragma unroll
         for (int i = 0; i < P; ++i)
@@ -1021,9 +1114,9 @@ __global__ __launch_bounds__(64 * WAVES) void cdc_walk_scan_kernel(CdcFiles f, C
                     if (anyz == 0) {
                         // the group's zero tests, in position order; the first valid one is the cut
                         const uint32_t g = CL + 16 * (uint32_t)(i >> 2);
-                        uint32_t bits = 0;
+                        uint32_t bits = 0;  // (built high position first: no shifted-constant registers)
 #pragma unroll
-                        for (int j = 0; j < 16; ++j) bits |= ((hh[j] & m) == 0 ? 1u : 0u) << j;
+                        for (int j = 15; j >= 0; --j) bits = (bits << 1) | ((hh[j] & m) == 0 ? 1u : 0u);
                         while (bits) {
                             const int j = __builtin_ctz(bits);
                             bits &= bits - 1;
@@ -1038,7 +1131,8 @@ __global__ __launch_bounds__(64 * WAVES) void cdc_walk_scan_kernel(CdcFiles f, C
                             // a cut: the next chunk starts at p (cut_gear returns the matching index)
                             L.cs = p;
                             walk_begin_chunk(L, prm, out);
-                            if (!L.done) NL = (L.cs + a0) & ~127u;
+                            if constexpr (FOLD) fold_reset();
+                            if (!L.done) NL = (L.cs + a0) & kLineMask;
                             RV = false;  // the line in flight belonged to the old chunk
                             m = kWalkFull;
                             cut_now = true;
@@ -1052,9 +1146,19 @@ __global__ __launch_bounds__(64 * WAVES) void cdc_walk_scan_kernel(CdcFiles f, C
         }
         // no cut before the end of the test window: the chunk ends at cs + rem (max, or the file end)
         if (CV && !cut_now && CL + 128 >= L.tL) {
+            if constexpr (FOLD) {
+                // the walk reads no further line of this chunk: a block that ended with the line just
+                // folded (a chunk of 1024 m + 1 bytes at a dword-aligned start) still lacks its word 15,
+                // which then lies wholly in this line (shift 0)
+                if (xlag && xbs == 0 && ((xk - 1) & 7u) == 7u) {
+                    fold_word(lag0, lag1, (uint32_t)S64(176), (uint32_t)(S64(176) >> 32), 7);  // key word 22
+                    fold_store();
+                }
+            }
             L.cs = L.cutm;
             walk_begin_chunk(L, prm, out);
-            if (!L.done) NL = (L.cs + a0) & ~127u;
+            if constexpr (FOLD) fold_reset();
+            if (!L.done) NL = (L.cs + a0) & kLineMask;
             RV = false;
         }
         if constexpr (LATE) {
@@ -1574,6 +1678,16 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     sc.want(&d_exit, n_sec);
     sc.want(&d_fix, n_sec * prm.speccap);
     sc.want(&d_out_base, n_sec + 1);
+    // W2 (the walk with K1's block sums folded in) + K1F: OXH_CDC_FOLD=1, on the walk path with digests
+    // asked for and `min` a whole number of 1 KiB blocks (C5: min 4 KiB). Sums: 64 B per KiB of arena.
+    const bool fold_env = getenv("OXH_CDC_FOLD") && atoi(getenv("OXH_CDC_FOLD")) != 0;
+    const bool fold = fold_env && walk && d_digests && capacity && min_size % 1024 == 0;
+    uint64_t* d_sums = nullptr;
+    uint8_t* d_flag = nullptr;
+    if (fold) {
+        sc.want(&d_sums, ((arena_bytes >> 10) + 4) * 8);
+        sc.want(&d_flag, capacity);
+    }
     CDC_HIP(sc.commit());
     const double t_malloc = since();
     CDC_HIP(hipMemcpyAsync(d_foff, offsets, n * 8, hipMemcpyHostToDevice, st));
@@ -1593,10 +1707,11 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
         // wrong); the serial pass for whatever is left; then the chunk counts' prefix
         const uint64_t nwaves = (n_sec + 63) / 64;
         static const bool late = getenv("OXH_CDC_WALK_LATE") && atoi(getenv("OXH_CDC_WALK_LATE")) != 0;
-        auto walk_kernel = late ? oxh::cdc_walk_scan_kernel<oxh::kScanWaves, true> : oxh::cdc_walk_scan_kernel<oxh::kScanWaves, false>;
+        auto walk_kernel = fold ? oxh::cdc_walk_scan_kernel<oxh::kScanWaves, false, true>
+                           : late ? oxh::cdc_walk_scan_kernel<oxh::kScanWaves, true> : oxh::cdc_walk_scan_kernel<oxh::kScanWaves, false>;
         hipLaunchKernelGGL(walk_kernel,
                            dim3((unsigned)((nwaves + oxh::kScanWaves - 1) / oxh::kScanWaves)), dim3(64 * oxh::kScanWaves), 0, st,
-                           f, prm, n_sec, oxh::WalkGeom{arena_bytes});
+                           f, prm, n_sec, oxh::WalkGeom{arena_bytes, d_sums});
         CDC_HIP(hipGetLastError());
         const size_t xlds = 2 * (size_t)prm.speccap * sizeof(uint32_t);
         static const unsigned xgrid = getenv("OXH_CDC_X_WGS") ? (unsigned)atoi(getenv("OXH_CDC_X_WGS")) : 16384u;
@@ -1648,7 +1763,7 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     if (total && (!d_chunk_offsets || !d_chunk_lens)) return cdc_fail(OXH_ERR_INVALID, "null chunk table");
     if (n_sec) {
         hipLaunchKernelGGL(oxh::cdc_emit_kernel, dim3((unsigned)((n_sec + 3) / 4)), dim3(256), 0, st, f, prm, sti, n_sec,
-                           d_chunk_offsets, d_chunk_lens);
+                           d_chunk_offsets, d_chunk_lens, fold ? d_flag : nullptr);
         CDC_HIP(hipGetLastError());
     }
     if (d_digests && total) {
@@ -1656,7 +1771,14 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
         // otherwise (oxh::k1_packed)
         uint64_t bytes = 0;
         for (uint64_t i = 0; i < n; ++i) bytes += lens[i];
-        rc = oxh::k1_packed(d_arena, d_chunk_offsets, d_chunk_lens, total, d_digests, bytes / total, st);
+        if (fold) {  // K1F: blocks 0-3 and the tail from the bytes, blocks 4.. from W2's sums
+            hipLaunchKernelGGL(oxh::xxh3_rows_fold_kernel, dim3((unsigned)((total + 7) / 8)), dim3(128), 0, st,
+                               (const uint8_t*)d_arena, d_chunk_offsets, d_chunk_lens, total, d_digests, d_sums, d_flag);
+            rc = hipGetLastError() == hipSuccess ? OXH_OK : OXH_ERR_HIP;
+            if (rc) oxh::set_error(rc, "K1F launch");
+        } else {
+            rc = oxh::k1_packed(d_arena, d_chunk_offsets, d_chunk_lens, total, d_digests, bytes / total, st);
+        }
         if (rc) return cdc_fail(rc, std::string("chunk digests: ") + oxh_last_error());
     }
     CDC_HIP(hipStreamSynchronize(st));

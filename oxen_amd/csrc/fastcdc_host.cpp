@@ -53,11 +53,12 @@ namespace {
 
 constexpr uint64_t kCdcBounce = 64ull << 20;  // one pinned bounce buffer (a window of the piece)
 constexpr int kCdcMaxBounce = 16;
-// the ring: reads of the next windows run while earlier H2Ds drain (OXH_CDC_NBOUNCE, 2..16, default 4)
+// the ring: reads of the next windows run while earlier H2Ds drain (OXH_CDC_NBOUNCE, 2..16, default 8:
+// 47.7 vs 43.6 GiB/s for 4 on 16 x 1 GiB from the page cache, profiles/r05/r05a_e2e_*)
 int cdc_nbounce() {
     static const int v = [] {
         const char* e = getenv("OXH_CDC_NBOUNCE");
-        const int k = e ? atoi(e) : 4;
+        const int k = e ? atoi(e) : 8;
         return std::max(2, std::min(k, kCdcMaxBounce));
     }();
     return v;

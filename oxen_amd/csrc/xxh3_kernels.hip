@@ -508,10 +508,19 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
 // allows (not the case in a chunk table) are hashed by one lane each (correct, slow: K1 is the shape
 // for such batches). Byte-shifted items load from the dword below their start and re-align in
 // registers (the shift is per lane, 0 for aligned items).
-template <bool DESC, int VARIANT>
+//
+// FOLDED (K1F, FastCDC's second pass behind the folded walk W2, fastcdc.hip): blocks 4 .. nb-1 of an
+// item whose flag is set are not read; their sums (8 u64 per block, stored by W2 at index
+// (arena offset of the block) >> 10 of `sums`) are loaded instead -- by the row's quad 0, lane k the
+// accumulator pair (2k, 2k + 1), the other quads contributing 0 to the row reduction -- and the chain
+// scrambles them as usual. Blocks 0-3, the partial block and the last stripe come from the bytes. A
+// byte-shifted item's first data block after the sums takes its w0 from a dword loaded up front.
+template <bool DESC, int VARIANT, bool FOLDED = false>
 __device__ __forceinline__ void rows_item(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offsets,
                                           const uint64_t* __restrict__ lens, uint64_t n, uint64_t chunk,
-                                          uint64_t total, uint64_t* __restrict__ out) {
+                                          uint64_t total, uint64_t* __restrict__ out,
+                                          const uint64_t* __restrict__ sums = nullptr,
+                                          const uint8_t* __restrict__ flags = nullptr) {
     constexpr int D = Cfg<VARIANT>::DEPTH;
     constexpr bool NT = Cfg<VARIANT>::NT;
     constexpr int RPI = Cfg<VARIANT>::ROWS2 ? 2 : 1;  // 16-lane rows per item
@@ -584,10 +593,21 @@ __device__ __forceinline__ void rows_item(const uint8_t* __restrict__ arena, con
         // pieces j < jpart of the partial block are live (stripe 4*RPI*j + st0 < ns)
         const uint32_t jpart = act && ns > (uint32_t)st0 ? (ns - (uint32_t)st0 + 4 * RPI - 1) / (4 * RPI) : 0u;
         uint64_t a0 = kInitW[2 * k], a1 = kInitW[2 * k + 1];
+        // FOLDED: blocks [4, nb) of a flagged item come from `sums`
+        const bool has_w = FOLDED && act && nb > 4 && flags[item] != 0;
+        auto wblk = [&](uint32_t b) -> bool { return has_w && b >= 4u && b < nb; };
         // pieces j < live_n(b) of iteration b are live: NL in a full block, jpart in the partial one
-        auto live_n = [&](uint32_t b) -> uint32_t { return (act & (b < nb)) ? (uint32_t)NL : (b == nb) ? jpart : 0u; };
+        auto live_n = [&](uint32_t b) -> uint32_t {
+            return wblk(b) ? 0u : (act & (b < nb)) ? (uint32_t)NL : (b == nb) ? jpart : 0u;
+        };
         const __amdgpu_buffer_rsrc_t rsrc =
             __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), (short)0, (int)(uint32_t)span, kRsrcFlags);
+        // the wave's sums under one descriptor, from the block index of its lowest start
+        const uint64_t sidx0 = FOLDED ? (base - reinterpret_cast<uint64_t>(arena)) >> 10 : 0;
+        const uint32_t sspan = FOLDED ? (uint32_t)(((span >> 10) + 2) * 64) : 0u;
+        const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(
+            FOLDED ? (void*)(sums + 8 * sidx0) : (void*)arena, (short)0, (int)sspan, kRsrcFlags);
+        const uint32_t sv = FOLDED && act ? (uint32_t)(((off >> 10) - sidx0) * 64) + 16u * (uint32_t)t : 0u;
         // Byte-shifted items load every piece 4 bytes late: the lane then holds dwords w1..w4 of the
         // five its piece spans (w0 = the dword holding the piece's first byte) and takes w0 from the
         // previous lane's w4 (DPP row_ror:1; a row's first lane from the previous row of the item
@@ -602,9 +622,18 @@ __device__ __forceinline__ void rows_item(const uint8_t* __restrict__ arena, con
             const uint32_t jn = live_n(b);
 #pragma unroll
             for (int j = 0; j < NL; ++j) dst[j] = bload16<NT>(rsrc, (uint32_t)j < jn ? vo + (uint32_t)(256 * RPI * j) : kOOB);
+            if constexpr (FOLDED) {
+                if (wblk(b)) dst[0] = bload16<false>(srsrc, t < 4 ? sv + (b << 6) : kOOB);
+            }
         };
         uint32_t carry = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (shifted & head) ? vb : kOOB, 0, 0);
+        // FOLDED: the dword before the partial block, for the head lane of a shifted item with sums
+        const uint32_t carry_nb =
+            FOLDED ? __builtin_amdgcn_raw_buffer_load_b32(rsrc, (shifted & head & has_w) ? vb + (nb << 10) : kOOB, 0, 0) : 0u;
         auto fold = [&](uint4 (&src)[NL], uint32_t b) {
+            if constexpr (FOLDED) {
+                if (has_w && b == nb) carry = carry_nb;
+            }
             uint32_t w0s[NL];
 #pragma unroll
             for (int j = 0; j < NL; ++j) {
@@ -627,6 +656,12 @@ __device__ __forceinline__ void rows_item(const uint8_t* __restrict__ arena, con
                 const uint4 d = make_uint4(__builtin_amdgcn_perm(a.x, w0s[j], psel), __builtin_amdgcn_perm(a.y, a.x, psel),
                                            __builtin_amdgcn_perm(a.z, a.y, psel), __builtin_amdgcn_perm(a.w, a.z, psel));
                 if ((uint32_t)j < jn) accum16(d, key0[j], key1[j], s0, s1);
+            }
+            if constexpr (FOLDED) {
+                if (wblk(b)) {  // W2's block sum: quad 0 holds it, the others 0
+                    s0 = ((uint64_t)src[0].y << 32) | src[0].x;
+                    s1 = ((uint64_t)src[0].w << 32) | src[0].z;
+                }
             }
             s0 += dpp64<DPP_ROW_ROR4>(s0);
             s1 += dpp64<DPP_ROW_ROR4>(s1);
@@ -681,6 +716,15 @@ __device__ __forceinline__ void rows_item(const uint8_t* __restrict__ arena, con
         out[2 * item] = h.lo;
         out[2 * item + 1] = h.hi;
     }
+}
+
+// K1F: FastCDC chunk digests behind the folded walk (rows_item FOLDED), K1R's shape (variant 264).
+__global__ __launch_bounds__(128) void xxh3_rows_fold_kernel(const uint8_t* __restrict__ arena,
+                                                             const uint64_t* __restrict__ offsets,
+                                                             const uint64_t* __restrict__ lens, uint64_t n,
+                                                             uint64_t* __restrict__ out, const uint64_t* __restrict__ sums,
+                                                             const uint8_t* __restrict__ flags) {
+    rows_item<true, 264, true>(arena, offsets, lens, n, 0, 0, out, sums, flags);
 }
 
 template <bool DESC, int VARIANT>

@@ -115,15 +115,18 @@ def test_chunker_argument_errors(built_lib):
 
 
 # ------------------------------------------------------------------------------ GPU parity
-@pytest.fixture(params=["auto", "scan"])
+@pytest.fixture(params=["auto", "scan", "fold"])
 def cdc_path(request, monkeypatch):
-    """Both chunking paths: "auto" takes the walk (W + X) wherever it applies (avg <= 16 KiB, masks at
+    """Every chunking path: "auto" takes the walk (W + X) wherever it applies (avg <= 16 KiB, masks at
     bit 16 or above: the 8 KiB and 4 KiB configs), F1 + F2 elsewhere; "scan" forces F1 + F2
-    (OXH_CDC_WALK=0) everywhere."""
+    (OXH_CDC_WALK=0) everywhere; "fold" takes the walk with K1's block sums folded in (W2 + K1F,
+    OXH_CDC_FOLD=1) wherever the walk applies and min is whole 1 KiB blocks."""
+    monkeypatch.delenv("OXH_CDC_WALK", raising=False)
+    monkeypatch.delenv("OXH_CDC_FOLD", raising=False)
     if request.param == "scan":
         monkeypatch.setenv("OXH_CDC_WALK", "0")
-    else:
-        monkeypatch.delenv("OXH_CDC_WALK", raising=False)
+    elif request.param == "fold":
+        monkeypatch.setenv("OXH_CDC_FOLD", "1")
     return request.param
 
 

@@ -25,6 +25,11 @@ step pytest 1200 python -u -m pytest tests -m gpu -q --maxfail=20 --timeout 300 
 step bench 240 python bench.py --gpus 1 --steps 20 --warmup 5
 step bench_dist 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --dist --steps 20 --warmup 5 --no-cpu-baseline
 step c5e2e_small 600 python tools/bench_fastcdc_e2e.py --dir /tmp/oxh_c5s --files 16 --gib 1 --chunk 8192 --reps 3 --cold
+step probe 120 tools/fold_probe
+step foldtests 900 python -u -m pytest tests/test_fastcdc.py -m gpu -q --timeout 300 --timeout-method thread -k "fold or files or host"
+step c5_8k_fold 400 env OXH_CDC_FOLD=1 python tools/bench_fastcdc.py --chunk 8192 --reps 5 --check-all
+step c5_8k_base 400 python tools/bench_fastcdc.py --chunk 8192 --reps 5
+step c5_8k_fold_prof 400 env OXH_CDC_FOLD=1 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${T}_fold -o run --output-format csv -- python tools/bench_fastcdc.py --chunk 8192 --reps 3
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step e2e_nb4 600 env OXH_TRACE=1 OXH_CDC_NBOUNCE=4 python tools/bench_fastcdc_e2e.py --dir /tmp/oxh_c5s --files 16 --gib 1 --chunk 8192 --reps 3 --keep
 step e2e_nb8 600 env OXH_TRACE=1 OXH_CDC_NBOUNCE=8 python tools/bench_fastcdc_e2e.py --dir /tmp/oxh_c5s --files 16 --gib 1 --chunk 8192 --reps 3
