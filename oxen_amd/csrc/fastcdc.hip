@@ -786,7 +786,10 @@ __global__ __launch_bounds__(256) void cdc_emit_kernel(CdcFiles f, CdcParams prm
         const uint64_t b = k + 1 < cnt ? sec_start + src[k + 1] : ex;
         c_off[base + k] = foff + a;
         c_len[base + k] = b - a;
-        if (c_flag) c_flag[base + k] = own;
+        // a chunk that starts within `max` of its section start may overlap the previous section's
+        // last chunk, whose blocks that lane stored too (and a lane that had not yet met the true walk
+        // there stored blocks of chunks that are not the crate's): K1F hashes those from the bytes
+        if (c_flag) c_flag[base + k] = own && src[k] >= prm.max;
     }
 }
 
@@ -1006,7 +1009,10 @@ __global__ __launch_bounds__(64 * WAVES) void cdc_walk_scan_kernel(CdcFiles f, C
     };
     // the sum of the chunk's block 4 + (xk - 1) / 8 is complete: store it (recorded chunks only), restart
     auto fold_store = [&]() {
-        if (L.cs >= L.mS) {
+        // only chunks starting `max` or more into the lane's section: the previous lane's last chunk
+        // ends within `max` of the section start, and its sums must not be overwritten by a chunk this
+        // lane walked before meeting the true walk (emit flags the chunks in between for K1F's bytes)
+        if (L.cs >= L.mS + (uint32_t)prm.max) {
             const uint64_t blk = (mbase + (uint64_t)L.cs + (uint64_t)a0 + 1024ull * ((xk - 1) >> 3)) >> 10;
             uint4* dst = reinterpret_cast<uint4*>(geo.sums + 8 * blk);
             dst[0] = make_uint4((uint32_t)xa[0], (uint32_t)(xa[0] >> 32), (uint32_t)xa[1], (uint32_t)(xa[1] >> 32));
@@ -1678,9 +1684,15 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
     sc.want(&d_exit, n_sec);
     sc.want(&d_fix, n_sec * prm.speccap);
     sc.want(&d_out_base, n_sec + 1);
-    // W2 (the walk with K1's block sums folded in) + K1F: OXH_CDC_FOLD=1, on the walk path with digests
-    // asked for and `min` a whole number of 1 KiB blocks (C5: min 4 KiB). Sums: 64 B per KiB of arena.
+    // W2 (the walk with K1's block sums folded in) + K1F: OXH_CDC_FOLD=1 in the probe build
+    // (tools/build_probe_lib.py, -DOXH_PROBE_FOLD), on the walk path with digests asked for and `min` a
+    // whole number of 1 KiB blocks (C5: min 4 KiB). Sums: 64 B per KiB of arena. It measured 55.4 ms
+    // for C5 at 8 KiB against 43.5 for W + K1R (DESIGN §4 "W2"), so the shipped library does not take it.
+#ifdef OXH_PROBE_FOLD
     const bool fold_env = getenv("OXH_CDC_FOLD") && atoi(getenv("OXH_CDC_FOLD")) != 0;
+#else
+    const bool fold_env = false;  // measured and not kept (DESIGN §4 "W2"): the probe build has it
+#endif
     const bool fold = fold_env && walk && d_digests && capacity && min_size % 1024 == 0;
     uint64_t* d_sums = nullptr;
     uint8_t* d_flag = nullptr;
@@ -1707,8 +1719,10 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
         // wrong); the serial pass for whatever is left; then the chunk counts' prefix
         const uint64_t nwaves = (n_sec + 63) / 64;
         static const bool late = getenv("OXH_CDC_WALK_LATE") && atoi(getenv("OXH_CDC_WALK_LATE")) != 0;
-        auto walk_kernel = fold ? oxh::cdc_walk_scan_kernel<oxh::kScanWaves, false, true>
-                           : late ? oxh::cdc_walk_scan_kernel<oxh::kScanWaves, true> : oxh::cdc_walk_scan_kernel<oxh::kScanWaves, false>;
+        auto walk_kernel = late ? oxh::cdc_walk_scan_kernel<oxh::kScanWaves, true> : oxh::cdc_walk_scan_kernel<oxh::kScanWaves, false>;
+#ifdef OXH_PROBE_FOLD
+        if (fold) walk_kernel = oxh::cdc_walk_scan_kernel<oxh::kScanWaves, false, true>;
+#endif
         hipLaunchKernelGGL(walk_kernel,
                            dim3((unsigned)((nwaves + oxh::kScanWaves - 1) / oxh::kScanWaves)), dim3(64 * oxh::kScanWaves), 0, st,
                            f, prm, n_sec, oxh::WalkGeom{arena_bytes, d_sums});
@@ -1772,8 +1786,10 @@ int oxh_fastcdc_device(const void* d_arena, const uint64_t* offsets, const uint6
         uint64_t bytes = 0;
         for (uint64_t i = 0; i < n; ++i) bytes += lens[i];
         if (fold) {  // K1F: blocks 0-3 and the tail from the bytes, blocks 4.. from W2's sums
+#ifdef OXH_PROBE_FOLD
             hipLaunchKernelGGL(oxh::xxh3_rows_fold_kernel, dim3((unsigned)((total + 7) / 8)), dim3(128), 0, st,
                                (const uint8_t*)d_arena, d_chunk_offsets, d_chunk_lens, total, d_digests, d_sums, d_flag);
+#endif
             rc = hipGetLastError() == hipSuccess ? OXH_OK : OXH_ERR_HIP;
             if (rc) oxh::set_error(rc, "K1F launch");
         } else {

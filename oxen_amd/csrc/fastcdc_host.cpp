@@ -55,6 +55,14 @@ constexpr uint64_t kCdcBounce = 64ull << 20;  // one pinned bounce buffer (a win
 constexpr int kCdcMaxBounce = 16;
 // the ring: reads of the next windows run while earlier H2Ds drain (OXH_CDC_NBOUNCE, 2..16, default 8:
 // 47.7 vs 43.6 GiB/s for 4 on 16 x 1 GiB from the page cache, profiles/r05/r05a_e2e_*)
+// H2D copy streams the windows alternate over (OXH_CDC_COPY_STREAMS, 1 or 2; default 1)
+int cdc_copy_streams() {
+    static const int v = [] {
+        const char* e = getenv("OXH_CDC_COPY_STREAMS");
+        return e && atoi(e) == 2 ? 2 : 1;
+    }();
+    return v;
+}
 int cdc_nbounce() {
     static const int v = [] {
         const char* e = getenv("OXH_CDC_NBOUNCE");
@@ -75,9 +83,11 @@ inline uint64_t align_up(uint64_t x) { return (x + kCdcAlign - 1) & ~(kCdcAlign 
 struct CdcHost {
     int device = 0;
     hipStream_t copy = nullptr, comp = nullptr;
+    hipStream_t copy2 = nullptr;  // a second copy stream (OXH_CDC_COPY_STREAMS=2): windows alternate
+    int ncopy = 1;
     uint64_t piece = 0;
     uint8_t* d_piece[2] = {};
-    hipEvent_t ev_copied[2] = {};
+    hipEvent_t ev_copied[2] = {}, ev_copied2[2] = {};
     int nbounce = 0;
     uint8_t* h_bounce[kCdcMaxBounce] = {};
     hipEvent_t ev_bounce[kCdcMaxBounce] = {};
@@ -95,12 +105,16 @@ struct CdcHost {
             if (p) (void)hipFree(p);
         for (auto e : ev_copied)
             if (e) (void)hipEventDestroy(e);
+        for (auto e : ev_copied2)
+            if (e) (void)hipEventDestroy(e);
+        if (copy2) (void)hipStreamSynchronize(copy2);
         for (int i = 0; i < kCdcMaxBounce; ++i) {
             if (h_bounce[i]) (void)hipHostFree(h_bounce[i]);
             if (ev_bounce[i]) (void)hipEventDestroy(ev_bounce[i]);
         }
         free_tables();
         if (copy) (void)hipStreamDestroy(copy);
+        if (copy2) (void)hipStreamDestroy(copy2);
         if (comp) (void)hipStreamDestroy(comp);
         delete pool;
     }
@@ -138,7 +152,7 @@ void free_cdc_host(void* p) { delete static_cast<CdcHost*>(p); }
 int cdc_host(oxh_ctx* ctx, uint64_t piece, CdcHost** out) {
     void*& slot = oxh::ctx_cdc_state(ctx, free_cdc_host);
     CdcHost* h = static_cast<CdcHost*>(slot);
-    if (h && h->piece == piece && h->nbounce == cdc_nbounce()) {
+    if (h && h->piece == piece && h->nbounce == cdc_nbounce() && h->ncopy == cdc_copy_streams()) {
         *out = h;
         return OXH_OK;
     }
@@ -155,9 +169,13 @@ int cdc_host(oxh_ctx* ctx, uint64_t piece, CdcHost** out) {
     if (hipStreamCreateWithFlags(&h->copy, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&h->comp, hipStreamNonBlocking) != hipSuccess)
         return bad(OXH_ERR_HIP, "streams");
+    h->ncopy = cdc_copy_streams();
+    if (h->ncopy == 2 && hipStreamCreateWithFlags(&h->copy2, hipStreamNonBlocking) != hipSuccess) return bad(OXH_ERR_HIP, "streams");
     for (int b = 0; b < 2; ++b) {
         if (hipMalloc(&h->d_piece[b], piece + 4096) != hipSuccess) return bad(OXH_ERR_NOMEM, "device piece buffers");
-        if (hipEventCreateWithFlags(&h->ev_copied[b], hipEventDisableTiming) != hipSuccess) return bad(OXH_ERR_HIP, "events");
+        if (hipEventCreateWithFlags(&h->ev_copied[b], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&h->ev_copied2[b], hipEventDisableTiming) != hipSuccess)
+            return bad(OXH_ERR_HIP, "events");
     }
     h->nbounce = cdc_nbounce();
     for (int i = 0; i < h->nbounce; ++i) {
@@ -369,7 +387,9 @@ void chunk_rounds(Call& C) {
         }
         const uint64_t need = oxh_fastcdc_max_chunks(lens.data(), m, C.mn) + 1;
         int rc = h.tables(need);
-        if (rc == OXH_OK && hipStreamWaitEvent(h.comp, h.ev_copied[R.b], 0) != hipSuccess) rc = oxh::set_error(OXH_ERR_HIP, "wait copies");
+        if (rc == OXH_OK && (hipStreamWaitEvent(h.comp, h.ev_copied[R.b], 0) != hipSuccess ||
+                             (h.ncopy == 2 && hipStreamWaitEvent(h.comp, h.ev_copied2[R.b], 0) != hipSuccess)))
+            rc = oxh::set_error(OXH_ERR_HIP, "wait copies");
         if (rc == OXH_OK)
             rc = oxh_fastcdc_device(h.d_piece[R.b], offs.data(), lens.data(), m, C.mn, C.av, C.mx, C.lv, h.d_off, h.d_len,
                                     C.dig ? h.d_dig : nullptr, h.tab_cap, first.data(), h.comp);
@@ -433,8 +453,9 @@ int upload_round(Call& C, const Round& R) {
         W.grp.wait();
         C.t_read_wait += now() - tw;
         if (W.used == 0) return OXH_OK;
-        if (hipMemcpyAsync(h.d_piece[R.b] + W.base, h.h_bounce[W.bb], W.used, hipMemcpyHostToDevice, h.copy) != hipSuccess ||
-            hipEventRecord(h.ev_bounce[W.bb], h.copy) != hipSuccess)
+        hipStream_t cs = (h.ncopy == 2 && (W.base / kCdcBounce) % 2) ? h.copy2 : h.copy;
+        if (hipMemcpyAsync(h.d_piece[R.b] + W.base, h.h_bounce[W.bb], W.used, hipMemcpyHostToDevice, cs) != hipSuccess ||
+            hipEventRecord(h.ev_bounce[W.bb], cs) != hipSuccess)
             return oxh::set_error(OXH_ERR_HIP, "piece H2D");
         h.bounce_used[W.bb] = true;
         return OXH_OK;
@@ -475,7 +496,9 @@ int upload_round(Call& C, const Round& R) {
         inflight.pop_front();
         if (rc == OXH_OK) rc = r2;
     }
-    if (rc == OXH_OK && hipEventRecord(h.ev_copied[R.b], h.copy) != hipSuccess) rc = oxh::set_error(OXH_ERR_HIP, "copy event");
+    if (rc == OXH_OK && (hipEventRecord(h.ev_copied[R.b], h.copy) != hipSuccess ||
+                         (h.ncopy == 2 && hipEventRecord(h.ev_copied2[R.b], h.copy2) != hipSuccess)))
+        rc = oxh::set_error(OXH_ERR_HIP, "copy event");
     return rc;
 }
 
@@ -595,6 +618,7 @@ int run(oxh_ctx* ctx, CdcSource& src, uint64_t n, uint32_t mn, uint32_t av, uint
     C.cv.notify_all();
     chunker.join();
     (void)hipStreamSynchronize(h->copy);
+    if (h->copy2) (void)hipStreamSynchronize(h->copy2);
     for (uint64_t i = 0; i < n; ++i) src.close(i);
     if (C.rc.load() != OXH_OK) return oxh::set_error(C.rc.load(), "FastCDC host pipeline: " + C.err);
     for (uint64_t i = 0; i < n; ++i) {

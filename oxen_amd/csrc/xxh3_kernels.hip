@@ -718,7 +718,9 @@ __device__ __forceinline__ void rows_item(const uint8_t* __restrict__ arena, con
     }
 }
 
-// K1F: FastCDC chunk digests behind the folded walk (rows_item FOLDED), K1R's shape (variant 264).
+#ifdef OXH_PROBE_FOLD
+// K1F: FastCDC chunk digests behind the folded walk (rows_item FOLDED), K1R's shape (variant 264). Probe
+// build only: measured and not kept (DESIGN §4 "W2").
 __global__ __launch_bounds__(128) void xxh3_rows_fold_kernel(const uint8_t* __restrict__ arena,
                                                              const uint64_t* __restrict__ offsets,
                                                              const uint64_t* __restrict__ lens, uint64_t n,
@@ -726,6 +728,7 @@ __global__ __launch_bounds__(128) void xxh3_rows_fold_kernel(const uint8_t* __re
                                                              const uint8_t* __restrict__ flags) {
     rows_item<true, 264, true>(arena, offsets, lens, n, 0, 0, out, sums, flags);
 }
+#endif
 
 template <bool DESC, int VARIANT>
 __global__ __launch_bounds__(256) void xxh3_wave_kernel(const uint8_t* __restrict__ arena,

@@ -115,12 +115,13 @@ def test_chunker_argument_errors(built_lib):
 
 
 # ------------------------------------------------------------------------------ GPU parity
-@pytest.fixture(params=["auto", "scan", "fold"])
+@pytest.fixture(params=["auto", "scan"] + (["fold"] if os.environ.get("OXH_TEST_FOLD") else []))
 def cdc_path(request, monkeypatch):
     """Every chunking path: "auto" takes the walk (W + X) wherever it applies (avg <= 16 KiB, masks at
     bit 16 or above: the 8 KiB and 4 KiB configs), F1 + F2 elsewhere; "scan" forces F1 + F2
-    (OXH_CDC_WALK=0) everywhere; "fold" takes the walk with K1's block sums folded in (W2 + K1F,
-    OXH_CDC_FOLD=1) wherever the walk applies and min is whole 1 KiB blocks."""
+    (OXH_CDC_WALK=0) everywhere; with OXH_TEST_FOLD=1 (against the probe build,
+    tools/build_probe_lib.py + tools/with_lib.py) also "fold": the walk with K1's block sums folded in
+    (W2 + K1F, OXH_CDC_FOLD=1; measured and not kept, DESIGN §4 "W2")."""
     monkeypatch.delenv("OXH_CDC_WALK", raising=False)
     monkeypatch.delenv("OXH_CDC_FOLD", raising=False)
     if request.param == "scan":
