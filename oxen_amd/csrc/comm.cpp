@@ -12,6 +12,7 @@
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 #include <dlfcn.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -159,7 +160,10 @@ int oxh_gather_digests(oxh_comm* c, const uint64_t* d_local, const uint64_t* cou
     if (counts[me] && !d_local) return oxh::set_error(OXH_ERR_INVALID, "null local table");
     if (receives && base[P] && !d_full) return oxh::set_error(OXH_ERR_INVALID, "null full table");
     hipStream_t st = (hipStream_t)stream;
-    const bool equal = std::all_of(counts, counts + P, [&](uint64_t k) { return k == counts[0]; });
+    // OXH_GATHER_P2P=1 takes the grouped point-to-point form even for equal shares (tests: the ragged
+    // path on a one-GPU box)
+    const char* pe = getenv("OXH_GATHER_P2P");
+    const bool equal = !(pe && atoi(pe) != 0) && std::all_of(counts, counts + P, [&](uint64_t k) { return k == counts[0]; });
     const size_t words = 2 * (size_t)counts[0];  // a digest is two u64 (lo, hi)
     int prev = 0;
     (void)hipGetDevice(&prev);

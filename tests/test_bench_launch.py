@@ -105,6 +105,18 @@ def test_pipelined_gather_rccl_in_process(cuda, oracle_lib):
         torch.cuda.synchronize()
         assert torch.equal(full, ref)
         comm.gather(ref[:0], [0], torch.empty((0, 2), dtype=torch.int64, device=cuda), root=-1)
+        # the ragged-share form (grouped ncclBroadcast for every rank, send/recv + the root's own copy)
+        import os
+
+        os.environ["OXH_GATHER_P2P"] = "1"
+        try:
+            for root in (-1, 0):
+                full = torch.zeros_like(ref)
+                comm.gather(ref, [len(lens)], full, root=root)
+                torch.cuda.synchronize()
+                assert torch.equal(full, ref), root
+        finally:
+            del os.environ["OXH_GATHER_P2P"]
         with pytest.raises(_capi.OxenError) as e:
             comm.gather(ref, [len(lens)], full, root=1)
         assert e.value.code == _capi.OXH_ERR_INVALID

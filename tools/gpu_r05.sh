@@ -36,5 +36,11 @@ step e2e_nb8 600 env OXH_TRACE=1 OXH_CDC_NBOUNCE=8 python tools/bench_fastcdc_e2
 step e2e_shm_8k 900 env OXH_TRACE=1 OXH_CDC_NBOUNCE=${NB:-8} python tools/bench_fastcdc_e2e.py --dir /dev/shm/oxh_c5 --files 16 --gib 8 --chunk 8192 --reps 3 --keep
 step e2e_shm_64k 900 env OXH_TRACE=1 OXH_CDC_NBOUNCE=${NB:-8} python tools/bench_fastcdc_e2e.py --dir /dev/shm/oxh_c5 --files 16 --gib 8 --chunk 65536 --reps 3
 step e2e_disk_8k 900 env OXH_TRACE=1 OXH_CDC_NBOUNCE=${NB:-8} python tools/bench_fastcdc_e2e.py --dir /tmp/oxh_c5d --files 8 --gib 8 --chunk 8192 --reps 2 --cold
+step profile_c2 900 env TAG=${T} WORKLOAD=c2 PMC=1 bash tools/gpu_profile_driver.sh
+step c5_64k_prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${T}_c5_64k -o run --output-format csv -- python tools/bench_fastcdc.py --chunk 65536 --reps 3
+step c5_8k_prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${T}_c5_8k -o run --output-format csv -- python tools/bench_fastcdc.py --chunk 8192 --reps 3
+step e2e_cs1 600 env OXH_TRACE=1 OXH_CDC_COPY_STREAMS=1 python tools/bench_fastcdc_e2e.py --dir /tmp/oxh_c5s --files 16 --gib 1 --chunk 8192 --reps 5 --keep --cpu none
+step e2e_cs2 600 env OXH_TRACE=1 OXH_CDC_COPY_STREAMS=2 python tools/bench_fastcdc_e2e.py --dir /tmp/oxh_c5s --files 16 --gib 1 --chunk 8192 --reps 5 --keep --cpu none
+step e2e_cs1b 600 env OXH_TRACE=1 OXH_CDC_COPY_STREAMS=1 python tools/bench_fastcdc_e2e.py --dir /tmp/oxh_c5s --files 16 --gib 1 --chunk 8192 --reps 5 --cpu none
 rm -rf /dev/shm/oxh_c5 /tmp/oxh_c5s /tmp/oxh_c5d
 echo "== done $(date +%T)"
