@@ -686,4 +686,95 @@ void LocalVersionStore::combine_version_chunks(const std::string& hash) const {
 }
 
 }  // namespace storage
+namespace dedup {
+namespace {
+std::vector<std::vector<Chunk>> split(const std::vector<uint64_t>& first, const std::vector<uint64_t>& off,
+                                      const std::vector<uint64_t>& len, const std::vector<uint64_t>& dig) {
+    std::vector<std::vector<Chunk>> r(first.size() - 1);
+    for (size_t i = 0; i + 1 < first.size(); ++i)
+        for (uint64_t k = first[i]; k < first[i + 1]; ++k) r[i].push_back({off[k], len[k], to_u128(dig[2 * k], dig[2 * k + 1])});
+    return r;
+}
+}  // namespace
+
+std::vector<ChunkedFile> fastcdc_files(const std::vector<std::string>& paths, uint32_t min_size, uint32_t avg_size,
+                                       uint32_t max_size, oxh_ctx* ctx) {
+    ctx = ctx ? ctx : util::hasher::default_context();
+    const size_t n = paths.size();
+    std::vector<const char*> cp(n);
+    std::vector<uint64_t> sz(n, 0);
+    for (size_t i = 0; i < n; ++i) {
+        cp[i] = paths[i].c_str();
+        struct stat sb;
+        if (stat(cp[i], &sb) == 0) sz[i] = (uint64_t)sb.st_size;
+    }
+    uint64_t cap = std::max<uint64_t>(1, oxh_fastcdc_max_chunks(sz.data(), n, min_size));
+    for (int attempt = 0;; ++attempt) {
+        std::vector<uint64_t> off(cap), len(cap), dig(2 * cap), first(n + 1), sizes(n);
+        std::vector<int32_t> status(n), oserr(n);
+        const int rc = oxh_fastcdc_files(ctx, cp.data(), n, min_size, avg_size, max_size, 1, off.data(), len.data(),
+                                         dig.data(), cap, first.data(), sizes.data(), status.data(), oserr.data());
+        if (rc == OXH_ERR_INVALID && attempt < 2) {  // a file grew since the stat: the text has the count
+            const std::string e = oxh_last_error();
+            const size_t at = e.find("need ");
+            if (at != std::string::npos) {
+                cap = std::stoull(e.substr(at + 5));
+                continue;
+            }
+        }
+        if (rc != OXH_OK) throw OxenError::basic_str(std::string("oxh_fastcdc_files: ") + oxh_last_error(), rc);
+        std::vector<std::vector<Chunk>> per = split(first, off, len, dig);
+        std::vector<ChunkedFile> r(n);
+        for (size_t i = 0; i < n; ++i) {
+            r[i].ok = status[i] == OXH_OK;
+            r[i].size = sizes[i];
+            r[i].code = status[i];
+            r[i].os_error = oserr[i];
+            r[i].chunks = std::move(per[i]);
+        }
+        return r;
+    }
+}
+
+std::vector<std::vector<Chunk>> fastcdc_buffers(const std::vector<std::string_view>& buffers, uint32_t min_size,
+                                                uint32_t avg_size, uint32_t max_size, oxh_ctx* ctx) {
+    ctx = ctx ? ctx : util::hasher::default_context();
+    const size_t n = buffers.size();
+    std::vector<const uint8_t*> ptrs(n);
+    std::vector<uint64_t> lens(n);
+    for (size_t i = 0; i < n; ++i) {
+        ptrs[i] = reinterpret_cast<const uint8_t*>(buffers[i].data());
+        lens[i] = buffers[i].size();
+    }
+    const uint64_t cap = std::max<uint64_t>(1, oxh_fastcdc_max_chunks(lens.data(), n, min_size));
+    std::vector<uint64_t> off(cap), len(cap), dig(2 * cap), first(n + 1);
+    check(oxh_fastcdc_host(ctx, ptrs.data(), lens.data(), n, min_size, avg_size, max_size, 1, off.data(), len.data(),
+                           dig.data(), cap, first.data()),
+          "oxh_fastcdc_host");
+    return split(first, off, len, dig);
+}
+
+std::string chunk_name(u128 hash) {
+    char b[48];
+    oxh_format_dec((uint64_t)hash, (uint64_t)(hash >> 64), b);
+    return b;
+}
+}  // namespace dedup
+
+namespace multigpu {
+std::vector<uint8_t> DigestGather::unique_id() {
+    std::vector<uint8_t> id(OXH_COMM_ID_BYTES);
+    check(oxh_comm_unique_id(id.data()), "oxh_comm_unique_id");
+    return id;
+}
+DigestGather::DigestGather(const std::vector<uint8_t>& id, int rank, int nranks, int device) {
+    if (id.size() != OXH_COMM_ID_BYTES) throw OxenError::basic_str("a comm id is OXH_COMM_ID_BYTES bytes", OXH_ERR_INVALID);
+    check(oxh_comm_create(id.data(), rank, nranks, device, &c_), "oxh_comm_create");
+}
+DigestGather::~DigestGather() { (void)oxh_comm_destroy(c_); }
+void DigestGather::gather(const uint64_t* d_local, const std::vector<uint64_t>& counts, uint64_t* d_full, int root,
+                          void* stream) const {
+    check(oxh_gather_digests(c_, d_local, counts.data(), d_full, root, stream), "oxh_gather_digests");
+}
+}  // namespace multigpu
 }  // namespace liboxen

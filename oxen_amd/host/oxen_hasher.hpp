@@ -293,4 +293,46 @@ class LocalVersionStore {
 };
 
 }  // namespace storage
+
+// experiments/block-level-dedup/src/chunker/fastcdchunker.rs:72-122 over the ABI's host entry points:
+// fs::read(input_file) (:75) -> v2020 chunking (:83-88) -> xxh3_128 per chunk (:95-98), the file read
+// inside the library and streamed through its piece pipeline (oxh_fastcdc_files / oxh_fastcdc_host).
+namespace dedup {
+struct Chunk {
+    uint64_t offset = 0, length = 0;  // the crate's Chunk.offset / length, relative to the file
+    u128 hash = 0;                    // xxh3_128 of the chunk (its file name is hash.to_string())
+};
+struct ChunkedFile {
+    bool ok = false;
+    uint64_t size = 0;
+    int code = 0, os_error = 0;  // as FileHash: OXH_ERR_OPEN / OXH_ERR_IO with the errno
+    std::vector<Chunk> chunks;
+};
+// One entry per path; min / avg / max as v2020::FastCDC::new (FastCDChunker: 4096, chunk, 2 * chunk).
+std::vector<ChunkedFile> fastcdc_files(const std::vector<std::string>& paths, uint32_t min_size, uint32_t avg_size,
+                                       uint32_t max_size, oxh_ctx* ctx = nullptr);
+std::vector<std::vector<Chunk>> fastcdc_buffers(const std::vector<std::string_view>& buffers, uint32_t min_size,
+                                                uint32_t avg_size, uint32_t max_size, oxh_ctx* ctx = nullptr);
+// u128::to_string() (fastcdchunker.rs:98, the chunk file name)
+std::string chunk_name(u128 hash);
+}  // namespace dedup
+
+// one process per GPU, the digest table gathered once over xGMI (oxh_comm_*).
+namespace multigpu {
+class DigestGather {
+   public:
+    static std::vector<uint8_t> unique_id();  // OXH_COMM_ID_BYTES; one rank makes it, every rank gets it
+    DigestGather(const std::vector<uint8_t>& id, int rank, int nranks, int device);  // blocks until all join
+    ~DigestGather();
+    DigestGather(const DigestGather&) = delete;
+    DigestGather& operator=(const DigestGather&) = delete;
+    // d_local: this rank's 2 * counts[rank] u64 on the device; d_full: 2 * sum(counts) u64 on the device
+    // (every rank when root < 0, else rank `root` only); enqueued on `stream` (hipStream_t)
+    void gather(const uint64_t* d_local, const std::vector<uint64_t>& counts, uint64_t* d_full, int root,
+                void* stream) const;
+
+   private:
+    oxh_comm* c_ = nullptr;
+};
+}  // namespace multigpu
 }  // namespace liboxen

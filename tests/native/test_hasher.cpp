@@ -458,6 +458,56 @@ static void verified_publish(const std::string& scratch) {
     CHECK((store2.list_version_chunks(wrong) == std::vector<uint64_t>{0, 5, 7}));
 }
 
+// dedup::fastcdc_files / fastcdc_buffers (fastcdchunker.rs:75-98 over oxh_fastcdc_files / _host): the two
+// entries agree, chunks tile each file within [min, max] (a file's last may be shorter), every chunk's hash
+// equals hash_buffer_128bit of its bytes (K1 through the host-buffer path), and a missing path is that
+// file's error only. The boundaries against the oracle: tests/test_fastcdc.py.
+static void dedup_chunks(const std::string& golden) {
+    namespace dd = liboxen::dedup;
+    std::string big(3000017, '\0');
+    uint64_t z = 12345;
+    for (auto& ch : big) {
+        z = z * 6364136223846793005ull + 1442695040888963407ull;
+        ch = (char)(z >> 56);
+    }
+    char tmpl[] = "/tmp/oxh_cdc_XXXXXX";
+    const char* dir = mkdtemp(tmpl);
+    CHECK(dir != nullptr);
+    if (!dir) return;
+    const std::string p_big = std::string(dir) + "/big.bin";
+    if (FILE* f = fopen(p_big.c_str(), "wb")) {
+        fwrite(big.data(), 1, big.size(), f);
+        fclose(f);
+    }
+    const std::string hello = golden + "/data_test/text/hello.txt", missing = std::string(dir) + "/missing";
+    const auto files = dd::fastcdc_files({p_big, missing, hello}, 4096, 8192, 16384);
+    CHECK(files.size() == 3 && files[0].ok && !files[1].ok && files[2].ok);
+    CHECK(files[1].code == OXH_ERR_OPEN && files[1].os_error == ENOENT && files[1].chunks.empty());
+    CHECK(files[0].size == big.size() && files[2].size == 5 && files[2].chunks.size() == 1);
+    const auto bufs = dd::fastcdc_buffers({std::string_view(big), std::string_view("hello")}, 4096, 8192, 16384);
+    CHECK(bufs.size() == 2 && bufs[0].size() == files[0].chunks.size());
+    uint64_t at = 0;
+    bool tiles = true, same = true, hashes = true;
+    for (size_t k = 0; k < files[0].chunks.size(); ++k) {
+        const auto& c = files[0].chunks[k];
+        tiles = tiles && c.offset == at && c.length <= 16384 && (c.length >= 4096 || k + 1 == files[0].chunks.size());
+        same = same && k < bufs[0].size() && bufs[0][k].offset == c.offset && bufs[0][k].length == c.length &&
+               bufs[0][k].hash == c.hash;
+        at += c.length;
+    }
+    for (size_t k = 0; k < files[0].chunks.size(); k += 37) {
+        const auto& c = files[0].chunks[k];
+        hashes = hashes && hasher::hash_buffer_128bit(big.data() + c.offset, c.length) == c.hash;
+    }
+    CHECK(tiles && at == big.size());
+    CHECK(same);
+    CHECK(hashes);
+    CHECK(files[2].chunks[0].hash == hex("1bfd09d1a433fb78117b4c7b1583d16d"));
+    CHECK(dd::chunk_name(files[2].chunks[0].hash) == "37203006142592822661058489871983956333");
+    const std::string rm = std::string("rm -rf ") + dir;
+    if (system(rm.c_str()) != 0) fprintf(stderr, "could not remove %s\n", dir);
+}
+
 int main(int argc, char** argv) {
     const std::string golden = argc > 1 ? argv[1] : "tests/golden";
     try {
@@ -469,6 +519,7 @@ int main(int argc, char** argv) {
         merkle_hash();
         long_stream();
         modified_check(golden);
+        dedup_chunks(golden);
         char tmpl[] = "/tmp/oxh_native_XXXXXX";
         const char* scratch = mkdtemp(tmpl);
         if (!scratch) throw std::runtime_error("mkdtemp failed");
