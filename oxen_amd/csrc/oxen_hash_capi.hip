@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <atomic>
 #include <condition_variable>
+#include <deque>
 #include <functional>
 #include <map>
 #include <memory>
@@ -279,9 +280,9 @@ struct oxh_ctx {
     // and two pinned bounce buffers the file is read into in pieces
     uint8_t* d_big = nullptr;
     uint64_t d_big_size = 0;
-    uint8_t* h_bounce[4] = {};   // kNBounce pinned bounce buffers, used as a ring
-    hipEvent_t ev_bounce[4] = {};
-    bool bounce_used[4] = {};
+    uint8_t* h_bounce[8] = {};   // kNBounce pinned bounce buffers, used as a ring
+    hipEvent_t ev_bounce[8] = {};
+    bool bounce_used[8] = {};
     uint64_t bounce_next = 0;    // the ring position (kept across pieces and files)
     hipEvent_t ev_piece_free[2] = {};
     void* live = nullptr;  // the engine's current run (a FileStream, for diagnostics), under qmu
@@ -574,7 +575,17 @@ int oversize_item(oxh_ctx* c, const uint8_t* src, uint64_t len, uint64_t* out2, 
 // add) every bounce part is also written to the sink's temp as it is read, and the temp is published
 // once the digest is known: the item never has to fit in host memory.
 constexpr uint64_t kBounce = 64ull << 20, kBigRead = 4ull << 20;
-constexpr int kNBounce = 4;  // bounce buffers in the ring: reads of the next parts run while earlier H2Ds drain
+constexpr int kNBounce = 8;  // bounce buffers in the ring: up to 7 windows read while earlier H2Ds drain
+
+// Bounce windows a large item reads at once (OXH_BIG_WINDOWS, 1 .. kNBounce - 1; 1 is the r03-r04 form)
+int big_windows() {
+    static const int v = [] {
+        const char* e = getenv("OXH_BIG_WINDOWS");
+        const int k = e ? atoi(e) : kNBounce - 1;
+        return std::max(1, std::min(k, kNBounce - 1));
+    }();
+    return v;
+}
 
 // Where a large item's bytes come from.
 struct LargeSource {
@@ -789,43 +800,79 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
         }
     }
     int rc = OXH_OK;
-    // piece [off, off + plen) of item q -> device buffer d on the copy stream; false on an I/O error
+    // piece [off, off + plen) of item q -> device buffer d on the copy stream; false on an I/O error.
+    // The piece goes through the bounce ring in windows of kBounce: up to kNBounce - 1 windows are read
+    // at once (their 4 MiB parts queued on the pool without a barrier between windows), and a window's
+    // H2D is issued as soon as its own parts are done (r05; r03-r04 read one window at a time).
+    struct Window {
+        int bb = 0;
+        uint64_t o = 0, m = 0;
+        std::atomic<bool> bad{false};
+        std::function<void(int)> fn;
+        oxh::Pool::Group grp;
+    };
     auto copy_piece = [&](int q, uint64_t off, uint64_t plen, uint8_t* d) -> bool {
         LargeSource& src = *jobs[q].src;
         State& S = st[q];
-        for (uint64_t o = 0; o < plen; o += kBounce) {  // bounce-buffer path
-            const int bb = (int)(c->bounce_next++ % kNBounce);
-            if (c->bounce_used[bb] && hipEventSynchronize(c->ev_bounce[bb]) != hipSuccess) return false;
-            const uint64_t m = std::min(kBounce, plen - o);
-            src.will_need(off + o + m, 2 * kBounce);  // two bounce pieces ahead while the pool reads this one
-            const int parts = (int)((m + kBigRead - 1) / kBigRead);
-            std::atomic<bool> bad{false};
-            c->pool->parallel_for(parts, [&](int t) {
+        std::vector<std::unique_ptr<Window>> wins;
+        std::deque<Window*> inflight;
+        bool ok = true;
+        auto finish = [&](Window& W) {
+            W.grp.wait();
+            if (W.bad.load()) ok = false;
+            if (!ok) return;
+            if (hipMemcpyAsync(d + W.o, c->h_bounce[W.bb], W.m, hipMemcpyHostToDevice, c->copy_stream) != hipSuccess ||
+                hipEventRecord(c->ev_bounce[W.bb], c->copy_stream) != hipSuccess) {
+                ok = false;
+                return;
+            }
+            c->bounce_used[W.bb] = true;
+        };
+        for (uint64_t o = 0; o < plen && ok; o += kBounce) {
+            wins.emplace_back(new Window);
+            Window& W = *wins.back();
+            W.bb = (int)(c->bounce_next++ % kNBounce);
+            W.o = o;
+            W.m = std::min(kBounce, plen - o);
+            if (c->bounce_used[W.bb] && hipEventSynchronize(c->ev_bounce[W.bb]) != hipSuccess) {
+                ok = false;
+                break;
+            }
+            c->bounce_used[W.bb] = false;
+            src.will_need(off + o + W.m, 2 * kBounce);  // two windows ahead of the ones being read
+            uint8_t* buf = c->h_bounce[W.bb];
+            const uint64_t base = off + o, m = W.m;
+            W.fn = [&src, &S, &W, buf, base, m](int t) {
                 const uint64_t lo = (uint64_t)t * kBigRead, hi = std::min(m, lo + kBigRead);
-                if (!src.read(off + o + lo, hi - lo, c->h_bounce[bb] + lo)) {
-                    bad.store(true);
+                if (!src.read(base + lo, hi - lo, buf + lo)) {
+                    W.bad.store(true);
                     return;
                 }
                 if (S.sfd >= 0 && S.sink_ok.load(std::memory_order_relaxed))  // the same bytes to the temp blob
                     for (uint64_t put = lo; put < hi;) {
-                        const ssize_t x = pwrite(S.sfd, c->h_bounce[bb] + put, hi - put, (off_t)(off + o + put));
+                        const ssize_t x = pwrite(S.sfd, buf + put, hi - put, (off_t)(base + put));
                         if (x <= 0) {
                             S.sink_ok.store(false);
                             break;
                         }
                         put += (uint64_t)x;
                     }
-            });
-            if (bad.load()) return false;
-            if (hipMemcpyAsync(d + o, c->h_bounce[bb], m, hipMemcpyHostToDevice, c->copy_stream) != hipSuccess ||
-                hipEventRecord(c->ev_bounce[bb], c->copy_stream) != hipSuccess)
-                return false;
-            c->bounce_used[bb] = true;
+            };
+            c->pool->start((int)((m + kBigRead - 1) / kBigRead), W.fn, W.grp);
+            inflight.push_back(&W);
+            if ((int)inflight.size() >= big_windows()) {
+                finish(*inflight.front());
+                inflight.pop_front();
+            }
         }
-        // no wait here: the piece's kernels wait for the copy stream through ev_copy, and a bounce
-        // buffer is refilled only after its own H2D (ev_bounce), so the next piece's reads overlap
-        // this piece's last copies
-        return true;
+        while (!inflight.empty()) {  // every started window is waited for, also after a failure
+            finish(*inflight.front());
+            inflight.pop_front();
+        }
+        // no wait for the copies here: the piece's kernels wait for the copy stream through ev_copy,
+        // and a bounce buffer is refilled only after its own H2D (ev_bounce), so the next piece's reads
+        // overlap this piece's last copies
+        return ok;
     };
     // With OXH_BIG_DIRECT=1, pieces whose pages are in the page cache are pinned in place and copied
     // asynchronously; the next round's pieces are pinned while this round's copies run, and a round's

@@ -42,5 +42,17 @@ step c5_8k_prof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${T}_c5_
 step e2e_cs1 600 env OXH_TRACE=1 OXH_CDC_COPY_STREAMS=1 python tools/bench_fastcdc_e2e.py --dir /tmp/oxh_c5s --files 16 --gib 1 --chunk 8192 --reps 5 --keep --cpu none
 step e2e_cs2 600 env OXH_TRACE=1 OXH_CDC_COPY_STREAMS=2 python tools/bench_fastcdc_e2e.py --dir /tmp/oxh_c5s --files 16 --gib 1 --chunk 8192 --reps 5 --keep --cpu none
 step e2e_cs1b 600 env OXH_TRACE=1 OXH_CDC_COPY_STREAMS=1 python tools/bench_fastcdc_e2e.py --dir /tmp/oxh_c5s --files 16 --gib 1 --chunk 8192 --reps 5 --cpu none
-rm -rf /dev/shm/oxh_c5 /tmp/oxh_c5s /tmp/oxh_c5d
+step c5_64k_walk 400 env OXH_CDC_WALK=1 python tools/bench_fastcdc.py --chunk 65536 --reps 3
+step c5_64k_fold 400 env OXH_CDC_WALK=1 OXH_CDC_FOLD=1 python tools/with_lib.py tools/probe/liboxen_hash.so tools/bench_fastcdc.py --chunk 65536 --reps 3
+step native 300 python -u -m pytest tests/test_native_mirror.py -m gpu -q --timeout 240 --timeout-method thread
+step shm_cs1 900 env OXH_TRACE=1 OXH_CDC_COPY_STREAMS=1 python tools/bench_fastcdc_e2e.py --dir /dev/shm/oxh_c5 --files 16 --gib 8 --chunk 8192 --reps 3 --keep --cpu none
+step shm_cs2 900 env OXH_TRACE=1 OXH_CDC_COPY_STREAMS=2 python tools/bench_fastcdc_e2e.py --dir /dev/shm/oxh_c5 --files 16 --gib 8 --chunk 8192 --reps 3 --keep --cpu none
+step shm_cs1b 900 env OXH_TRACE=1 OXH_CDC_COPY_STREAMS=1 python tools/bench_fastcdc_e2e.py --dir /dev/shm/oxh_c5 --files 16 --gib 8 --chunk 8192 --reps 3 --keep --cpu none
+step shm_cs2b 900 env OXH_TRACE=1 OXH_CDC_COPY_STREAMS=2 python tools/bench_fastcdc_e2e.py --dir /dev/shm/oxh_c5 --files 16 --gib 8 --chunk 8192 --reps 3 --cpu none
+step largetests 600 python -u -m pytest tests/test_gpu_large_items.py tests/test_gpu_publish.py tests/test_gpu_parity.py -m gpu -q --timeout 300 --timeout-method thread -k "large or big or publish or nomem or oversize or piece"
+step big_w7 600 python tools/big_file_probe.py --files 2 --gib 4 --dir /tmp/oxh_big --reps 3
+step big_w1 600 env OXH_BIG_WINDOWS=1 python tools/big_file_probe.py --files 2 --gib 4 --dir /tmp/oxh_big --reps 3
+step big_w7b 600 python tools/big_file_probe.py --files 2 --gib 4 --dir /tmp/oxh_big --reps 3
+step big_w1b 600 env OXH_BIG_WINDOWS=1 python tools/big_file_probe.py --files 2 --gib 4 --dir /tmp/oxh_big --reps 3
+rm -rf /dev/shm/oxh_c5 /tmp/oxh_c5s /tmp/oxh_c5d /tmp/oxh_big
 echo "== done $(date +%T)"
