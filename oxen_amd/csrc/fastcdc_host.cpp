@@ -55,11 +55,12 @@ constexpr uint64_t kCdcBounce = 64ull << 20;  // one pinned bounce buffer (a win
 constexpr int kCdcMaxBounce = 16;
 // the ring: reads of the next windows run while earlier H2Ds drain (OXH_CDC_NBOUNCE, 2..16, default 8:
 // 47.7 vs 43.6 GiB/s for 4 on 16 x 1 GiB from the page cache, profiles/r05/r05a_e2e_*)
-// H2D copy streams the windows alternate over (OXH_CDC_COPY_STREAMS, 1 or 2; default 1)
+// H2D copy streams the windows alternate over (OXH_CDC_COPY_STREAMS, 1 or 2; default 2: C5 from the
+// page cache 2.57-2.64 s against 2.91-2.92 s with one, alternating on one box, profiles/r05/r05e_shm_cs*)
 int cdc_copy_streams() {
     static const int v = [] {
         const char* e = getenv("OXH_CDC_COPY_STREAMS");
-        return e && atoi(e) == 2 ? 2 : 1;
+        return e && atoi(e) == 1 ? 1 : 2;
     }();
     return v;
 }
