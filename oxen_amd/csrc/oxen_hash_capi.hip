@@ -257,6 +257,8 @@ int default_reader_threads() { return default_threads(); }
 struct oxh_ctx {
     int device = 0;
     hipStream_t stream = nullptr, copy_stream = nullptr;
+    hipStream_t copy_stream2 = nullptr;  // large items: every other bounce window's H2D (created on first use)
+    hipEvent_t ev_copy2_join = nullptr;  // copy_stream waits for copy_stream2's windows of a piece
     uint64_t stage_bytes = 0, max_items = 0;
     uint8_t* h_stage[NSLOT] = {};
     uint8_t* d_stage[NSLOT] = {};
@@ -766,6 +768,8 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
     }
     for (int b = 0; b < 2; ++b)
         if (!c->ev_piece_free[b]) HIP_TRY(hipEventCreateWithFlags(&c->ev_piece_free[b], hipEventDisableTiming));
+    if (!c->copy_stream2) HIP_TRY(hipStreamCreateWithFlags(&c->copy_stream2, hipStreamNonBlocking));
+    if (!c->ev_copy2_join) HIP_TRY(hipEventCreateWithFlags(&c->ev_copy2_join, hipEventDisableTiming));
     uint64_t* sums = nullptr;
     oxh::ScratchLease lease(c->stream);  // block sums of the two rounds in flight
     const uint64_t sums_per = (cap >> 10) * 8;
@@ -821,8 +825,11 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
             W.grp.wait();
             if (W.bad.load()) ok = false;
             if (!ok) return;
-            if (hipMemcpyAsync(d + W.o, c->h_bounce[W.bb], W.m, hipMemcpyHostToDevice, c->copy_stream) != hipSuccess ||
-                hipEventRecord(c->ev_bounce[W.bb], c->copy_stream) != hipSuccess) {
+            // windows alternate over two copy streams: two DMA queues keep the PCIe link busier (the
+            // FastCDC host pipeline measured 53.5 vs 47 GB/s)
+            hipStream_t cs = ((W.o / kBounce) & 1) ? c->copy_stream2 : c->copy_stream;
+            if (hipMemcpyAsync(d + W.o, c->h_bounce[W.bb], W.m, hipMemcpyHostToDevice, cs) != hipSuccess ||
+                hipEventRecord(c->ev_bounce[W.bb], cs) != hipSuccess) {
                 ok = false;
                 return;
             }
@@ -869,6 +876,10 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
             finish(*inflight.front());
             inflight.pop_front();
         }
+        // the piece's event is recorded on copy_stream: it waits for copy_stream2's windows first
+        if (ok && (hipEventRecord(c->ev_copy2_join, c->copy_stream2) != hipSuccess ||
+                   hipStreamWaitEvent(c->copy_stream, c->ev_copy2_join, 0) != hipSuccess))
+            ok = false;
         // no wait for the copies here: the piece's kernels wait for the copy stream through ev_copy,
         // and a bounce buffer is refilled only after its own H2D (ev_bounce), so the next piece's reads
         // overlap this piece's last copies
@@ -978,6 +989,7 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
     }
     // a failure mid-way: release what is still pinned
     if (hipStreamSynchronize(c->copy_stream) != hipSuccess && rc == OXH_OK) rc = fail(OXH_ERR_HIP, "large-item copy");
+    if (hipStreamSynchronize(c->copy_stream2) != hipSuccess && rc == OXH_OK) rc = fail(OXH_ERR_HIP, "large-item copy");
     for (int q = 0; q < n; ++q) {
         if (pinned[q]) jobs[q].src->unpin(pinned[q]);
         if (next_pin[q]) jobs[q].src->unpin(next_pin[q]);
@@ -1144,6 +1156,11 @@ int oxh_ctx_destroy(oxh_ctx* c) {
         if (c->ev_piece_free[b]) (void)hipEventDestroy(c->ev_piece_free[b]);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+    if (c->copy_stream2) {
+        (void)hipStreamSynchronize(c->copy_stream2);
+        (void)hipStreamDestroy(c->copy_stream2);
+    }
+    if (c->ev_copy2_join) (void)hipEventDestroy(c->ev_copy2_join);
     delete c->pool;
     delete c->wpool;
     delete c->rpool;

@@ -509,3 +509,58 @@ def test_oracle_files_driver_matches_buffers(oracle_lib, tmp_path):
             dig = oracle_lib.batch(d, want[:, 0], want[:, 1]) if len(want) else np.zeros((0, 2), np.uint64)
             assert int(counts[i]) == len(want)
             assert (int(fp[i, 0]), int(fp[i, 1])) == F.record_fingerprint(want[:, 0], want[:, 1], dig)
+
+
+@pytest.mark.gpu
+def test_fastcdc_host_entries_concurrent(cuda, oracle_lib, tmp_path, monkeypatch):
+    """Three callers at once on one device: oxh_fastcdc_files on one context, oxh_fastcdc_host on a second
+    (each with its own piece pipeline; the device's two scratch buffers are shared by lease), and
+    oxh_hash_files on the process's default context's engine -- every result equal to the oracle's,
+    three rounds each. Small pieces (32 MiB) make every call cross piece boundaries."""
+    import threading
+
+    from oxen_amd import _capi, dedup, hasher
+
+    monkeypatch.setenv("OXH_CDC_PIECE_MIB", "32")
+    rng = np.random.default_rng(33)
+    datas = [rng.integers(0, 256, s, dtype=np.uint8) for s in (70_000_001, 5_000_000, 123_457, 0, 40_000_000)]
+    paths = []
+    for i, d in enumerate(datas):
+        p = tmp_path / f"c{i}"
+        p.write_bytes(d.tobytes())
+        paths.append(str(p))
+    errs = []
+
+    def files_worker():
+        try:
+            with _capi.Context(0) as c:
+                for _ in range(3):
+                    _check_table(oracle_lib, dedup.fastcdc_files(paths, 4096, 8192, 16384, ctx=c), datas, 4096, 8192, 16384)
+        except Exception as e:  # noqa: BLE001
+            errs.append(("files", repr(e)))
+
+    def host_worker():
+        try:
+            with _capi.Context(0) as c:
+                for _ in range(3):
+                    _check_table(oracle_lib, dedup.fastcdc_host(datas, 4096, 65536, 131072, ctx=c), datas, 4096, 65536, 131072)
+        except Exception as e:  # noqa: BLE001
+            errs.append(("host", repr(e)))
+
+    def hash_worker():
+        try:
+            from oracle import oracle
+
+            want = [oracle.xxh3_128_int(d.tobytes()) for d in datas]
+            for _ in range(3):
+                got, sizes, status = hasher.hash_files_128bit(paths)
+                assert status == [0] * len(paths) and got == want
+        except Exception as e:  # noqa: BLE001
+            errs.append(("hash", repr(e)))
+
+    ts = [threading.Thread(target=f) for f in (files_worker, host_worker, hash_worker)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(600)
+    assert not errs, errs
