@@ -75,6 +75,9 @@ int cdc_nbounce() {
 constexpr uint64_t kCdcPart = 4ull << 20;     // one reader task
 constexpr uint64_t kCdcAlign = 256;           // segment placement in a piece
 constexpr uint64_t kProbeWindow = 256;        // files opened (and stat'ed) ahead of the planner
+// files per round: every planned file holds its descriptor until its last segment is read, so a piece
+// of many small files must not need more than a process's descriptor limit (often 1024-20000)
+constexpr size_t kMaxSegsPerRound = 2048;
 
 inline uint64_t align_up(uint64_t x) { return (x + kCdcAlign - 1) & ~(kCdcAlign - 1); }
 
@@ -560,7 +563,7 @@ int run(oxh_ctx* ctx, CdcSource& src, uint64_t n, uint32_t mn, uint32_t av, uint
         // plan: files in order into this piece; a file that does not fit whole takes the rest of the
         // piece (if at least min_seg) and continues in the next round from `max` before its end
         uint64_t off = 0;
-        while (cur < n) {
+        while (cur < n && R.segs.size() < kMaxSegsPerRound) {
             if (cur >= probed) probe_to(cur + kProbeWindow);
             FileState& F = C.files[cur];
             if (F.status.load() != OXH_OK || F.size == 0) {  // no (more) chunks: an error, or an empty file

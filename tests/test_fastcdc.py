@@ -564,3 +564,22 @@ def test_fastcdc_host_entries_concurrent(cuda, oracle_lib, tmp_path, monkeypatch
     for t in ts:
         t.join(600)
     assert not errs, errs
+
+
+@pytest.mark.gpu
+def test_fastcdc_files_many_small(cuda, oracle_lib, tmp_path):
+    """5 000 small files in one call (more than a round's 2 048 files, each holding a descriptor until it
+    is read): every file chunked exactly, in order, no descriptor exhaustion."""
+    from oxen_amd import dedup
+
+    rng = np.random.default_rng(5000)
+    datas, paths = [], []
+    for i in range(5000):
+        d = rng.integers(0, 256, int(rng.integers(0, 40_000)), dtype=np.uint8)
+        p = tmp_path / f"s{i:05d}"
+        p.write_bytes(d.tobytes())
+        datas.append(d)
+        paths.append(str(p))
+    tab = dedup.fastcdc_files(paths, 4096, 8192, 16384)
+    assert (tab.status == 0).all()
+    _check_table(oracle_lib, tab, datas, 4096, 8192, 16384)
