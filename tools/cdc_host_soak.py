@@ -40,6 +40,7 @@ def main():
     t_end = time.time() + a.seconds
     it = files_checked = chunks_checked = bytes_checked = 0
     failures = []
+    last = time.time()
     while time.time() < t_end:
         mn, av, mx = PARAMS[int(rng.integers(len(PARAMS)))]
         piece = int(rng.choice([32, 48, 64, 256, 1024]))
@@ -93,6 +94,10 @@ def main():
             chunks_checked += len(want)
             bytes_checked += int(d.size)
         it += 1
+        if time.time() - last >= 20:  # progress (a silent GPU command is taken for a hung one)
+            print(f"[soak] {it} iterations, {files_checked} files, {chunks_checked} chunks, {len(failures)} failures",
+                  file=sys.stderr, flush=True)
+            last = time.time()
     shutil.rmtree(a.dir, ignore_errors=True)
     print(json.dumps({"iterations": it, "files_checked": files_checked, "chunks_checked": chunks_checked,
                       "bytes_checked": bytes_checked, "failures": failures[:20], "n_failures": len(failures)}),
