@@ -583,3 +583,18 @@ def test_fastcdc_files_many_small(cuda, oracle_lib, tmp_path):
     tab = dedup.fastcdc_files(paths, 4096, 8192, 16384)
     assert (tab.status == 0).all()
     _check_table(oracle_lib, tab, datas, 4096, 8192, 16384)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("level", [0, 1, 2, 3])
+def test_fastcdc_host_levels(cuda, oracle_lib, monkeypatch, level):
+    """The normalization levels (v2020::FastCDC::with_level, Level0..Level3: MASKS[bits +/- level])
+    through the host entry, files split over 32 MiB pieces."""
+    from oxen_amd import dedup
+
+    monkeypatch.setenv("OXH_CDC_PIECE_MIB", "32")
+    rng = np.random.default_rng(100 + level)
+    datas = [rng.integers(0, 256, s, dtype=np.uint8) for s in (45_000_003, 9_999, 0, 4096)]
+    for mn, av, mx in [(4096, 8192, 16384), (4096, 65536, 131072)]:
+        tab = dedup.fastcdc_host(datas, mn, av, mx, level=level)
+        _check_table(oracle_lib, tab, datas, mn, av, mx, level=level)
