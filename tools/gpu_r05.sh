@@ -55,6 +55,8 @@ step big_w1 600 env OXH_BIG_WINDOWS=1 python tools/big_file_probe.py --files 2 -
 step big_w7b 600 python tools/big_file_probe.py --files 2 --gib 4 --dir /tmp/oxh_big --reps 3
 step big_w1b 600 env OXH_BIG_WINDOWS=1 python tools/big_file_probe.py --files 2 --gib 4 --dir /tmp/oxh_big --reps 3
 step concurrent 600 python -u -m pytest tests/test_fastcdc.py -m gpu -q --timeout 500 --timeout-method thread -k concurrent
+step comm2 240 env NCCL_DEBUG=WARN python tools/comm_two_ranks.py --world 2
+step levels 600 python -u -m pytest tests/test_fastcdc.py -m gpu -q --timeout 300 --timeout-method thread -k "levels or many_small"
 step cdcsoak 400 python tools/cdc_host_soak.py --seconds 240
 rm -rf /dev/shm/oxh_c5 /tmp/oxh_c5s /tmp/oxh_c5d /tmp/oxh_big
 echo "== done $(date +%T)"
