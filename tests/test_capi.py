@@ -105,3 +105,15 @@ def test_comm_argument_checks_without_device(built_lib):
     if not torch.cuda.is_available():
         assert L.oxh_comm_create(uid, 0, 1, 0, ctypes.byref(h)) == _capi.OXH_ERR_NODEVICE
         assert not h.value
+
+
+def test_header_compiles_standalone_as_c_and_cpp(tmp_path):
+    """include/oxen_hash.h is what a cgo / bindgen / plain-C caller includes: it must stand alone as C99
+    (no C++ or HIP types) and as C++17, warning-free."""
+    import os
+
+    hdr = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "oxen_hash.h")
+    for lang, std in (("c", "-std=c99"), ("c++", "-std=c++17")):
+        r = subprocess.run(["gcc" if lang == "c" else "g++", std, "-Wall", "-Wextra", "-pedantic", "-Werror",
+                            "-fsyntax-only", "-x", lang, hdr], capture_output=True, text=True)
+        assert r.returncode == 0, (lang, r.stderr)
