@@ -312,6 +312,20 @@ int oxh_fastcdc_host(oxh_ctx* ctx, const uint8_t* const* bufs, const uint64_t* l
                      uint64_t* digests, uint64_t capacity, uint64_t* first_chunk);
 /* Upper bound on the chunk count of files of these lengths (every chunk but a file's last is >= min). */
 uint64_t oxh_fastcdc_max_chunks(const uint64_t* lens, uint64_t n, uint32_t min_size);
+/* Fixed-size chunk digests from host memory to host memory: the block-level dedup's fixed-size
+ * chunkers (fixedsize_multithreaded.rs:78-110 -- chunk i = [i*chunk_size, min((i+1)*chunk_size, size)),
+ * xxh3_128 of each -- and fixedsize.rs:67-91, which reads the same chunks through a BufReader) over n
+ * files (oxh_chunk_digests_files) or n host buffers (oxh_chunk_digests_host), through the same pipeline
+ * as oxh_fastcdc_files (segments of whole chunks, so nothing is carried between them). File i's
+ * chunks are first_chunk[i] .. first_chunk[i+1]-1 (n+1 entries), digests[2k..2k+1] = XXH3-128 (lo, hi)
+ * of chunk k; an empty file has none. Errors per file as oxh_fastcdc_files. `capacity` entries of
+ * `digests`; the count needed is sum(ceil(size_i / chunk_size)) (more fails with OXH_ERR_INVALID,
+ * "need N entries"). chunk_size 0 -> OXH_ERR_INVALID ("Chunk size cannot be zero", fixedsize.rs:43-47);
+ * chunk_size is at most 3 GiB - 64 MiB (a chunk fits one device piece). */
+int oxh_chunk_digests_files(oxh_ctx* ctx, const char* const* paths, uint64_t n, uint64_t chunk_size, uint64_t* digests,
+                            uint64_t capacity, uint64_t* first_chunk, uint64_t* sizes, int32_t* status, int32_t* os_error);
+int oxh_chunk_digests_host(oxh_ctx* ctx, const uint8_t* const* bufs, const uint64_t* lens, uint64_t n,
+                           uint64_t chunk_size, uint64_t* digests, uint64_t capacity, uint64_t* first_chunk);
 /* The compiled-in GEAR table (256 u64) and the (mask_s, mask_l) pair for an average size and
  * normalization level (fastcdc v2020 MASKS[bits +/- level], bits = round(log2(avg))). Host only. */
 int oxh_fastcdc_gear(uint64_t* out256);

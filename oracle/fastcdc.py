@@ -135,6 +135,24 @@ def files(paths, min_size: int, avg: int, max_size: int, level: int = 1, threads
     return counts, fp, status
 
 
+def fixed_files(paths, chunk: int, threads: int = 1, mmap_files: bool = False):
+    """C oracle over files (oxo_fixed_files): fixedsize_multithreaded.rs:78-110 per file -- chunk i =
+    [i*chunk, min((i+1)*chunk, size)), xxh3_128 of each -- `threads` files at a time; returns as files()."""
+    L = _lib()
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    L.oxo_fixed_files.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
+                                  ctypes.c_int, u64p, u64p, ctypes.POINTER(ctypes.c_int32)]
+    L.oxo_fixed_files.restype = None
+    n = len(paths)
+    arr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
+    counts = np.zeros(n, dtype=np.uint64)
+    fp = np.zeros((n, 2), dtype=np.uint64)
+    status = np.zeros(n, dtype=np.int32)
+    L.oxo_fixed_files(arr, n, int(chunk), 1 if mmap_files else 0, int(threads), counts.ctypes.data_as(u64p),
+                      fp.ctypes.data_as(u64p), status.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    return counts, fp, status
+
+
 def record_fingerprint(offsets, lens, digests) -> tuple[int, int]:
     """XXH3-128 (lo, hi) of a chunk table's (offset, length, lo, hi) u64 LE records -- what
     oxo_fastcdc_files reports per file -- for comparing a GPU table against the C oracle at full size."""

@@ -130,6 +130,7 @@ typedef struct {
     u32 min, avg, max, level;
     const u64* gear;
     int mode;
+    u64 fixed;  /* > 0: fixed-size chunks of this many bytes instead of FastCDC */
     u64* counts;
     u64* fp;
     int32_t* status;
@@ -160,14 +161,15 @@ static int cdc_one_file(cdc_files_job* j, u64 i) {
         }
     }
     close(fd);
-    u64 m[2];
-    oxo_fastcdc_masks(j->avg, j->level, m);
-    const u64 cap = sz / (j->min ? j->min : 1) + 2;
+    u64 m[2] = {0, 0};
+    if (!j->fixed) oxo_fastcdc_masks(j->avg, j->level, m);
+    const u64 cap = sz / (j->fixed ? j->fixed : j->min ? j->min : 1) + 2;
     u64* rec = (u64*)malloc(cap * 4 * sizeof(u64));
     if (!rec) { if (mapped) munmap(buf, sz); else free(buf); return 3; }
     u64 processed = 0, k = 0;
     while (processed < sz) {
-        const u64 cut = cut_gear(buf + processed, sz - processed, j->min, j->avg, j->max, m[0], m[1], j->gear);
+        const u64 cut = j->fixed ? (sz - processed < j->fixed ? sz - processed : j->fixed)
+                                 : cut_gear(buf + processed, sz - processed, j->min, j->avg, j->max, m[0], m[1], j->gear);
         if (cut == 0 || k >= cap) break;
         u64 d[2];
         oxo_xxh3_128(buf + processed, cut, d);
@@ -202,6 +204,22 @@ void oxo_fastcdc_files(const char* const* paths, u64 n, u32 min, u32 avg, u32 ma
     cdc_files_job j;
     memset(&j, 0, sizeof j);
     j.paths = paths, j.n = n, j.min = min, j.avg = avg, j.max = max, j.level = level, j.gear = gear, j.mode = mode;
+    j.counts = counts, j.fp = fp, j.status = status;
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    for (int t = 1; t < nthreads; ++t) pthread_create(&th[t], NULL, cdc_files_worker, &j);
+    cdc_files_worker(&j);
+    for (int t = 1; t < nthreads; ++t) pthread_join(th[t], NULL);
+}
+
+/* fixedsize_multithreaded.rs:78-110 per file: chunk i = [i*chunk, min((i+1)*chunk, size)), xxh3_128 of
+ * each; the same per-file records / fingerprint as oxo_fastcdc_files. */
+void oxo_fixed_files(const char* const* paths, u64 n, u64 chunk, int mode, int nthreads, u64* counts, u64* fp,
+                     int32_t* status) {
+    cdc_files_job j;
+    memset(&j, 0, sizeof j);
+    j.paths = paths, j.n = n, j.fixed = chunk ? chunk : 1, j.mode = mode;
     j.counts = counts, j.fp = fp, j.status = status;
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;

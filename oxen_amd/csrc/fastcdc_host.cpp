@@ -291,6 +291,7 @@ struct Call {
     CdcSource* src;
     uint64_t n;
     uint32_t mn, av, mx, lv;
+    uint64_t fixed = 0;  // fixed-size chunking (oxh_chunk_digests_files / _host): the chunk size; 0 = FastCDC
     uint64_t* c_off;
     uint64_t* c_len;
     uint64_t* dig;
@@ -356,6 +357,67 @@ void stitch(Call& C, const Round& R, const std::vector<uint64_t>& first, const s
     }
 }
 
+// Fixed-size chunking of one round: every segment starts at a multiple of the chunk size in its file,
+// so its chunks are [poff + k*chunk, + min(chunk, rest)) of the piece. One K1 launch over the round's
+// chunk descriptors, the digests come back, and they are appended per file. false = the call failed.
+bool fixed_round(Call& C, const Round& R) {
+    CdcHost& h = *C.h;
+    const uint64_t ck = C.fixed;
+    std::vector<uint64_t> first(R.segs.size() + 1, 0);
+    for (size_t j = 0; j < R.segs.size(); ++j) {
+        const Seg& s = R.segs[j];
+        const bool ok = C.files[s.file].status.load() == OXH_OK;
+        first[j + 1] = first[j] + (ok ? (s.hi - s.lo + ck - 1) / ck : 0);
+    }
+    const uint64_t m = first.back();
+    int rc = h.tables(m);
+    for (size_t j = 0; rc == OXH_OK && j < R.segs.size(); ++j) {
+        const Seg& s = R.segs[j];
+        for (uint64_t k = first[j], o = s.lo; k < first[j + 1]; ++k, o += ck) {
+            h.h_off[k] = s.poff + (o - s.lo);
+            h.h_len[k] = std::min(ck, s.hi - o);
+        }
+    }
+    if (rc == OXH_OK && m &&
+        (hipMemcpyAsync(h.d_off, h.h_off, m * 8, hipMemcpyHostToDevice, h.comp) != hipSuccess ||
+         hipMemcpyAsync(h.d_len, h.h_len, m * 8, hipMemcpyHostToDevice, h.comp) != hipSuccess))
+        rc = oxh::set_error(OXH_ERR_HIP, "chunk descriptors H2D");
+    if (rc == OXH_OK && (hipStreamWaitEvent(h.comp, h.ev_copied[R.b], 0) != hipSuccess ||
+                         (h.ncopy == 2 && hipStreamWaitEvent(h.comp, h.ev_copied2[R.b], 0) != hipSuccess)))
+        rc = oxh::set_error(OXH_ERR_HIP, "wait copies");
+    if (rc == OXH_OK && m)
+        rc = oxh_xxh3_128_batch_device(h.d_piece[R.b], h.d_off, h.d_len, m, h.d_dig,
+                                       ck <= 16384 ? OXH_MODE_WAVE_SHORT : OXH_MODE_WAVE, h.comp);
+    if (rc == OXH_OK && m && hipMemcpyAsync(h.h_dig, h.d_dig, m * 16, hipMemcpyDeviceToHost, h.comp) != hipSuccess)
+        rc = oxh::set_error(OXH_ERR_HIP, "digests D2H");
+    if (rc == OXH_OK && hipStreamSynchronize(h.comp) != hipSuccess) rc = oxh::set_error(OXH_ERR_HIP, "chunking stream");
+    if (rc != OXH_OK) {
+        C.fail(rc, oxh_last_error());
+        return false;
+    }
+    {
+        std::lock_guard<std::mutex> g(C.mu);
+        C.buf_busy[R.b] = false;
+    }
+    C.cv.notify_all();
+    for (size_t j = 0; j < R.segs.size(); ++j) {
+        const Seg& s = R.segs[j];
+        FileState& F = C.files[s.file];
+        if (s.first) F.first = C.total;
+        if (F.status.load() != OXH_OK) {  // a read of this file failed: drop what it emitted
+            C.total = F.first;
+        } else {
+            for (uint64_t k = first[j]; k < first[j + 1]; ++k, ++C.total)
+                if (C.total < C.capacity && C.dig) {
+                    C.dig[2 * C.total] = h.h_dig[2 * k];
+                    C.dig[2 * C.total + 1] = h.h_dig[2 * k + 1];
+                }
+        }
+        if (s.last) C.first_chunk[s.file + 1] = C.total;
+    }
+    return true;
+}
+
 // The chunking thread: rounds in order; each waits for its copies, is chunked on the device, its table
 // comes back, and its piece buffer is handed back to the planner.
 void chunk_rounds(Call& C) {
@@ -375,6 +437,11 @@ void chunk_rounds(Call& C) {
             C.ready.pop_front();
         }
         const double t0 = now();
+        if (C.fixed) {
+            if (!fixed_round(C, R)) return;
+            C.t_chunk += now() - t0;
+            continue;
+        }
         const size_t m = R.segs.size();
         offs.assign(m, 0), lens.assign(m, 0), item_off.assign(m, 0), first.assign(m + 1, 0);
         for (size_t j = 0; j < m; ++j) {
@@ -506,30 +573,47 @@ int upload_round(Call& C, const Round& R) {
     return rc;
 }
 
-int run(oxh_ctx* ctx, CdcSource& src, uint64_t n, uint32_t mn, uint32_t av, uint32_t mx, uint32_t lv, uint64_t* c_off,
-        uint64_t* c_len, uint64_t* dig, uint64_t capacity, uint64_t* first_chunk, uint64_t* sizes, int32_t* status,
-        int32_t* os_error) {
+// fixed-size chunks per round: bounds the descriptor / digest buffers (32 B a chunk) for tiny chunks
+constexpr uint64_t kMaxFixedChunksPerRound = 4ull << 20;
+// largest fixed chunk: a chunk must fit a piece, and pieces stop at 3 GiB
+constexpr uint64_t kMaxFixedChunk = (3ull << 30) - kCdcBounce;
+
+int run(oxh_ctx* ctx, CdcSource& src, uint64_t n, uint32_t mn, uint32_t av, uint32_t mx, uint32_t lv, uint64_t fixed,
+        uint64_t* c_off, uint64_t* c_len, uint64_t* dig, uint64_t capacity, uint64_t* first_chunk, uint64_t* sizes,
+        int32_t* status, int32_t* os_error) {
     if (!ctx) return oxh::set_error(OXH_ERR_INVALID, "null context");
     if (!first_chunk) return oxh::set_error(OXH_ERR_INVALID, "null first_chunk");
-    if (capacity && (!c_off || !c_len)) return oxh::set_error(OXH_ERR_INVALID, "null chunk table");
-    // the crate's asserts (v2020::FastCDC::with_level), checked before any I/O
-    uint64_t ms = 0, ml = 0;
-    if (mn < 64 || mn > 1048576) return oxh::set_error(OXH_ERR_INVALID, "min_size must be in [64, 1048576]");
-    if (mx < 1024 || mx > 16777216) return oxh::set_error(OXH_ERR_INVALID, "max_size must be in [1024, 16777216]");
-    if (int rc = oxh_fastcdc_masks(av, lv, &ms, &ml)) return rc;
+    if (capacity && !fixed && (!c_off || !c_len)) return oxh::set_error(OXH_ERR_INVALID, "null chunk table");
+    if (capacity && fixed && !dig) return oxh::set_error(OXH_ERR_INVALID, "null digests");
+    uint64_t min_seg = 0;
+    if (fixed) {
+        if (fixed > kMaxFixedChunk) return oxh::set_error(OXH_ERR_INVALID, "chunk_size above 3 GiB - 64 MiB");
+        // a segment is whole chunks: at least one, and 16 MiB when the chunks are smaller (within the
+        // round's chunk budget)
+        min_seg = fixed * std::max<uint64_t>(1, std::min<uint64_t>((16ull << 20) / fixed, kMaxFixedChunksPerRound));
+    } else {
+        // the crate's asserts (v2020::FastCDC::with_level), checked before any I/O
+        uint64_t ms = 0, ml = 0;
+        if (mn < 64 || mn > 1048576) return oxh::set_error(OXH_ERR_INVALID, "min_size must be in [64, 1048576]");
+        if (mx < 1024 || mx > 16777216) return oxh::set_error(OXH_ERR_INVALID, "max_size must be in [1024, 16777216]");
+        if (int rc = oxh_fastcdc_masks(av, lv, &ms, &ml)) return rc;
+        // a segment is at least 16 MiB and 4 max chunks
+        min_seg = std::max<uint64_t>(16ull << 20, 4ull * mx + kCdcAlign);
+    }
     std::lock_guard<std::mutex> call_lock(oxh::ctx_call_mutex(ctx));
     (void)hipSetDevice(oxh::ctx_device(ctx));
-    // pieces of OXH_CDC_PIECE_MIB (default 1 GiB); a segment is at least 16 MiB and 4 max chunks
+    // pieces of OXH_CDC_PIECE_MIB (default 1 GiB), at least two minimal segments (one for a fixed chunk
+    // size above 1 GiB)
     const char* pe = getenv("OXH_CDC_PIECE_MIB");
-    const uint64_t min_seg = std::max<uint64_t>(16ull << 20, 4ull * mx + kCdcAlign);
     uint64_t piece = (pe && atoll(pe) > 0 ? (uint64_t)atoll(pe) : 1024ull) << 20;
-    piece = std::min<uint64_t>(std::max<uint64_t>(piece, 2 * min_seg), 3ull << 30);
+    piece = std::max<uint64_t>(piece, fixed > (1ull << 30) ? min_seg + kCdcAlign : 2 * min_seg);
+    piece = std::min<uint64_t>(piece, 3ull << 30);
     piece = (piece + kCdcBounce - 1) / kCdcBounce * kCdcBounce;
     CdcHost* h = nullptr;
     if (int rc = cdc_host(ctx, piece, &h)) return rc;
 
     Call C;
-    C.h = h, C.src = &src, C.n = n, C.mn = mn, C.av = av, C.mx = mx, C.lv = lv;
+    C.h = h, C.src = &src, C.n = n, C.mn = mn, C.av = av, C.mx = mx, C.lv = lv, C.fixed = fixed;
     C.c_off = c_off, C.c_len = c_len, C.dig = dig, C.capacity = capacity, C.first_chunk = first_chunk;
     C.files = std::vector<FileState>(n);
     first_chunk[0] = 0;
@@ -562,7 +646,7 @@ int run(oxh_ctx* ctx, CdcSource& src, uint64_t n, uint32_t mn, uint32_t av, uint
         R.b = round_no & 1;
         // plan: files in order into this piece; a file that does not fit whole takes the rest of the
         // piece (if at least min_seg) and continues in the next round from `max` before its end
-        uint64_t off = 0;
+        uint64_t off = 0, nchunks = 0;  // (nchunks: fixed-size chunks planned this round)
         while (cur < n && R.segs.size() < kMaxSegsPerRound) {
             if (cur >= probed) probe_to(cur + kProbeWindow);
             FileState& F = C.files[cur];
@@ -575,7 +659,25 @@ int run(oxh_ctx* ctx, CdcSource& src, uint64_t n, uint32_t mn, uint32_t av, uint
             }
             const uint64_t lo = F.next_lo, left = F.size - lo;
             const uint64_t at = align_up(off);
-            const uint64_t room = at < piece ? piece - at : 0;
+            uint64_t room = at < piece ? piece - at : 0;
+            if (fixed) {  // whole chunks, and the round's chunk budget
+                room = std::min(room, (kMaxFixedChunksPerRound - nchunks) * fixed);
+                if (left <= room) {
+                    R.segs.push_back({cur, lo, F.size, at, lo == 0, true});
+                    ++F.segs_left;
+                    off = at + left;
+                    nchunks += (left + fixed - 1) / fixed;
+                    ++cur;
+                    continue;
+                }
+                const uint64_t take = room / fixed * fixed;
+                if (take >= min_seg) {  // the next segment starts where this one ends: no chunk straddles
+                    R.segs.push_back({cur, lo, lo + take, at, lo == 0, false});
+                    ++F.segs_left;
+                    F.next_lo = lo + take;
+                }
+                break;
+            }
             if (left <= room) {
                 R.segs.push_back({cur, lo, F.size, at, lo == 0, true});
                 ++F.segs_left;
@@ -654,7 +756,7 @@ int oxh_fastcdc_files(oxh_ctx* ctx, const char* const* paths, uint64_t n, uint32
     for (uint64_t i = 0; i < n; ++i)
         if (!paths[i]) return oxh::set_error(OXH_ERR_INVALID, "null path");
     FileSrc src(paths, n);
-    return run(ctx, src, n, min_size, avg_size, max_size, level, chunk_offsets, chunk_lens, digests, capacity, first_chunk,
+    return run(ctx, src, n, min_size, avg_size, max_size, level, 0, chunk_offsets, chunk_lens, digests, capacity, first_chunk,
                sizes, status, os_error);
 }
 
@@ -665,8 +767,33 @@ int oxh_fastcdc_host(oxh_ctx* ctx, const uint8_t* const* bufs, const uint64_t* l
     for (uint64_t i = 0; i < n; ++i)
         if (lens[i] && !bufs[i]) return oxh::set_error(OXH_ERR_INVALID, "null buffer");
     MemSrc src(bufs, lens);
-    return run(ctx, src, n, min_size, avg_size, max_size, level, chunk_offsets, chunk_lens, digests, capacity, first_chunk,
+    return run(ctx, src, n, min_size, avg_size, max_size, level, 0, chunk_offsets, chunk_lens, digests, capacity, first_chunk,
                nullptr, nullptr, nullptr);
+}
+
+// Fixed-size chunk digests from host memory: the block-level dedup's fixed-size chunkers
+// (fixedsize_multithreaded.rs:78-110: chunk i = [i*chunk, min((i+1)*chunk, size)), xxh3_128 of each;
+// fixedsize.rs:67-91 reads the same chunks through a BufReader) over n files or host buffers.
+int oxh_chunk_digests_files(oxh_ctx* ctx, const char* const* paths, uint64_t n, uint64_t chunk_size, uint64_t* digests,
+                            uint64_t capacity, uint64_t* first_chunk, uint64_t* sizes, int32_t* status, int32_t* os_error) {
+    if (chunk_size == 0) return oxh::set_error(OXH_ERR_INVALID, "Chunk size cannot be zero");
+    if (n && !paths) return oxh::set_error(OXH_ERR_INVALID, "null paths");
+    for (uint64_t i = 0; i < n; ++i)
+        if (!paths[i]) return oxh::set_error(OXH_ERR_INVALID, "null path");
+    FileSrc src(paths, n);
+    return run(ctx, src, n, 0, 0, 0, 0, chunk_size, nullptr, nullptr, digests, capacity, first_chunk, sizes, status,
+               os_error);
+}
+
+int oxh_chunk_digests_host(oxh_ctx* ctx, const uint8_t* const* bufs, const uint64_t* lens, uint64_t n,
+                           uint64_t chunk_size, uint64_t* digests, uint64_t capacity, uint64_t* first_chunk) {
+    if (chunk_size == 0) return oxh::set_error(OXH_ERR_INVALID, "Chunk size cannot be zero");
+    if (n && (!bufs || !lens)) return oxh::set_error(OXH_ERR_INVALID, "null buffers");
+    for (uint64_t i = 0; i < n; ++i)
+        if (lens[i] && !bufs[i]) return oxh::set_error(OXH_ERR_INVALID, "null buffer");
+    MemSrc src(bufs, lens);
+    return run(ctx, src, n, 0, 0, 0, 0, chunk_size, nullptr, nullptr, digests, capacity, first_chunk, nullptr, nullptr,
+               nullptr);
 }
 
 }  // extern "C"

@@ -213,6 +213,101 @@ def fastcdc_host(buffers, min_size: int, avg_size: int, max_size: int, level: in
     return FastCdcTable(off[:total], ln[:total], dig[:total] if dig is not None else None, first)
 
 
+class FixedChunkTable:
+    """Fixed-size chunk digests in host memory (oxh_chunk_digests_files / _host): digests[k] = (lo, hi)
+    of chunk k; file i's chunks are rows first[i] .. first[i+1]-1, chunk j of a file being its bytes
+    [j*chunk, min((j+1)*chunk, size)). sizes / status / os_error per file (files only)."""
+
+    def __init__(self, digests, first, sizes=None, status=None, os_error=None):
+        self.digests, self.first, self.sizes, self.status, self.os_error = digests, first, sizes, status, os_error
+
+    def file(self, i: int):
+        return self.digests[int(self.first[i]):int(self.first[i + 1])]
+
+
+def _fixed_count(sizes, chunk: int) -> int:
+    return int(sum((int(x) + chunk - 1) // chunk for x in sizes))
+
+
+def chunk_digests_files(paths, chunk_size: int, ctx: Optional[_capi.Context] = None) -> FixedChunkTable:
+    """oxh_chunk_digests_files: XXH3-128 of every fixed-size chunk of files on disk, read by the library
+    (fixedsize_multithreaded.rs:78-110), digests in host memory; per-file errors as fastcdc_files."""
+    from .hasher import _PathTable, default_context
+
+    if chunk_size <= 0:
+        raise _capi.OxenError("Chunk size cannot be zero", _capi.OXH_ERR_INVALID)
+    ctx = ctx or default_context()
+    n = len(paths)
+    hint = []
+    for p in paths:
+        try:
+            hint.append(os.stat(p).st_size)
+        except OSError:
+            hint.append(0)
+    cap = max(1, _fixed_count(hint, chunk_size))
+    table = _PathTable(paths) if n else None
+    L = _capi.lib()
+    for _ in range(3):  # a file that grew since the stat above: retry with the count the call reports
+        dig = np.zeros((cap, 2), dtype=np.uint64)
+        first = np.zeros(n + 1, dtype=np.uint64)
+        sizes = np.zeros(n, dtype=np.uint64)
+        status = np.zeros(n, dtype=np.int32)
+        oserr = np.zeros(n, dtype=np.int32)
+        rc = L.oxh_chunk_digests_files(ctx.handle, table.arg if table else None, n, int(chunk_size),
+                                       dig.ctypes.data_as(_capi._u64p), cap, first.ctypes.data_as(_capi._u64p),
+                                       sizes.ctypes.data_as(_capi._u64p), status.ctypes.data_as(_capi._i32p),
+                                       oserr.ctypes.data_as(_capi._i32p))
+        try:
+            _capi.check(rc, "oxh_chunk_digests_files")
+        except _capi.OxenError as e:
+            need = _need_from_error(e)
+            if need is None:
+                raise
+            cap = need
+            continue
+        return FixedChunkTable(dig[:int(first[n])], first, sizes, status, oserr)
+    raise _capi.OxenError("oxh_chunk_digests_files: the files keep growing", _capi.OXH_ERR_INVALID)
+
+
+def chunk_digests_host(buffers, chunk_size: int, ctx: Optional[_capi.Context] = None) -> FixedChunkTable:
+    """oxh_chunk_digests_host: the same over host buffers (bytes / numpy uint8 arrays)."""
+    from .hasher import default_context
+
+    if chunk_size <= 0:
+        raise _capi.OxenError("Chunk size cannot be zero", _capi.OXH_ERR_INVALID)
+    ctx = ctx or default_context()
+    arrs = [np.frombuffer(b, dtype=np.uint8) if isinstance(b, (bytes, bytearray, memoryview)) else np.ascontiguousarray(b, dtype=np.uint8)
+            for b in buffers]
+    n = len(arrs)
+    lens_in = np.array([a.size for a in arrs], dtype=np.uint64)
+    ptrs = (ctypes.c_char_p * max(n, 1))(*[ctypes.cast(a.ctypes.data, ctypes.c_char_p) if a.size else None for a in arrs])
+    cap = max(1, _fixed_count(lens_in, chunk_size))
+    dig = np.zeros((cap, 2), dtype=np.uint64)
+    first = np.zeros(n + 1, dtype=np.uint64)
+    _capi.check(_capi.lib().oxh_chunk_digests_host(ctx.handle, ptrs, lens_in.ctypes.data_as(_capi._u64p), n, int(chunk_size),
+                                                   dig.ctypes.data_as(_capi._u64p), cap, first.ctypes.data_as(_capi._u64p)),
+                "oxh_chunk_digests_host")
+    return FixedChunkTable(dig[:int(first[n])], first)
+
+
+# fixedsize.rs:67-91 reads through `BufReader::new(File)` (8 KiB buffer) and stops at the first read
+# shorter than chunk_size. BufReader::read serves a request from what is buffered (refilling with one
+# 8 KiB read when empty) unless the buffer is empty and the request is >= 8 KiB, which goes to the
+# file directly; Linux returns at most MAX_RW_COUNT (0x7ffff000) bytes from one read(2).
+BUFREADER_CAPACITY = 8192
+MAX_RW_COUNT = 0x7FFFF000
+
+
+def bufreader_prefix(size: int, chunk: int) -> int:
+    """Bytes of a `size`-byte regular file that fixedsize.rs's loop chunks (its chunks are then the
+    fixed-size chunks of that prefix): the whole file unless chunk < 8 KiB does not divide 8 KiB (the
+    read after the last whole chunk of the first buffer comes back short: the file stops at 8 KiB) or
+    chunk > MAX_RW_COUNT (the first read comes back short)."""
+    if chunk < BUFREADER_CAPACITY:
+        return min(size, BUFREADER_CAPACITY) if BUFREADER_CAPACITY % chunk else size
+    return min(size, MAX_RW_COUNT) if chunk > MAX_RW_COUNT else size
+
+
 class FastCDChunker:
     """fastcdchunker.rs:30-66 + the Chunker trait (chunker.rs): name / pack / unpack / get_chunk_hashes."""
 
@@ -279,9 +374,6 @@ class FastCDChunker:
         return decode_metadata(open(os.path.join(input_dir, METADATA_FILE_NAME), "rb").read())[2]
 
 
-SEGMENT_BYTES = 1 << 30  # bytes of a file on the device at a time (whole chunks)
-
-
 class _FixedSizeBase:
     """Shared by both fixed-size chunkers: a file -> its chunk names, chunks written as they are named."""
 
@@ -294,40 +386,49 @@ class _FixedSizeBase:
         self.concurrency = int(concurrency)
         self.device = device or "cuda"
 
+    def _prefix(self, size: int) -> int:
+        """Bytes of the file the reference chunks (all of them; FixedSizeChunker overrides)."""
+        return size
+
     def chunk_file(self, path: str, output_dir: str) -> list[str]:
         """Decimal xxh3_128 names of the file's chunks; a chunk file is written unless one of that
-        name exists (fixedsize.rs:78-89, fixedsize_multithreaded.rs:95-105)."""
+        name exists (fixedsize.rs:78-89, fixedsize_multithreaded.rs:95-105). The library reads the file
+        and returns the digests (oxh_chunk_digests_files); the chunk files are written from a read-only
+        map of it by `concurrency` threads."""
+        import errno as _errno
+        import mmap
         from concurrent.futures import ThreadPoolExecutor
 
-        from .device import chunk_digests_device
-
         size = os.stat(path).st_size
-        seg = max(self.chunk_size, SEGMENT_BYTES // self.chunk_size * self.chunk_size)
-        names: list[str] = []
-        host = torch.empty(min(seg, max(size, 1)), dtype=torch.uint8).pin_memory()
-        dev = torch.empty(host.numel(), dtype=torch.uint8, device=self.device)
-        hv = host.numpy()
-        with open(path, "rb", buffering=0) as fh, ThreadPoolExecutor(self.concurrency) as ex:
-            off = 0
-            while off < size:
-                n = min(seg, size - off)
-                got = fh.readinto(memoryview(hv)[:n])
-                if got != n:
-                    raise _capi.OxenError(f"short read of {path!r}", _capi.OXH_ERR_IO)
-                dev[:n].copy_(host[:n], non_blocking=True)
-                dig = to_numpy_u64(chunk_digests_device(dev, self.chunk_size, n)).reshape(-1, 2)
-                seg_names = [chunk_name(lo, hi) for lo, hi in dig.tolist()]
-
-                def write(k, seg_names=seg_names, n=n):
-                    p = os.path.join(output_dir, seg_names[k])
+        pre = self._prefix(size)
+        if pre == size:
+            tab = chunk_digests_files([path], self.chunk_size)
+            if int(tab.status[0]) != _capi.OXH_OK:  # File::open / read: the io::Error
+                e = int(tab.os_error[0]) or _errno.EIO
+                raise OSError(e, os.strerror(e), path)
+            size = int(tab.sizes[0])
+            dig = tab.digests
+        else:  # the reference's loop stops early: chunk the prefix it reads
+            with open(path, "rb") as fh:
+                head = fh.read(pre)
+            dig = chunk_digests_host([head], self.chunk_size).digests
+        names = [chunk_name(lo, hi) for lo, hi in dig.tolist()]
+        if not names:
+            return names
+        with open(path, "rb") as fh:
+            content = mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_READ)
+            try:
+                def write(k):
+                    p = os.path.join(output_dir, names[k])
                     if not os.path.exists(p):
                         lo = k * self.chunk_size
                         with open(p, "wb") as out:
-                            out.write(hv[lo:min(n, lo + self.chunk_size)].tobytes())
+                            out.write(content[lo:min(pre, lo + self.chunk_size)])
 
-                list(ex.map(write, range(len(seg_names))))
-                names += seg_names
-                off += n
+                with ThreadPoolExecutor(self.concurrency) as ex:
+                    list(ex.map(write, range(len(names))))
+            finally:
+                content.close()
         return names
 
 
@@ -340,6 +441,9 @@ class FixedSizeChunker(_FixedSizeBase):
 
     def name(self) -> str:
         return "fixed-size-chunker"
+
+    def _prefix(self, size: int) -> int:
+        return bufreader_prefix(size, self.chunk_size)
 
     def _file_entry(self, path: str, base: str, output_dir: str) -> dict:
         chunks = self.chunk_file(path, output_dir)

@@ -754,6 +754,65 @@ std::vector<std::vector<Chunk>> fastcdc_buffers(const std::vector<std::string_vi
     return split(first, off, len, dig);
 }
 
+std::vector<ChunkedFile> fixed_chunk_files(const std::vector<std::string>& paths, uint64_t chunk_size, oxh_ctx* ctx) {
+    ctx = ctx ? ctx : util::hasher::default_context();
+    const size_t n = paths.size();
+    std::vector<const char*> cp(n);
+    uint64_t cap = 1;
+    for (size_t i = 0; i < n; ++i) {
+        cp[i] = paths[i].c_str();
+        struct stat sb;
+        if (chunk_size && stat(cp[i], &sb) == 0) cap += ((uint64_t)sb.st_size + chunk_size - 1) / chunk_size;
+    }
+    for (int attempt = 0;; ++attempt) {
+        std::vector<uint64_t> dig(2 * cap), first(n + 1), sizes(n);
+        std::vector<int32_t> status(n), oserr(n);
+        const int rc = oxh_chunk_digests_files(ctx, cp.data(), n, chunk_size, dig.data(), cap, first.data(), sizes.data(),
+                                               status.data(), oserr.data());
+        if (rc == OXH_ERR_INVALID && attempt < 2) {  // a file grew since the stat: the text has the count
+            const std::string e = oxh_last_error();
+            const size_t at = e.find("need ");
+            if (at != std::string::npos) {
+                cap = std::stoull(e.substr(at + 5));
+                continue;
+            }
+        }
+        if (rc != OXH_OK) throw OxenError::basic_str(std::string("oxh_chunk_digests_files: ") + oxh_last_error(), rc);
+        std::vector<ChunkedFile> r(n);
+        for (size_t i = 0; i < n; ++i) {
+            r[i].ok = status[i] == OXH_OK;
+            r[i].size = sizes[i];
+            r[i].code = status[i];
+            r[i].os_error = oserr[i];
+            for (uint64_t k = first[i], o = 0; k < first[i + 1]; ++k, o += chunk_size)
+                r[i].chunks.push_back({o, std::min(chunk_size, sizes[i] - o), to_u128(dig[2 * k], dig[2 * k + 1])});
+        }
+        return r;
+    }
+}
+
+std::vector<std::vector<Chunk>> fixed_chunk_buffers(const std::vector<std::string_view>& buffers, uint64_t chunk_size,
+                                                    oxh_ctx* ctx) {
+    ctx = ctx ? ctx : util::hasher::default_context();
+    const size_t n = buffers.size();
+    std::vector<const uint8_t*> ptrs(n);
+    std::vector<uint64_t> lens(n);
+    uint64_t cap = 1;
+    for (size_t i = 0; i < n; ++i) {
+        ptrs[i] = reinterpret_cast<const uint8_t*>(buffers[i].data());
+        lens[i] = buffers[i].size();
+        if (chunk_size) cap += (lens[i] + chunk_size - 1) / chunk_size;
+    }
+    std::vector<uint64_t> dig(2 * cap), first(n + 1);
+    check(oxh_chunk_digests_host(ctx, ptrs.data(), lens.data(), n, chunk_size, dig.data(), cap, first.data()),
+          "oxh_chunk_digests_host");
+    std::vector<std::vector<Chunk>> r(n);
+    for (size_t i = 0; i < n; ++i)
+        for (uint64_t k = first[i], o = 0; k < first[i + 1]; ++k, o += chunk_size)
+            r[i].push_back({o, std::min(chunk_size, lens[i] - o), to_u128(dig[2 * k], dig[2 * k + 1])});
+    return r;
+}
+
 std::string chunk_name(u128 hash) {
     char b[48];
     oxh_format_dec((uint64_t)hash, (uint64_t)(hash >> 64), b);

@@ -504,6 +504,19 @@ static void dedup_chunks(const std::string& golden) {
     CHECK(hashes);
     CHECK(files[2].chunks[0].hash == hex("1bfd09d1a433fb78117b4c7b1583d16d"));
     CHECK(dd::chunk_name(files[2].chunks[0].hash) == "37203006142592822661058489871983956333");
+    // fixed-size chunks (fixedsize_multithreaded.rs:78-110) of the same files and buffers
+    const auto fx = dd::fixed_chunk_files({p_big, missing, hello}, 65536);
+    const auto fb = dd::fixed_chunk_buffers({std::string_view(big), std::string_view("hello")}, 65536);
+    CHECK(fx.size() == 3 && fx[0].ok && !fx[1].ok && fx[1].os_error == ENOENT && fx[2].ok);
+    CHECK(fx[0].chunks.size() == (big.size() + 65535) / 65536 && fb[0].size() == fx[0].chunks.size());
+    bool fixed_ok = true;
+    for (size_t k = 0; k < fx[0].chunks.size(); ++k) {
+        const auto& c = fx[0].chunks[k];
+        fixed_ok = fixed_ok && c.offset == 65536 * k && c.length == std::min<uint64_t>(65536, big.size() - c.offset) &&
+                   c.hash == fb[0][k].hash && c.hash == hasher::hash_buffer_128bit(big.data() + c.offset, c.length);
+    }
+    CHECK(fixed_ok);
+    CHECK(fx[2].chunks.size() == 1 && fx[2].chunks[0].hash == files[2].chunks[0].hash && fb[1][0].hash == fx[2].chunks[0].hash);
     const std::string rm = std::string("rm -rf ") + dir;
     if (system(rm.c_str()) != 0) fprintf(stderr, "could not remove %s\n", dir);
 }

@@ -37,11 +37,14 @@ def test_chunker_arguments():
         dedup.get_chunker("nope", 4096)
 
 
-def _ref_chunks(oracle_lib, data: bytes, chunk: int, out_dir: str) -> list[str]:
-    """fixedsize.rs:69-94 restated (read chunk_size at a time, name = u128 decimal, write if absent)."""
+def _ref_chunks(oracle_lib, data: bytes, chunk: int, out_dir: str, bufreader: bool = False) -> list[str]:
+    """fixedsize.rs:69-94 (bufreader: its BufReader read loop, oracle/fixedsize.reads) or
+    fixedsize_multithreaded.rs:78-110 (every chunk) restated: name = u128 decimal, write if absent."""
+    from oracle import fixedsize
+
     names = []
-    for lo in range(0, len(data), chunk):
-        piece = data[lo:lo + chunk]
+    for lo, n in (fixedsize.reads if bufreader else fixedsize.extents)(len(data), chunk):
+        piece = data[lo:lo + n]
         name = str(oracle_lib.xxh3_128_int(piece))
         names.append(name)
         p = os.path.join(out_dir, name)
@@ -63,8 +66,28 @@ def _tree(root, rng):
     return data
 
 
+def test_bufreader_prefix_matches_the_read_loop():
+    """dedup.bufreader_prefix (the product's closed form) against oracle/fixedsize.reads stepping
+    BufReader read by read: the reference chunks exactly the fixed-size chunks of that prefix."""
+    from oracle import fixedsize
+
+    from oxen_amd import dedup
+
+    sizes = [0, 1, 4095, 4096, 5000, 8191, 8192, 8193, 10_000, 16_384, 70_001, 1 << 20]
+    chunks = [1, 3, 1000, 3000, 4096, 5000, 8191, 8192, 8193, 10_000, 65_536]
+    for size in sizes:
+        for chunk in chunks:
+            got = fixedsize.reads(size, chunk)
+            pre = dedup.bufreader_prefix(size, chunk)
+            assert got == fixedsize.extents(pre, chunk), (size, chunk)
+    # chunks beyond one read(2): the first read comes back at MAX_RW_COUNT and the loop stops
+    for size, chunk in [(5 << 30, 3 << 30), (1 << 30, 3 << 30), (3 << 30, 0x7FFFF000), (3 << 30, 0x7FFFF001)]:
+        assert fixedsize.reads(size, chunk) == fixedsize.extents(dedup.bufreader_prefix(size, chunk), chunk)
+    assert dedup.bufreader_prefix(70_001, 5000) == 8192  # 5000 + a short 3192, then the loop ends
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("chunk", [4096, 8192, 65_536])
+@pytest.mark.parametrize("chunk", [4096, 5000, 8192, 65_536])
 def test_fixed_size_chunker_tree(cuda, oracle_lib, tmp_path, chunk):
     from oxen_amd import dedup
 
@@ -86,7 +109,7 @@ def test_fixed_size_chunker_tree(cuda, oracle_lib, tmp_path, chunk):
                     walk(e.path)
                 elif e.is_file():
                     b = open(e.path, "rb").read()
-                    entries.append({"path": rel, "is_dir": False, "chunks": _ref_chunks(oracle_lib, b, chunk, ref),
+                    entries.append({"path": rel, "is_dir": False, "chunks": _ref_chunks(oracle_lib, b, chunk, ref, True),
                                     "size": len(b)})
 
     walk(src)
@@ -100,17 +123,18 @@ def test_fixed_size_chunker_tree(cuda, oracle_lib, tmp_path, chunk):
     for dp, _, fns in os.walk(src):
         for fn in fns:
             rel = os.path.relpath(os.path.join(dp, fn), src)
-            assert open(os.path.join(back, rel), "rb").read() == open(os.path.join(src, rel), "rb").read()
+            b = open(os.path.join(src, rel), "rb").read()
+            # what the reference packed: all of the file, or the prefix its read loop reached
+            assert open(os.path.join(back, rel), "rb").read() == b[:dedup.bufreader_prefix(len(b), chunk)]
     assert os.path.isdir(os.path.join(back, "empty_dir"))
     assert dedup.FixedSizeChunker(chunk).get_chunk_hashes(out) == [c for e in entries if not e["is_dir"] for c in e["chunks"]]
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("size", [0, 1, 65_536, 65_536 * 5, 65_536 * 5 + 17, (3 << 20) + 1])
-def test_fixed_size_multi_chunker_file(cuda, oracle_lib, tmp_path, monkeypatch, size):
+def test_fixed_size_multi_chunker_file(cuda, oracle_lib, tmp_path, size):
     from oxen_amd import dedup
 
-    monkeypatch.setattr(dedup, "SEGMENT_BYTES", 1 << 20)  # several device segments per file
     data = np.random.default_rng(size).integers(0, 256, size, dtype=np.uint8).tobytes()
     p = tmp_path / "input.parquet"
     p.write_bytes(data)
@@ -130,3 +154,70 @@ def test_fixed_size_multi_chunker_file(cuda, oracle_lib, tmp_path, monkeypatch, 
             dedup.FixedSizeMultiChunker(65_536, 16).unpack(out, back)
     with pytest.raises(FileNotFoundError, match="Failed to read input file metadata"):
         dedup.FixedSizeMultiChunker(65_536, 16).pack(str(tmp_path / "missing"), out)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", [64, 4096, 5000, 65_536, (1 << 20) + 3, 40 << 20])
+def test_chunk_digests_files_segments(cuda, oracle_lib, tmp_path, monkeypatch, chunk):
+    """oxh_chunk_digests_files / _host over files that span several 64 MiB device pieces (segments of
+    whole chunks, none carried), ragged tails, an empty file, a missing one and a directory, against
+    the oracle's xxh3_128 of every chunk."""
+    from oracle import fixedsize
+
+    from oxen_amd import dedup
+
+    monkeypatch.setenv("OXH_CDC_PIECE_MIB", "64")
+    rng = np.random.default_rng(chunk)
+    sizes = [150_000_017, 0, 3, chunk, chunk * 7 + 1, 70_000_000, 5_000_001]
+    paths, blobs = [], []
+    for i, n in enumerate(sizes):
+        b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        p = tmp_path / f"f{i}.bin"
+        p.write_bytes(b)
+        paths.append(str(p))
+        blobs.append(b)
+    paths.insert(2, str(tmp_path / "missing"))
+    blobs.insert(2, None)
+    paths.insert(4, str(tmp_path))
+    blobs.insert(4, None)
+    t = dedup.chunk_digests_files(paths, chunk)
+    h = dedup.chunk_digests_host([b for b in blobs if b is not None], chunk)
+    k = 0
+    for i, b in enumerate(blobs):
+        got = t.file(i)
+        if b is None:
+            assert len(got) == 0 and int(t.status[i]) != 0
+            assert int(t.os_error[i]) in (2, 21)  # ENOENT, EISDIR
+            continue
+        assert int(t.status[i]) == 0 and int(t.sizes[i]) == len(b)
+        want = oracle_lib.chunk_digests(np.frombuffer(b, dtype=np.uint8), chunk, threads=8)
+        assert len(want) == len(fixedsize.extents(len(b), chunk))
+        assert np.array_equal(got, want), i
+        assert np.array_equal(h.file(k), want), i
+        k += 1
+
+
+@pytest.mark.gpu
+def test_chunk_digests_host_one_byte_chunks(cuda, oracle_lib):
+    """chunk_size 1 over 9 M bytes: more chunks than one round's budget (4 M), so rounds end on the
+    budget rather than the piece; every digest is the xxh3_128 of its byte."""
+    from oxen_amd import dedup
+
+    data = np.random.default_rng(1).integers(0, 256, 9_000_001, dtype=np.uint8)
+    t = dedup.chunk_digests_host([data, b"", b"xy"], 1)
+    table = np.array([oracle_lib.xxh3_128(bytes([v])) for v in range(256)], dtype=np.uint64).reshape(-1, 2)
+    assert list(t.first) == [0, data.size, data.size, data.size + 2]
+    assert np.array_equal(t.file(0), table[data])
+    assert np.array_equal(t.file(2), table[np.frombuffer(b"xy", dtype=np.uint8)])
+
+
+def test_chunk_digests_arguments():
+    """Argument errors before any device work (no GPU needed)."""
+    from oxen_amd import _capi, dedup
+
+    with pytest.raises(_capi.OxenError, match="Chunk size cannot be zero"):
+        dedup.chunk_digests_host([b"abc"], 0)
+    L = _capi.lib()
+    first = np.zeros(2, dtype=np.uint64)
+    rc = L.oxh_chunk_digests_host(None, None, None, 0, 0, None, 0, first.ctypes.data_as(_capi._u64p))
+    assert rc == _capi.OXH_ERR_INVALID and b"zero" in L.oxh_last_error()

@@ -2,7 +2,10 @@
 (BASELINE configs[4], experiments/block-level-dedup fastcdchunker.rs:75-98: fs::read -> v2020 ->
 xxh3_128 per chunk), through the C ABI's oxh_fastcdc_files. Prints one JSON object.
 
-    python tools/bench_fastcdc_e2e.py --dir /tmp/c5 --files 16 --gib 8 --chunk 8192 --reps 3 [--cold]
+    python tools/bench_fastcdc_e2e.py --dir /tmp/c5 --files 16 --gib 8 --chunk 8192 --reps 3 [--cold] [--fixed]
+
+--fixed: fixed-size chunks of --chunk bytes instead (fixedsize_multithreaded.rs:78-110, through
+oxh_chunk_digests_files; the oracle's oxo_fixed_files beside it).
 
 The files (splitmix64 bytes, seed 5000 + i) are written once (generated on the GPU, written through the
 page cache) and reused. Warm = every file in the page cache; cold = posix_fadvise(DONTNEED) on every file
@@ -96,6 +99,7 @@ def main():
     ap.add_argument("--cpu", choices=["read", "mmap", "none"], default="mmap",
                     help="the CPU baseline's file access: read() whole files (fs::read) or mmap")
     ap.add_argument("--keep", action="store_true", help="keep the files")
+    ap.add_argument("--fixed", action="store_true", help="fixed-size chunks of --chunk bytes instead of FastCDC")
     args = ap.parse_args()
 
     from oracle import fastcdc as F
@@ -111,18 +115,25 @@ def main():
     gen_s = time.perf_counter() - t0
     total = size * len(paths)
     ctx = _capi.Context(0)
-    res = {"workload": f"{len(paths)} x {size} B files on disk (splitmix64), FastCDC v2020 min {mn} avg {av} max {mx} "
+    what = (f"fixed-size {args.chunk} B chunks" if args.fixed else f"FastCDC v2020 min {mn} avg {av} max {mx}")
+    res = {"workload": f"{len(paths)} x {size} B files on disk (splitmix64), {what} "
                        f"+ XXH3-128 per chunk, chunk table + digests in host memory",
            "bytes": total, "gen_s": round(gen_s, 1), "host_threads": threads}
 
     def gpu_once():
         t = time.perf_counter()
-        tab = dedup.fastcdc_files(paths, mn, av, mx, ctx=ctx)
+        if args.fixed:
+            tab = dedup.chunk_digests_files(paths, args.chunk, ctx=ctx)
+        else:
+            tab = dedup.fastcdc_files(paths, mn, av, mx, ctx=ctx)
         return time.perf_counter() - t, tab
 
     def cpu_once():
         t = time.perf_counter()
-        c, fp, st = F.files(paths, mn, av, mx, threads=threads, mmap_files=args.cpu == "mmap")
+        if args.fixed:
+            c, fp, st = F.fixed_files(paths, args.chunk, threads=threads, mmap_files=args.cpu == "mmap")
+        else:
+            c, fp, st = F.files(paths, mn, av, mx, threads=threads, mmap_files=args.cpu == "mmap")
         return time.perf_counter() - t, (c, fp, st)
 
     warm_cache(paths, threads)
@@ -145,13 +156,21 @@ def main():
         c, fp, st = cres
         ok = bool((st == 0).all())
         for i in range(len(paths)):
-            off, ln, dig = tab.file(i)
+            if args.fixed:
+                dig = tab.file(i)
+                sz = int(tab.sizes[i])
+                off = np.arange(0, sz, args.chunk, dtype=np.uint64)
+                ln = np.minimum(np.uint64(args.chunk), np.uint64(sz) - off)
+            else:
+                off, ln, dig = tab.file(i)
             ok = ok and int(c[i]) == len(off) and (int(fp[i, 0]), int(fp[i, 1])) == F.record_fingerprint(off, ln, dig)
         res["all_chunks_bit_exact"] = ok
         res["cpu_warm_s"] = [round(x, 3) for x in ct]
         res["cpu_warm_gib_s"] = round(total / min(ct) / 2**30, 2)
         res["cpu"] = {"threads": threads, "kind": "port", "access": args.cpu,
-                      "what": "oracle/fastcdc_oracle.c oxo_fastcdc_files: per file read/mmap -> v2020 -> xxh3_128 per chunk"}
+                      "what": "oracle/fastcdc_oracle.c " + ("oxo_fixed_files: per file read/mmap -> xxh3_128 per fixed chunk"
+                                                            if args.fixed else
+                                                            "oxo_fastcdc_files: per file read/mmap -> v2020 -> xxh3_128 per chunk")}
     if args.cold:
         gc = []
         for _ in range(max(1, min(args.reps, 2))):

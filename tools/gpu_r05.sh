@@ -58,5 +58,9 @@ step concurrent 600 python -u -m pytest tests/test_fastcdc.py -m gpu -q --timeou
 step comm2 240 env NCCL_DEBUG=WARN python tools/comm_two_ranks.py --world 2
 step levels 600 python -u -m pytest tests/test_fastcdc.py -m gpu -q --timeout 300 --timeout-method thread -k "levels or many_small"
 step cdcsoak 400 python tools/cdc_host_soak.py --seconds 240
-rm -rf /dev/shm/oxh_c5 /tmp/oxh_c5s /tmp/oxh_c5d /tmp/oxh_big
+step fixed 600 python -u -m pytest tests/test_dedup_fixed.py tests/test_native_mirror.py -m gpu -v --timeout 300 --timeout-method thread
+step fixed_e2e_small 600 env OXH_TRACE=1 python tools/bench_fastcdc_e2e.py --fixed --dir /tmp/oxh_fx --files 16 --gib 1 --chunk 65536 --reps 3
+step fixed_e2e_shm 900 env OXH_TRACE=1 python tools/bench_fastcdc_e2e.py --fixed --dir /dev/shm/oxh_c5 --files 16 --gib 8 --chunk 65536 --reps 3 --keep
+step fixed_e2e_shm4k 900 env OXH_TRACE=1 python tools/bench_fastcdc_e2e.py --fixed --dir /dev/shm/oxh_c5 --files 16 --gib 8 --chunk 4096 --reps 3 --keep
+rm -rf /dev/shm/oxh_c5 /tmp/oxh_c5s /tmp/oxh_c5d /tmp/oxh_big /tmp/oxh_fx
 echo "== done $(date +%T)"
