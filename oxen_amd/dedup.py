@@ -361,8 +361,14 @@ class FastCDChunker:
         return output_dir
 
     def unpack(self, input_dir: str, output_path: str) -> str:
-        """The reference leaves this unimplemented (fastcdchunker.rs:124-127); here: concatenate the
-        chunks listed in metadata.bin."""
+        """fastcdchunker.rs:123-126: the reference's unpack is a stub -- it prints and returns
+        output_path without writing anything (so its `Test` command fails to hash the unpacked file).
+        Kept as such; `restore` is the working inverse."""
+        print(f"To Implement: Unpacking files from {input_dir!r}")
+        return output_path
+
+    def restore(self, input_dir: str, output_path: str) -> str:
+        """Not in the reference: concatenate the chunks listed in metadata.bin into output_path."""
         _, _, chunks = decode_metadata(open(os.path.join(input_dir, METADATA_FILE_NAME), "rb").read())
         with open(output_path, "wb") as out:
             for c in chunks:
@@ -555,3 +561,52 @@ def fastcdc_masks(avg_size: int, level: int = 1) -> tuple[int, int]:
     _capi.check(_capi.lib().oxh_fastcdc_masks(int(avg_size), int(level), s.ctypes.data_as(_capi._u64p),
                                               l.ctypes.data_as(_capi._u64p)), "oxh_fastcdc_masks")
     return int(s[0]), int(l[0])
+
+
+def hash_file_128bit(path) -> int:
+    """xhash.rs:6-20: File::open, 8 KiB BufReader reads into Xxh3, digest128 -- the XXH3-128 of the
+    whole file, here read and hashed by the library (oxh_hash_files_ex). The io::Error of the open /
+    read comes back as OSError."""
+    import errno as _errno
+
+    from .hasher import hash_files_with_errors_128bit
+
+    digests, _, status, oserr = hash_files_with_errors_128bit([os.fspath(path)])
+    if status[0] != _capi.OXH_OK:
+        e = int(oserr[0]) or _errno.EIO
+        raise OSError(e, os.strerror(e), os.fspath(path))
+    return int(digests[0])
+
+
+class VerificationFailed(Exception):
+    """FrameworkError::VerificationFailed (main.rs:232-234)."""
+
+
+def run_chunker_test(algorithm: str, chunk_size: int, input_file: str, base_dir: Optional[str] = None) -> dict:
+    """main.rs:156-241, `Commands::Test`: pack input_file into base_dir/chunker_test_<ns>, unpack it to
+    <that dir>/unpacked_output, time both, then compare hash_file_128bit of the original and of the
+    unpacked file (VerificationFailed when they differ; a failed hash is "Failed to hash ... file")."""
+    import time
+
+    chunker = get_chunker(algorithm, chunk_size)
+    base = base_dir if base_dir is not None else os.getcwd()
+    test_dir = os.path.join(base, f"chunker_test_{time.time_ns()}")
+    os.makedirs(test_dir, exist_ok=True)
+    t0 = time.perf_counter()
+    chunker.pack(input_file, test_dir)
+    pack_s = time.perf_counter() - t0
+    unpacked = os.path.join(test_dir, "unpacked_output")
+    t0 = time.perf_counter()
+    chunker.unpack(test_dir, unpacked)
+    unpack_s = time.perf_counter() - t0
+    try:
+        original = hash_file_128bit(input_file)
+    except OSError as e:
+        raise _capi.OxenError(f"Failed to hash original file: {e}", _capi.OXH_ERR_IO) from e
+    try:
+        restored = hash_file_128bit(unpacked)
+    except OSError as e:
+        raise _capi.OxenError(f"Failed to hash unpacked file: {e}", _capi.OXH_ERR_IO) from e
+    if original != restored:
+        raise VerificationFailed("Verification FAILED: Unpacked file does NOT match original.")
+    return {"test_dir": test_dir, "pack_s": pack_s, "unpack_s": unpack_s, "original_file_hash": str(original)}

@@ -221,3 +221,36 @@ def test_chunk_digests_arguments():
     first = np.zeros(2, dtype=np.uint64)
     rc = L.oxh_chunk_digests_host(None, None, None, 0, 0, None, 0, first.ctypes.data_as(_capi._u64p))
     assert rc == _capi.OXH_ERR_INVALID and b"zero" in L.oxh_last_error()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", [4096, 65_536, 100_003])
+def test_chunker_test_command_round_trip(cuda, oracle_lib, tmp_path, chunk):
+    """main.rs:156-241 (`Test`) with the multithreaded fixed-size chunker: pack, unpack, and the
+    whole-file hash_file_128bit of both agree; the digest is the oracle's xxh3_128 of the file."""
+    from oxen_amd import dedup
+
+    data = np.random.default_rng(chunk).integers(0, 256, 3_000_017, dtype=np.uint8).tobytes()
+    src = tmp_path / "input.bin"
+    src.write_bytes(data)
+    r = dedup.run_chunker_test("fixed-size-multithreaded", chunk, str(src), str(tmp_path))
+    assert r["original_file_hash"] == str(oracle_lib.xxh3_128_int(data))
+    assert dedup.hash_file_128bit(os.path.join(r["test_dir"], "unpacked_output")) == int(r["original_file_hash"])
+    with pytest.raises(OSError):
+        dedup.hash_file_128bit(str(tmp_path / "missing"))
+
+
+@pytest.mark.gpu
+def test_chunker_test_command_fixed_size_reads(cuda, tmp_path):
+    """The `fixed-size` (tree) chunker's unpack writes a DIRECTORY at unpacked_output, so the Test
+    command fails hashing it, as the reference does (File::open of a directory succeeds, its first
+    read fails with EISDIR): "Failed to hash unpacked file"."""
+    from oxen_amd import _capi, dedup
+
+    src = tmp_path / "input.bin"
+    src.write_bytes(np.random.default_rng(5).integers(0, 256, 70_001, dtype=np.uint8).tobytes())
+    with pytest.raises(_capi.OxenError, match="Failed to hash unpacked file"):
+        dedup.run_chunker_test("fixed-size", 5000, str(src), str(tmp_path))
+    # fastcdc's unpack is the reference's stub: nothing at unpacked_output, the hash fails (ENOENT)
+    with pytest.raises(_capi.OxenError, match="Failed to hash unpacked file"):
+        dedup.run_chunker_test("fastcdc", 8192, str(src), str(tmp_path))

@@ -237,8 +237,8 @@ def test_fastcdc_invalid_params(cuda):
 
 @pytest.mark.gpu
 def test_fastcdchunker_pack(cuda, oracle_lib, tmp_path):
-    """fastcdchunker.rs pack(): chunk files named by decimal digests + bincode metadata; unpack
-    restores the file."""
+    """fastcdchunker.rs pack(): chunk files named by decimal digests + bincode metadata; unpack is the
+    reference's stub (writes nothing), restore() rebuilds the file."""
     from oxen_amd import dedup
 
     rng = np.random.default_rng(8)
@@ -256,7 +256,9 @@ def test_fastcdchunker_pack(cuda, oracle_lib, tmp_path):
         assert os.path.getsize(os.path.join(out, name)) == l
     name, size, _ = dedup.decode_metadata(open(os.path.join(out, "metadata.bin"), "rb").read())
     assert (name, size) == ("blob.parquet", len(data))
-    ch.unpack(out, str(tmp_path / "restored"))
+    assert ch.unpack(out, str(tmp_path / "restored")) == str(tmp_path / "restored")  # the reference's stub
+    assert not (tmp_path / "restored").exists()
+    ch.restore(out, str(tmp_path / "restored"))
     assert (tmp_path / "restored").read_bytes() == data.tobytes()
 
 
