@@ -1,7 +1,8 @@
-"""Soak of the host FastCDC entries (oxh_fastcdc_files / oxh_fastcdc_host) against the C oracle: random
-file sets (empty, tiny, around min / avg / max, a few MiB to 200 MiB, constant runs), random chunk
-parameters and piece sizes (OXH_CDC_PIECE_MIB changes the context's pipeline between iterations),
-files and buffers alternating; every boundary and digest checked. Prints one JSON object.
+"""Soak of the host chunking entries against the C oracle: FastCDC (oxh_fastcdc_files / _host) and
+fixed-size chunks (oxh_chunk_digests_files / _host) over random file sets (empty, tiny, around min /
+avg / max, a few MiB to 200 MiB, constant runs), random chunk parameters and piece sizes
+(OXH_CDC_PIECE_MIB changes the context's pipeline between iterations), the four entries in turn, half
+the iterations on one long-lived context; every boundary and digest checked. Prints one JSON object.
 
     python tools/cdc_host_soak.py --seconds 120 [--dir /tmp/oxh_soak]
 """
@@ -19,6 +20,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+FIXED = [64, 1000, 4096, 5000, 65536, 1 << 20, (3 << 20) + 7]
 PARAMS = [(4096, 8192, 16384), (4096, 65536, 131072), (4096, 4096, 8192), (64, 256, 1024), (300, 257, 1500),
           (8192, 16384, 65536)]
 
@@ -41,7 +43,10 @@ def main():
     it = files_checked = chunks_checked = bytes_checked = 0
     failures = []
     last = time.time()
+    shared = _capi.Context(0)
     while time.time() < t_end:
+        entry = ("files", "host", "fixed_files", "fixed_host")[it % 4]
+        fixed = int(rng.choice(FIXED))
         mn, av, mx = PARAMS[int(rng.integers(len(PARAMS)))]
         piece = int(rng.choice([32, 48, 64, 256, 1024]))
         if piece * (1 << 20) < 2 * max(16 << 20, 4 * mx + 256):
@@ -66,30 +71,43 @@ def main():
                 lo = int(rng.integers(0, size))
                 d[lo:lo + int(rng.integers(1, 3 * mx))] = int(rng.integers(256))
             datas.append(d)
-        ctx = _capi.Context(0)
+        own = (it // 4) % 2 == 0
+        ctx = _capi.Context(0) if own else shared
         try:
-            if it % 2 == 0:
+            if entry in ("files", "fixed_files"):
                 paths = []
                 for i, d in enumerate(datas):
                     p = os.path.join(a.dir, f"f{i}")
                     d.tofile(p)
                     paths.append(p)
-                tab = dedup.fastcdc_files(paths, mn, av, mx, ctx=ctx)
+                if entry == "files":
+                    tab = dedup.fastcdc_files(paths, mn, av, mx, ctx=ctx)
+                else:
+                    tab = dedup.chunk_digests_files(paths, fixed, ctx=ctx)
                 if not (tab.status == 0).all():
                     failures.append({"it": it, "what": "status", "status": tab.status.tolist()})
-            else:
+            elif entry == "host":
                 tab = dedup.fastcdc_host(datas, mn, av, mx, ctx=ctx)
+            else:
+                tab = dedup.chunk_digests_host(datas, fixed, ctx=ctx)
         finally:
-            ctx.close()
+            if own:
+                ctx.close()
         for i, d in enumerate(datas):
-            off, ln, dig = tab.file(i)
-            want = F.chunks(d, mn, av, mx)
+            if entry.startswith("fixed"):
+                dig = tab.file(i)
+                off = np.arange(0, d.size, fixed, dtype=np.uint64)
+                ln = np.minimum(np.uint64(fixed), np.uint64(d.size) - off)
+                want = np.stack([off, ln], axis=1) if d.size else np.zeros((0, 2), dtype=np.uint64)
+            else:
+                off, ln, dig = tab.file(i)
+                want = F.chunks(d, mn, av, mx)
             ok = len(off) == len(want) and np.array_equal(off, want[:, 0]) and np.array_equal(ln, want[:, 1])
             if ok and len(want):
                 ok = np.array_equal(dig, oracle.batch(d, want[:, 0], want[:, 1], threads=8))
             if not ok:
-                failures.append({"it": it, "file": i, "size": int(d.size), "params": [mn, av, mx], "piece_mib": piece,
-                                 "entry": "files" if it % 2 == 0 else "host"})
+                failures.append({"it": it, "file": i, "size": int(d.size), "piece_mib": piece, "entry": entry,
+                                 "params": [fixed] if entry.startswith("fixed") else [mn, av, mx]})
             files_checked += 1
             chunks_checked += len(want)
             bytes_checked += int(d.size)
@@ -98,6 +116,7 @@ def main():
             print(f"[soak] {it} iterations, {files_checked} files, {chunks_checked} chunks, {len(failures)} failures",
                   file=sys.stderr, flush=True)
             last = time.time()
+    shared.close()
     shutil.rmtree(a.dir, ignore_errors=True)
     print(json.dumps({"iterations": it, "files_checked": files_checked, "chunks_checked": chunks_checked,
                       "bytes_checked": bytes_checked, "failures": failures[:20], "n_failures": len(failures)}),
