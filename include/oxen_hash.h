@@ -326,6 +326,18 @@ int oxh_chunk_digests_files(oxh_ctx* ctx, const char* const* paths, uint64_t n, 
                             uint64_t capacity, uint64_t* first_chunk, uint64_t* sizes, int32_t* status, int32_t* os_error);
 int oxh_chunk_digests_host(oxh_ctx* ctx, const uint8_t* const* bufs, const uint64_t* lens, uint64_t n,
                            uint64_t chunk_size, uint64_t* digests, uint64_t capacity, uint64_t* first_chunk);
+/* oxh_fastcdc_files / oxh_chunk_digests_files over several contexts (one per device, so one PCIe link,
+ * pipeline and reader pool each): the files split into nctx contiguous shares balanced by
+ * their stat sizes, the shares run side by side, and the tables come back concatenated in file order --
+ * every output exactly as the single-context call gives it. Contexts may repeat (shares on the same
+ * context run one after the other). A failing share fails the call with its text ("share k ..."). */
+int oxh_fastcdc_files_multi(oxh_ctx* const* ctxs, int nctx, const char* const* paths, uint64_t n, uint32_t min_size,
+                            uint32_t avg_size, uint32_t max_size, uint32_t level, uint64_t* chunk_offsets,
+                            uint64_t* chunk_lens, uint64_t* digests, uint64_t capacity, uint64_t* first_chunk,
+                            uint64_t* sizes, int32_t* status, int32_t* os_error);
+int oxh_chunk_digests_files_multi(oxh_ctx* const* ctxs, int nctx, const char* const* paths, uint64_t n,
+                                  uint64_t chunk_size, uint64_t* digests, uint64_t capacity, uint64_t* first_chunk,
+                                  uint64_t* sizes, int32_t* status, int32_t* os_error);
 /* The compiled-in GEAR table (256 u64) and the (mask_s, mask_l) pair for an average size and
  * normalization level (fastcdc v2020 MASKS[bits +/- level], bits = round(log2(avg))). Host only. */
 int oxh_fastcdc_gear(uint64_t* out256);

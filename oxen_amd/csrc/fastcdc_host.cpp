@@ -578,25 +578,29 @@ constexpr uint64_t kMaxFixedChunksPerRound = 4ull << 20;
 // largest fixed chunk: a chunk must fit a piece, and pieces stop at 3 GiB
 constexpr uint64_t kMaxFixedChunk = (3ull << 30) - kCdcBounce;
 
+// the crate's asserts (v2020::FastCDC::with_level) or the fixed chunk size's range, before any I/O
+int check_params(uint32_t mn, uint32_t av, uint32_t mx, uint32_t lv, uint64_t fixed) {
+    if (fixed) return fixed > kMaxFixedChunk ? oxh::set_error(OXH_ERR_INVALID, "chunk_size above 3 GiB - 64 MiB") : OXH_OK;
+    uint64_t ms = 0, ml = 0;
+    if (mn < 64 || mn > 1048576) return oxh::set_error(OXH_ERR_INVALID, "min_size must be in [64, 1048576]");
+    if (mx < 1024 || mx > 16777216) return oxh::set_error(OXH_ERR_INVALID, "max_size must be in [1024, 16777216]");
+    return oxh_fastcdc_masks(av, lv, &ms, &ml);
+}
+
 int run(oxh_ctx* ctx, CdcSource& src, uint64_t n, uint32_t mn, uint32_t av, uint32_t mx, uint32_t lv, uint64_t fixed,
         uint64_t* c_off, uint64_t* c_len, uint64_t* dig, uint64_t capacity, uint64_t* first_chunk, uint64_t* sizes,
-        int32_t* status, int32_t* os_error) {
+        int32_t* status, int32_t* os_error, uint64_t* total_out = nullptr) {
     if (!ctx) return oxh::set_error(OXH_ERR_INVALID, "null context");
     if (!first_chunk) return oxh::set_error(OXH_ERR_INVALID, "null first_chunk");
     if (capacity && !fixed && (!c_off || !c_len)) return oxh::set_error(OXH_ERR_INVALID, "null chunk table");
     if (capacity && fixed && !dig) return oxh::set_error(OXH_ERR_INVALID, "null digests");
+    if (int rc = check_params(mn, av, mx, lv, fixed)) return rc;
     uint64_t min_seg = 0;
     if (fixed) {
-        if (fixed > kMaxFixedChunk) return oxh::set_error(OXH_ERR_INVALID, "chunk_size above 3 GiB - 64 MiB");
         // a segment is whole chunks: at least one, and 16 MiB when the chunks are smaller (within the
         // round's chunk budget)
         min_seg = fixed * std::max<uint64_t>(1, std::min<uint64_t>((16ull << 20) / fixed, kMaxFixedChunksPerRound));
     } else {
-        // the crate's asserts (v2020::FastCDC::with_level), checked before any I/O
-        uint64_t ms = 0, ml = 0;
-        if (mn < 64 || mn > 1048576) return oxh::set_error(OXH_ERR_INVALID, "min_size must be in [64, 1048576]");
-        if (mx < 1024 || mx > 16777216) return oxh::set_error(OXH_ERR_INVALID, "max_size must be in [1024, 16777216]");
-        if (int rc = oxh_fastcdc_masks(av, lv, &ms, &ml)) return rc;
         // a segment is at least 16 MiB and 4 max chunks
         min_seg = std::max<uint64_t>(16ull << 20, 4ull * mx + kCdcAlign);
     }
@@ -740,8 +744,126 @@ int run(oxh_ctx* ctx, CdcSource& src, uint64_t n, uint32_t mn, uint32_t av, uint
                 (unsigned long long)n, round_no, (unsigned long long)(piece >> 20), (unsigned long long)C.total,
                 1e3 * (now() - t_start), 1e3 * C.t_read, 1e3 * C.t_chunk, 1e3 * C.t_wait, 1e3 * C.t_read_wait,
                 1e3 * C.t_h2d_wait, h->nbounce, (unsigned long long)(kCdcBounce >> 20), h->pool->size());
+    if (total_out) *total_out = C.total;
     if (C.total > capacity)
         return oxh::set_error(OXH_ERR_INVALID, "chunk capacity too small: need " + std::to_string(C.total) + " entries");
+    return OXH_OK;
+}
+
+// One call over several contexts (one per device: each its own PCIe link, pipeline and readers): the
+// files split into nctx contiguous shares balanced by bytes, the shares run side by side, and their
+// tables are concatenated in file order -- the multi-GPU form of SURVEY §8e for files in host memory,
+// no collective (the tables meet in host memory).
+int run_sharded(oxh_ctx* const* ctxs, int nctx, const char* const* paths, uint64_t n, uint32_t mn, uint32_t av, uint32_t mx,
+                uint32_t lv, uint64_t fixed, uint64_t* c_off, uint64_t* c_len, uint64_t* dig, uint64_t capacity,
+                uint64_t* first_chunk, uint64_t* sizes, int32_t* status, int32_t* os_error) {
+    if (!ctxs || nctx < 1) return oxh::set_error(OXH_ERR_INVALID, "no contexts");
+    for (int k = 0; k < nctx; ++k)
+        if (!ctxs[k]) return oxh::set_error(OXH_ERR_INVALID, "null context");
+    if (!first_chunk) return oxh::set_error(OXH_ERR_INVALID, "null first_chunk");
+    if (n && !paths) return oxh::set_error(OXH_ERR_INVALID, "null paths");
+    for (uint64_t i = 0; i < n; ++i)
+        if (!paths[i]) return oxh::set_error(OXH_ERR_INVALID, "null path");
+    if (int rc = check_params(mn, av, mx, lv, fixed)) return rc;
+    if (capacity && !fixed && (!c_off || !c_len)) return oxh::set_error(OXH_ERR_INVALID, "null chunk table");
+    if (capacity && fixed && !dig) return oxh::set_error(OXH_ERR_INVALID, "null digests");
+    if (nctx == 1 || n <= 1) {
+        FileSrc src(paths, n);
+        return run(ctxs[0], src, n, mn, av, mx, lv, fixed, c_off, c_len, dig, capacity, first_chunk, sizes, status, os_error);
+    }
+    // sizes for the split (a file that cannot be stat'ed weighs nothing; its share reports it)
+    std::vector<uint64_t> sz(n, 0);
+    {
+        std::vector<std::thread> th;
+        const int nt = std::min<int>(nctx * 2, 16);
+        for (int t = 0; t < nt; ++t)
+            th.emplace_back([&, t] {
+                for (uint64_t i = (uint64_t)t; i < n; i += (uint64_t)nt) {
+                    struct stat sb;
+                    if (stat(paths[i], &sb) == 0 && S_ISREG(sb.st_mode)) sz[i] = (uint64_t)sb.st_size;
+                }
+            });
+        for (auto& t : th) t.join();
+    }
+    // contiguous shares, cut where the running byte count (+1 per file) passes k/nctx of the total
+    std::vector<uint64_t> lo(nctx + 1, n);
+    {
+        uint64_t total = 0, run_w = 0;
+        for (uint64_t i = 0; i < n; ++i) total += sz[i] + 1;
+        int k = 1;
+        lo[0] = 0;
+        for (uint64_t i = 0; i < n && k < nctx; ++i) {
+            run_w += sz[i] + 1;
+            while (k < nctx && run_w * (uint64_t)nctx >= total * (uint64_t)k) lo[k++] = i + 1;
+        }
+        while (k < nctx) lo[k++] = n;
+    }
+    struct Share {
+        std::vector<uint64_t> off, len, dig, first, sizes;
+        std::vector<int32_t> st, oe;
+        uint64_t total = 0;
+        int rc = OXH_OK;
+        std::string err;
+    };
+    std::vector<Share> sh(nctx);
+    auto work = [&](int k) {
+        Share& S = sh[k];
+        const uint64_t a = lo[k], m = lo[k + 1] - a;
+        S.first.assign(m + 1, 0);
+        if (m == 0) return;  // (more contexts than files)
+        uint64_t cap = 1;
+        if (fixed) {
+            for (uint64_t i = a; i < a + m; ++i) cap += (sz[i] + fixed - 1) / fixed;
+        } else {
+            cap += oxh_fastcdc_max_chunks(sz.data() + a, m, mn);
+        }
+        for (int attempt = 0; attempt < 3; ++attempt) {  // a file that grew since its stat: retry with the count
+            if (!fixed) S.off.assign(cap, 0), S.len.assign(cap, 0);
+            if (dig) S.dig.assign(2 * cap, 0);
+            S.first.assign(m + 1, 0), S.sizes.assign(m, 0), S.st.assign(m, 0), S.oe.assign(m, 0);
+            FileSrc src(paths + a, m);
+            S.total = 0;
+            S.rc = run(ctxs[k], src, m, mn, av, mx, lv, fixed, fixed ? nullptr : S.off.data(), fixed ? nullptr : S.len.data(),
+                       dig ? S.dig.data() : nullptr, cap, S.first.data(), S.sizes.data(), S.st.data(), S.oe.data(), &S.total);
+            if (S.rc == OXH_ERR_INVALID && S.total > cap) {
+                cap = S.total;
+                continue;
+            }
+            break;
+        }
+        if (S.rc != OXH_OK) S.err = oxh_last_error();
+    };
+    {
+        std::vector<std::thread> th;
+        for (int k = 1; k < nctx; ++k) th.emplace_back(work, k);
+        work(0);
+        for (auto& t : th) t.join();
+    }
+    for (int k = 0; k < nctx; ++k)
+        if (sh[k].rc != OXH_OK)
+            return oxh::set_error(sh[k].rc, "share " + std::to_string(k) + " (files " + std::to_string(lo[k]) + ".." +
+                                                std::to_string(lo[k + 1]) + "): " + sh[k].err);
+    uint64_t base = 0;
+    for (int k = 0; k < nctx; ++k) {
+        const Share& S = sh[k];
+        const uint64_t a = lo[k], m = lo[k + 1] - a;
+        for (uint64_t i = 0; i < m; ++i) {
+            first_chunk[a + i] = base + S.first[i];
+            if (sizes) sizes[a + i] = S.sizes[i];
+            if (status) status[a + i] = S.st[i];
+            if (os_error) os_error[a + i] = S.oe[i];
+        }
+        const uint64_t keep = base < capacity ? std::min(S.total, capacity - base) : 0;
+        if (keep && !fixed) {
+            memcpy(c_off + base, S.off.data(), keep * 8);
+            memcpy(c_len + base, S.len.data(), keep * 8);
+        }
+        if (keep && dig) memcpy(dig + 2 * base, S.dig.data(), keep * 16);
+        base += S.total;
+    }
+    first_chunk[n] = base;
+    if (base > capacity)
+        return oxh::set_error(OXH_ERR_INVALID, "chunk capacity too small: need " + std::to_string(base) + " entries");
     return OXH_OK;
 }
 
@@ -794,6 +916,23 @@ int oxh_chunk_digests_host(oxh_ctx* ctx, const uint8_t* const* bufs, const uint6
     MemSrc src(bufs, lens);
     return run(ctx, src, n, 0, 0, 0, 0, chunk_size, nullptr, nullptr, digests, capacity, first_chunk, nullptr, nullptr,
                nullptr);
+}
+
+// The file entries over several contexts (devices): run_sharded above.
+int oxh_fastcdc_files_multi(oxh_ctx* const* ctxs, int nctx, const char* const* paths, uint64_t n, uint32_t min_size,
+                            uint32_t avg_size, uint32_t max_size, uint32_t level, uint64_t* chunk_offsets,
+                            uint64_t* chunk_lens, uint64_t* digests, uint64_t capacity, uint64_t* first_chunk,
+                            uint64_t* sizes, int32_t* status, int32_t* os_error) {
+    return run_sharded(ctxs, nctx, paths, n, min_size, avg_size, max_size, level, 0, chunk_offsets, chunk_lens, digests,
+                       capacity, first_chunk, sizes, status, os_error);
+}
+
+int oxh_chunk_digests_files_multi(oxh_ctx* const* ctxs, int nctx, const char* const* paths, uint64_t n,
+                                  uint64_t chunk_size, uint64_t* digests, uint64_t capacity, uint64_t* first_chunk,
+                                  uint64_t* sizes, int32_t* status, int32_t* os_error) {
+    if (chunk_size == 0) return oxh::set_error(OXH_ERR_INVALID, "Chunk size cannot be zero");
+    return run_sharded(ctxs, nctx, paths, n, 0, 0, 0, 0, chunk_size, nullptr, nullptr, digests, capacity, first_chunk, sizes,
+                       status, os_error);
 }
 
 }  // extern "C"

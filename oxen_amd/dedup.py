@@ -144,14 +144,21 @@ def _need_from_error(e: _capi.OxenError) -> Optional[int]:
     return int(m.group(1)) if m and e.code == _capi.OXH_ERR_INVALID else None
 
 
+def _ctx_array(ctxs):
+    arr = (ctypes.c_void_p * len(ctxs))(*[c.handle.value if isinstance(c.handle, ctypes.c_void_p) else c.handle
+                                          for c in ctxs])
+    return arr
+
+
 def fastcdc_files(paths, min_size: int, avg_size: int, max_size: int, level: int = 1, digests: bool = True,
-                  ctx: Optional[_capi.Context] = None) -> FastCdcTable:
+                  ctx: Optional[_capi.Context] = None, ctxs=None) -> FastCdcTable:
     """oxh_fastcdc_files: FastCDC v2020 boundaries and XXH3-128 chunk digests of files on disk, read by
     the library (fastcdchunker.rs:75-98: fs::read, v2020 chunking, xxh3_128 per chunk), results in
-    host memory. A file that cannot be opened / read has no chunks and its status / errno set."""
+    host memory. A file that cannot be opened / read has no chunks and its status / errno set.
+    ctxs (several contexts, e.g. one per device): oxh_fastcdc_files_multi, the files shared out."""
     from .hasher import _PathTable, default_context
 
-    ctx = ctx or default_context()
+    ctx = ctx or (None if ctxs else default_context())
     n = len(paths)
     sizes_hint = np.zeros(n, dtype=np.uint64)
     for i, p in enumerate(paths):
@@ -170,11 +177,14 @@ def fastcdc_files(paths, min_size: int, avg_size: int, max_size: int, level: int
         sizes = np.zeros(n, dtype=np.uint64)
         status = np.zeros(n, dtype=np.int32)
         oserr = np.zeros(n, dtype=np.int32)
-        rc = L.oxh_fastcdc_files(ctx.handle, table.arg if table else None, n, int(min_size), int(avg_size), int(max_size),
-                                 int(level), off.ctypes.data_as(_capi._u64p), ln.ctypes.data_as(_capi._u64p),
-                                 dig.ctypes.data_as(_capi._u64p) if dig is not None else None, cap,
-                                 first.ctypes.data_as(_capi._u64p), sizes.ctypes.data_as(_capi._u64p),
-                                 status.ctypes.data_as(_capi._i32p), oserr.ctypes.data_as(_capi._i32p))
+        tail = (int(min_size), int(avg_size), int(max_size), int(level), off.ctypes.data_as(_capi._u64p),
+                ln.ctypes.data_as(_capi._u64p), dig.ctypes.data_as(_capi._u64p) if dig is not None else None, cap,
+                first.ctypes.data_as(_capi._u64p), sizes.ctypes.data_as(_capi._u64p), status.ctypes.data_as(_capi._i32p),
+                oserr.ctypes.data_as(_capi._i32p))
+        if ctxs:
+            rc = L.oxh_fastcdc_files_multi(_ctx_array(ctxs), len(ctxs), table.arg if table else None, n, *tail)
+        else:
+            rc = L.oxh_fastcdc_files(ctx.handle, table.arg if table else None, n, *tail)
         try:
             _capi.check(rc, "oxh_fastcdc_files")
         except _capi.OxenError as e:
@@ -229,14 +239,15 @@ def _fixed_count(sizes, chunk: int) -> int:
     return int(sum((int(x) + chunk - 1) // chunk for x in sizes))
 
 
-def chunk_digests_files(paths, chunk_size: int, ctx: Optional[_capi.Context] = None) -> FixedChunkTable:
+def chunk_digests_files(paths, chunk_size: int, ctx: Optional[_capi.Context] = None, ctxs=None) -> FixedChunkTable:
     """oxh_chunk_digests_files: XXH3-128 of every fixed-size chunk of files on disk, read by the library
-    (fixedsize_multithreaded.rs:78-110), digests in host memory; per-file errors as fastcdc_files."""
+    (fixedsize_multithreaded.rs:78-110), digests in host memory; per-file errors as fastcdc_files.
+    ctxs: oxh_chunk_digests_files_multi over several contexts."""
     from .hasher import _PathTable, default_context
 
     if chunk_size <= 0:
         raise _capi.OxenError("Chunk size cannot be zero", _capi.OXH_ERR_INVALID)
-    ctx = ctx or default_context()
+    ctx = ctx or (None if ctxs else default_context())
     n = len(paths)
     hint = []
     for p in paths:
@@ -253,10 +264,12 @@ def chunk_digests_files(paths, chunk_size: int, ctx: Optional[_capi.Context] = N
         sizes = np.zeros(n, dtype=np.uint64)
         status = np.zeros(n, dtype=np.int32)
         oserr = np.zeros(n, dtype=np.int32)
-        rc = L.oxh_chunk_digests_files(ctx.handle, table.arg if table else None, n, int(chunk_size),
-                                       dig.ctypes.data_as(_capi._u64p), cap, first.ctypes.data_as(_capi._u64p),
-                                       sizes.ctypes.data_as(_capi._u64p), status.ctypes.data_as(_capi._i32p),
-                                       oserr.ctypes.data_as(_capi._i32p))
+        tail = (int(chunk_size), dig.ctypes.data_as(_capi._u64p), cap, first.ctypes.data_as(_capi._u64p),
+                sizes.ctypes.data_as(_capi._u64p), status.ctypes.data_as(_capi._i32p), oserr.ctypes.data_as(_capi._i32p))
+        if ctxs:
+            rc = L.oxh_chunk_digests_files_multi(_ctx_array(ctxs), len(ctxs), table.arg if table else None, n, *tail)
+        else:
+            rc = L.oxh_chunk_digests_files(ctx.handle, table.arg if table else None, n, *tail)
         try:
             _capi.check(rc, "oxh_chunk_digests_files")
         except _capi.OxenError as e:

@@ -699,7 +699,12 @@ std::vector<std::vector<Chunk>> split(const std::vector<uint64_t>& first, const 
 
 std::vector<ChunkedFile> fastcdc_files(const std::vector<std::string>& paths, uint32_t min_size, uint32_t avg_size,
                                        uint32_t max_size, oxh_ctx* ctx) {
-    ctx = ctx ? ctx : util::hasher::default_context();
+    return fastcdc_files(paths, min_size, avg_size, max_size, std::vector<oxh_ctx*>{ctx ? ctx : util::hasher::default_context()});
+}
+
+std::vector<ChunkedFile> fastcdc_files(const std::vector<std::string>& paths, uint32_t min_size, uint32_t avg_size,
+                                       uint32_t max_size, const std::vector<oxh_ctx*>& ctxs) {
+    if (ctxs.empty()) throw OxenError::basic_str("no contexts", OXH_ERR_INVALID);
     const size_t n = paths.size();
     std::vector<const char*> cp(n);
     std::vector<uint64_t> sz(n, 0);
@@ -712,8 +717,12 @@ std::vector<ChunkedFile> fastcdc_files(const std::vector<std::string>& paths, ui
     for (int attempt = 0;; ++attempt) {
         std::vector<uint64_t> off(cap), len(cap), dig(2 * cap), first(n + 1), sizes(n);
         std::vector<int32_t> status(n), oserr(n);
-        const int rc = oxh_fastcdc_files(ctx, cp.data(), n, min_size, avg_size, max_size, 1, off.data(), len.data(),
-                                         dig.data(), cap, first.data(), sizes.data(), status.data(), oserr.data());
+        const int rc = ctxs.size() == 1
+                           ? oxh_fastcdc_files(ctxs[0], cp.data(), n, min_size, avg_size, max_size, 1, off.data(), len.data(),
+                                               dig.data(), cap, first.data(), sizes.data(), status.data(), oserr.data())
+                           : oxh_fastcdc_files_multi(ctxs.data(), (int)ctxs.size(), cp.data(), n, min_size, avg_size, max_size,
+                                                     1, off.data(), len.data(), dig.data(), cap, first.data(), sizes.data(),
+                                                     status.data(), oserr.data());
         if (rc == OXH_ERR_INVALID && attempt < 2) {  // a file grew since the stat: the text has the count
             const std::string e = oxh_last_error();
             const size_t at = e.find("need ");
@@ -755,7 +764,12 @@ std::vector<std::vector<Chunk>> fastcdc_buffers(const std::vector<std::string_vi
 }
 
 std::vector<ChunkedFile> fixed_chunk_files(const std::vector<std::string>& paths, uint64_t chunk_size, oxh_ctx* ctx) {
-    ctx = ctx ? ctx : util::hasher::default_context();
+    return fixed_chunk_files(paths, chunk_size, std::vector<oxh_ctx*>{ctx ? ctx : util::hasher::default_context()});
+}
+
+std::vector<ChunkedFile> fixed_chunk_files(const std::vector<std::string>& paths, uint64_t chunk_size,
+                                           const std::vector<oxh_ctx*>& ctxs) {
+    if (ctxs.empty()) throw OxenError::basic_str("no contexts", OXH_ERR_INVALID);
     const size_t n = paths.size();
     std::vector<const char*> cp(n);
     uint64_t cap = 1;
@@ -767,8 +781,11 @@ std::vector<ChunkedFile> fixed_chunk_files(const std::vector<std::string>& paths
     for (int attempt = 0;; ++attempt) {
         std::vector<uint64_t> dig(2 * cap), first(n + 1), sizes(n);
         std::vector<int32_t> status(n), oserr(n);
-        const int rc = oxh_chunk_digests_files(ctx, cp.data(), n, chunk_size, dig.data(), cap, first.data(), sizes.data(),
-                                               status.data(), oserr.data());
+        const int rc = ctxs.size() == 1
+                           ? oxh_chunk_digests_files(ctxs[0], cp.data(), n, chunk_size, dig.data(), cap, first.data(),
+                                                     sizes.data(), status.data(), oserr.data())
+                           : oxh_chunk_digests_files_multi(ctxs.data(), (int)ctxs.size(), cp.data(), n, chunk_size, dig.data(),
+                                                           cap, first.data(), sizes.data(), status.data(), oserr.data());
         if (rc == OXH_ERR_INVALID && attempt < 2) {  // a file grew since the stat: the text has the count
             const std::string e = oxh_last_error();
             const size_t at = e.find("need ");

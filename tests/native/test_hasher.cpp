@@ -518,6 +518,22 @@ static void dedup_chunks(const std::string& golden) {
     CHECK(fixed_ok);
     CHECK(fx[2].chunks.size() == 1 && fx[2].chunks[0].hash == files[2].chunks[0].hash);
     CHECK(fb[1].size() == 1 && fb[1][0].hash == hasher::hash_buffer_128bit("hello", 5));
+    // the same over two contexts on device 0 (oxh_*_files_multi): identical tables
+    oxh_ctx* c2 = nullptr;
+    CHECK(oxh_ctx_create(0, 0, &c2) == OXH_OK);
+    const std::vector<oxh_ctx*> two{liboxen::util::hasher::default_context(), c2};
+    const auto fx2 = dd::fixed_chunk_files({p_big, missing, hello}, 65536, two);
+    const auto cd2 = dd::fastcdc_files({p_big, missing, hello}, 4096, 8192, 16384, two);
+    bool multi_same = fx2.size() == 3 && cd2.size() == 3;
+    for (size_t i = 0; multi_same && i < 3; ++i) {
+        multi_same = fx2[i].ok == fx[i].ok && fx2[i].chunks.size() == fx[i].chunks.size() && cd2[i].ok == files[i].ok &&
+                     cd2[i].chunks.size() == files[i].chunks.size() && cd2[i].os_error == files[i].os_error;
+        for (size_t k = 0; multi_same && k < fx[i].chunks.size(); ++k) multi_same = fx2[i].chunks[k].hash == fx[i].chunks[k].hash;
+        for (size_t k = 0; multi_same && k < files[i].chunks.size(); ++k)
+            multi_same = cd2[i].chunks[k].hash == files[i].chunks[k].hash && cd2[i].chunks[k].offset == files[i].chunks[k].offset;
+    }
+    CHECK(multi_same);
+    (void)oxh_ctx_destroy(c2);
     const std::string rm = std::string("rm -rf ") + dir;
     if (system(rm.c_str()) != 0) fprintf(stderr, "could not remove %s\n", dir);
 }

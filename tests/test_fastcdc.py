@@ -8,6 +8,7 @@ rule), the mask selection and the min/max walk. Beyond them the bar is: GPU chun
 bit-identical to the oracle on the same bytes, for every parameter class and the edge cases (empty,
 < min, odd tails, dense/pathological candidates).
 """
+import ctypes
 import os
 
 import numpy as np
@@ -429,6 +430,75 @@ def test_fastcdc_files_ragged(cuda, oracle_lib, tmp_path, monkeypatch, cfg, piec
     _check_table(oracle_lib, tab, datas, mn, av, mx)
     # the same bytes from host buffers
     _check_table(oracle_lib, dedup.fastcdc_host(datas, mn, av, mx), datas, mn, av, mx)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nctx", [2, 3, 13])
+def test_files_multi_contexts(cuda, oracle_lib, tmp_path, monkeypatch, nctx):
+    """oxh_fastcdc_files_multi / oxh_chunk_digests_files_multi (one context per device; here all on
+    device 0, two of them repeated): byte-balanced contiguous shares side by side, every output --
+    offsets, lengths, digests, first_chunk, sizes, status, errno -- equal to the one-context call, which
+    the oracle checks. 13 contexts for 12 paths leaves shares empty."""
+    from oxen_amd import _capi, dedup
+
+    monkeypatch.setenv("OXH_CDC_PIECE_MIB", "32")
+    rng = np.random.default_rng(nctx)
+    sizes = [0, 70_000_003, 1, 4095, 3_000_001, 41_000_000, 17, 262_145, 9_000_000, 5]
+    datas, paths = [], []
+    for i, n in enumerate(sizes):
+        d = rng.integers(0, 256, n, dtype=np.uint8)
+        p = tmp_path / f"m{i}"
+        p.write_bytes(d.tobytes())
+        datas.append(d)
+        paths.append(str(p))
+    paths.insert(3, str(tmp_path / "missing"))
+    paths.insert(7, str(tmp_path))
+    own = [_capi.Context(0) for _ in range(min(nctx, 3))]
+    ctxs = [own[k % len(own)] for k in range(nctx)]
+    try:
+        one = dedup.fastcdc_files(paths, 4096, 8192, 16384, ctx=own[0])
+        many = dedup.fastcdc_files(paths, 4096, 8192, 16384, ctxs=ctxs)
+        for f in ("offsets", "lens", "digests", "first", "sizes", "status", "os_error"):
+            assert np.array_equal(getattr(one, f), getattr(many, f)), f
+        k = 0
+        for i in range(len(paths)):
+            off, ln, dig = one.file(i)
+            if i in (3, 7):
+                assert len(off) == 0 and int(one.status[i]) != 0
+                continue
+            want = F.chunks(datas[k], 4096, 8192, 16384)
+            assert np.array_equal(off, want[:, 0]) and np.array_equal(ln, want[:, 1]), i
+            if len(want):
+                assert np.array_equal(dig, oracle_lib.batch(datas[k], want[:, 0], want[:, 1], threads=8)), i
+            k += 1
+        fone = dedup.chunk_digests_files(paths, 65_536, ctx=own[0])
+        fmany = dedup.chunk_digests_files(paths, 65_536, ctxs=ctxs)
+        for f in ("digests", "first", "sizes", "status", "os_error"):
+            assert np.array_equal(getattr(fone, f), getattr(fmany, f)), f
+        k = 0
+        for i in range(len(paths)):
+            if i in (3, 7):
+                continue
+            assert np.array_equal(fone.file(i), oracle_lib.chunk_digests(datas[k], 65_536, threads=8)), i
+            k += 1
+    finally:
+        for c in own:
+            c.close()
+
+
+def test_files_multi_arguments():
+    """Argument errors of the _multi entries before any device work."""
+    from oxen_amd import _capi
+
+    L = _capi.lib()
+    first = np.zeros(2, dtype=np.uint64)
+    assert L.oxh_fastcdc_files_multi(None, 0, None, 0, 4096, 8192, 16384, 1, None, None, None, 0,
+                                     first.ctypes.data_as(_capi._u64p), None, None, None) == _capi.OXH_ERR_INVALID
+    assert b"no contexts" in L.oxh_last_error()
+    arr = (ctypes.c_void_p * 2)(None, None)
+    assert L.oxh_chunk_digests_files_multi(arr, 2, None, 0, 0, None, 0, first.ctypes.data_as(_capi._u64p), None, None,
+                                           None) == _capi.OXH_ERR_INVALID
+    assert b"zero" in L.oxh_last_error()
 
 
 @pytest.mark.gpu

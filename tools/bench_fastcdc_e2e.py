@@ -4,6 +4,8 @@ xxh3_128 per chunk), through the C ABI's oxh_fastcdc_files. Prints one JSON obje
 
     python tools/bench_fastcdc_e2e.py --dir /tmp/c5 --files 16 --gib 8 --chunk 8192 --reps 3 [--cold] [--fixed]
 
+--devices 0,1,...: one context per entry (oxh_*_files_multi: the files shared out by bytes, one PCIe
+link per GPU on a multi-GPU node; a repeated device gives that device two pipelines).
 --fixed: fixed-size chunks of --chunk bytes instead (fixedsize_multithreaded.rs:78-110, through
 oxh_chunk_digests_files; the oracle's oxo_fixed_files beside it).
 
@@ -100,6 +102,7 @@ def main():
                     help="the CPU baseline's file access: read() whole files (fs::read) or mmap")
     ap.add_argument("--keep", action="store_true", help="keep the files")
     ap.add_argument("--fixed", action="store_true", help="fixed-size chunks of --chunk bytes instead of FastCDC")
+    ap.add_argument("--devices", default="", help="comma-separated devices, one context each (the _multi entries)")
     args = ap.parse_args()
 
     from oracle import fastcdc as F
@@ -114,18 +117,20 @@ def main():
     paths = make_files(args.dir, args.files, size)
     gen_s = time.perf_counter() - t0
     total = size * len(paths)
-    ctx = _capi.Context(0)
+    devices = [int(x) for x in args.devices.split(",") if x.strip()]
+    ctxs = [_capi.Context(d) for d in devices] if len(devices) > 1 else None
+    ctx = None if ctxs else _capi.Context(devices[0] if devices else 0)
     what = (f"fixed-size {args.chunk} B chunks" if args.fixed else f"FastCDC v2020 min {mn} avg {av} max {mx}")
     res = {"workload": f"{len(paths)} x {size} B files on disk (splitmix64), {what} "
                        f"+ XXH3-128 per chunk, chunk table + digests in host memory",
-           "bytes": total, "gen_s": round(gen_s, 1), "host_threads": threads}
+           "bytes": total, "gen_s": round(gen_s, 1), "host_threads": threads, "devices": devices or [0]}
 
     def gpu_once():
         t = time.perf_counter()
         if args.fixed:
-            tab = dedup.chunk_digests_files(paths, args.chunk, ctx=ctx)
+            tab = dedup.chunk_digests_files(paths, args.chunk, ctx=ctx, ctxs=ctxs)
         else:
-            tab = dedup.fastcdc_files(paths, mn, av, mx, ctx=ctx)
+            tab = dedup.fastcdc_files(paths, mn, av, mx, ctx=ctx, ctxs=ctxs)
         return time.perf_counter() - t, tab
 
     def cpu_once():
@@ -189,7 +194,8 @@ def main():
         res["cpu_model"] = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
     except (OSError, StopIteration):
         pass
-    ctx.close()
+    for c in ctxs or [ctx]:
+        c.close()
     if not args.keep:
         for p in paths:
             os.unlink(p)
