@@ -1,0 +1,115 @@
+"""The restore / merge checks (core/v_latest/index/restore.rs:231-297 should_restore_partial_node,
+:300-405 should_restore_file) batched over the ABI (oxen_amd/restore.py), against a per-file
+restatement of those functions over the oracle's XXH3-128."""
+import os
+
+import numpy as np
+import pytest
+
+
+def _meta_hash(oracle_lib, data: bytes) -> int:
+    """maybe_get_metadata_hash(MetadataText) on the oracle: count_lines with chars -> serde_json -> XXH3."""
+    lines = 1 + data.count(b"\n")
+    chars = sum(1 for b in data if (b & 0xC0) != 0x80)
+    return oracle_lib.xxh3_128_int(('{"text":{"num_lines":%d,"num_chars":%d}}' % (lines, chars)).encode())
+
+
+def _combined(oracle_lib, content: int, meta) -> int:
+    """get_combined_hash (hasher.rs:67-80) on the oracle."""
+    if meta is None:
+        return content
+    return oracle_lib.xxh3_128_int(content.to_bytes(16, "little") + int(meta).to_bytes(16, "little"))
+
+
+def _reference(oracle_lib, path, target, base, mtime_ok, combined, meta_hash):
+    """restore.rs:231-297 / :300-405 for one file, restated."""
+    if not os.path.exists(path):
+        return True
+    size = os.stat(path).st_size
+    ref = base if base is not None else target
+    if mtime_ok and size == ref.num_bytes:
+        return True
+    h = oracle_lib.xxh3_128_int(open(path, "rb").read())
+    if combined:
+        h = _combined(oracle_lib, h, meta_hash)
+        want, base_h = target.combined_hash, (base.combined_hash if base is not None else None)
+    else:
+        want, base_h = target.hash, (base.hash if base is not None else None)
+    if base is not None:
+        if h == want:
+            return True
+        return h == base_h
+    return h == want
+
+
+def _case(oracle_lib, tmp_path, combined: bool):
+    from oxen_amd import hasher
+    from oxen_amd.restore import NodeHashes
+
+    rng = np.random.default_rng(7 if combined else 3)
+    texts = [b"line one\nline two\n", "café über\n".encode(), b"", b"x" * 70_000]
+    old, new, other = {}, {}, {}
+    for i, t in enumerate(texts):
+        old[i] = t
+        new[i] = t + b"changed\n"
+        other[i] = bytes(rng.integers(0, 256, 333, dtype=np.uint8))
+
+    def node(data, text_meta):
+        c = oracle_lib.xxh3_128_int(data)
+        m = _meta_hash(oracle_lib, data) if text_meta else None
+        return NodeHashes(hash=c, num_bytes=len(data), combined_hash=_combined(oracle_lib, c, m))
+
+    paths, targets, bases, mt, meta, metah = [], [], [], [], [], []
+    k = 0
+    # working content x (target, base) x mtime verdict
+    for wi, working in enumerate(["old", "new", "other", "missing"]):
+        for has_base in (False, True):
+            for mtime_ok in (False, True):
+                for ti in range(len(texts)):
+                    p = tmp_path / f"w{k}.txt"
+                    k += 1
+                    if working != "missing":
+                        p.write_bytes({"old": old, "new": new, "other": other}[working][ti])
+                    text_meta = combined and ti % 2 == 0  # half the files carry MetadataText
+                    paths.append(str(p))
+                    targets.append(node(new[ti], text_meta))
+                    bases.append(node(old[ti], text_meta) if has_base else None)
+                    mt.append(mtime_ok)
+                    meta.append(hasher.TEXT if text_meta else None)
+                    data = p.read_bytes() if p.exists() else b""
+                    metah.append(_meta_hash(oracle_lib, data) if text_meta else None)
+    want = [_reference(oracle_lib, p, t, b, m, combined, mh) for p, t, b, m, mh in zip(paths, targets, bases, mt, metah)]
+    return paths, targets, bases, mt, meta, want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("combined", [False, True], ids=["partial_node", "file_node"])
+def test_should_restore_matches_the_reference(cuda, oracle_lib, tmp_path, combined):
+    """Every branch: missing working file, mtime + size short cut (taken even when the content differs),
+    the target's hash, the base's hash, neither; with and without a base node; combined hashes with
+    MetadataText counted on the hashing read."""
+    from oxen_amd import restore
+
+    paths, targets, bases, mt, meta, want = _case(oracle_lib, tmp_path, combined)
+    got = restore.should_restore(paths, targets, bases, mt, combined=combined, file_metadata=meta if combined else None)
+    assert got == want
+    assert any(want) and not all(want)
+
+
+@pytest.mark.gpu
+def test_should_restore_errors(cuda, oracle_lib, tmp_path):
+    """A working path that exists but cannot be read fails the call with hasher.rs's text (the
+    reference's `u128_hash_file_contents(..)?`); a directory is such a path (EISDIR on the read)."""
+    from oxen_amd import _capi, restore
+    from oxen_amd.restore import NodeHashes
+
+    d = tmp_path / "adir"
+    d.mkdir()
+    f = tmp_path / "ok.txt"
+    f.write_bytes(b"hello")
+    n = NodeHashes(hash=1, num_bytes=5, combined_hash=1)
+    with pytest.raises(_capi.OxenError, match="Could not read file for hashing"):
+        restore.should_restore([str(f), str(d)], [n, n], [None, None], [False, False])
+    assert restore.should_restore([str(f)], [n], [None], [True]) == [True]  # short cut: no read
+    with pytest.raises(_capi.OxenError, match="lengths differ"):
+        restore.should_restore([str(f)], [n, n], [None], [True])

@@ -64,6 +64,7 @@ step fixed_e2e_shm 900 env OXH_TRACE=1 python tools/bench_fastcdc_e2e.py --fixed
 step multi 600 python -u -m pytest tests/test_fastcdc.py tests/test_native_mirror.py -m gpu -v --timeout 300 --timeout-method thread -k "multi or native"
 step multi_e2e_2 900 env OXH_TRACE=1 python tools/bench_fastcdc_e2e.py --dir /dev/shm/oxh_c5 --files 16 --gib 8 --chunk 8192 --reps 3 --keep --cpu none --devices 0,0
 step multi_e2e_1 900 env OXH_TRACE=1 python tools/bench_fastcdc_e2e.py --dir /dev/shm/oxh_c5 --files 16 --gib 8 --chunk 8192 --reps 3 --keep --cpu none
+step restore 300 python -u -m pytest tests/test_restore.py -m gpu -v --timeout 200 --timeout-method thread
 step fixed_e2e_shm4k 900 env OXH_TRACE=1 python tools/bench_fastcdc_e2e.py --fixed --dir /dev/shm/oxh_c5 --files 16 --gib 8 --chunk 4096 --reps 3 --keep
 rm -rf /dev/shm/oxh_c5 /tmp/oxh_c5s /tmp/oxh_c5d /tmp/oxh_big /tmp/oxh_fx
 echo "== done $(date +%T)"
