@@ -18,6 +18,7 @@
 #include <thread>
 
 #include "../../include/oxen_hash.h"
+#include "commit_writer.hpp"
 
 namespace liboxen {
 
@@ -836,6 +837,81 @@ std::string chunk_name(u128 hash) {
     return b;
 }
 }  // namespace dedup
+
+namespace core::restore {
+std::vector<bool> should_restore_batch(const std::vector<RestoreCheck>& files, bool combined, oxh_ctx* ctx) {
+    ctx = ctx ? ctx : util::hasher::default_context();
+    const size_t n = files.size();
+    std::vector<bool> out(n, true);
+    std::vector<size_t> need;
+    for (size_t i = 0; i < n; ++i) {
+        const RestoreCheck& f = files[i];
+        struct stat sb;
+        if (stat(f.working_path.c_str(), &sb) != 0) {
+            if (errno == ENOENT || errno == ENOTDIR) continue;  // working_path.exists() is false: restore
+            throw OxenError::basic_str("Could not get file metadata: " + util::hasher::rust_path_debug(f.working_path) +
+                                           " error " + util::hasher::rust_io_error_debug(errno),
+                                       OXH_ERR_IO);
+        }
+        const NodeHashes& ref = f.base ? *f.base : f.target;
+        if (f.mtime_matched && (uint64_t)sb.st_size == ref.num_bytes) continue;
+        if (combined && f.file_metadata.kind == util::fs::FileMetadataHash::Error)
+            throw OxenError::basic_str(f.file_metadata.error.empty() ? "could not compute file metadata" : f.file_metadata.error,
+                                       OXH_ERR_META);
+        need.push_back(i);
+    }
+    if (need.empty()) return out;
+    const size_t m = need.size();
+    std::vector<const char*> cp(m);
+    for (size_t j = 0; j < m; ++j) cp[j] = files[need[j]].working_path.c_str();
+    std::vector<uint64_t> dig(2 * m), sizes(m), counts(2 * m);
+    std::vector<int32_t> status(m), oserr(m);
+    check(oxh_hash_files_ex(ctx, cp.data(), nullptr, m, dig.data(), sizes.data(), status.data(), oserr.data(),
+                            combined ? counts.data() : nullptr, nullptr),
+          "oxh_hash_files_ex");
+    for (size_t j = 0; j < m; ++j)  // u128_hash_file_contents(&working_path)? -- the first failure in order
+        if (status[j] != OXH_OK)
+            throw OxenError::basic_str(util::hasher::file_error_text(files[need[j]].working_path, status[j], oserr[j], sizes[j]),
+                                       status[j]);
+    std::vector<u128> h(m);
+    for (size_t j = 0; j < m; ++j) h[j] = to_u128(dig[2 * j], dig[2 * j + 1]);
+    if (combined) {  // maybe_get_metadata_hash + get_combined_hash (hasher.rs:67-100), batched
+        std::string arena;
+        std::vector<uint64_t> offs, lens;
+        std::vector<size_t> text;
+        for (size_t j = 0; j < m; ++j)
+            if (files[need[j]].file_metadata.kind == util::fs::FileMetadataHash::Text) {
+                const std::string js = "{\"text\":{\"num_lines\":" + std::to_string(counts[2 * j]) + ",\"num_chars\":" +
+                                       std::to_string(counts[2 * j + 1]) + "}}";
+                offs.push_back(arena.size()), lens.push_back(js.size()), arena += js, text.push_back(j);
+            }
+        const std::vector<u128> th = commit_writer::hash_streams(arena, offs, lens, ctx);
+        std::vector<std::optional<u128>> mh(m);
+        for (size_t t = 0; t < text.size(); ++t) mh[text[t]] = th[t];
+        for (size_t j = 0; j < m; ++j)
+            if (files[need[j]].file_metadata.kind == util::fs::FileMetadataHash::Given) mh[j] = files[need[j]].file_metadata.hash;
+        arena.clear(), offs.clear(), lens.clear();
+        std::vector<size_t> with;
+        for (size_t j = 0; j < m; ++j)
+            if (mh[j]) {
+                uint8_t b[32];
+                for (int k = 0; k < 16; ++k) b[k] = (uint8_t)(h[j] >> (8 * k)), b[16 + k] = (uint8_t)(*mh[j] >> (8 * k));
+                offs.push_back(arena.size()), lens.push_back(32), arena.append(reinterpret_cast<char*>(b), 32), with.push_back(j);
+            }
+        const std::vector<u128> ch = commit_writer::hash_streams(arena, offs, lens, ctx);
+        for (size_t t = 0; t < with.size(); ++t) h[with[t]] = ch[t];
+    }
+    for (size_t j = 0; j < m; ++j) {
+        const RestoreCheck& f = files[need[j]];
+        const u128 want = combined ? f.target.combined_hash : f.target.hash;
+        if (f.base)
+            out[need[j]] = h[j] == want || h[j] == (combined ? f.base->combined_hash : f.base->hash);
+        else
+            out[need[j]] = h[j] == want;
+    }
+    return out;
+}
+}  // namespace core::restore
 
 namespace multigpu {
 std::vector<uint8_t> DigestGather::unique_id() {

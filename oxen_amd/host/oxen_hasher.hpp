@@ -328,6 +328,27 @@ std::vector<std::vector<Chunk>> fixed_chunk_buffers(const std::vector<std::strin
 std::string chunk_name(u128 hash);
 }  // namespace dedup
 
+// core/v_latest/index/restore.rs:231-405: may restore / merge overwrite this working file?
+namespace core::restore {
+struct NodeHashes {  // PartialNode {hash, size} (:231) or FileNode {hash, combined_hash, num_bytes} (:300)
+    u128 hash = 0;
+    uint64_t num_bytes = 0;
+    u128 combined_hash = 0;
+};
+struct RestoreCheck {
+    std::string working_path;
+    NodeHashes target;                       // the node being restored / merged in
+    std::optional<NodeHashes> base;          // the merge base's node, if any
+    bool mtime_matched = false;              // LocalRepository::mtime_matches (local_repository.rs:556)
+    util::fs::FileMetadataHash file_metadata;  // combined only: None / Given / Text (Error: the call fails)
+};
+// should_restore_partial_node (combined = false) or should_restore_file (combined = true) x n: the
+// existence and mtime + size short cuts, then every remaining file hashed in one pass (oxh_hash_files_ex;
+// its text counts give MetadataText) and compared with the target / base hashes. The first file in
+// order whose stat, read or metadata fails throws OxenError, as the reference's `?` does.
+std::vector<bool> should_restore_batch(const std::vector<RestoreCheck>& files, bool combined, oxh_ctx* ctx = nullptr);
+}  // namespace core::restore
+
 // one process per GPU, the digest table gathered once over xGMI (oxh_comm_*).
 namespace multigpu {
 class DigestGather {

@@ -538,6 +538,66 @@ static void dedup_chunks(const std::string& golden) {
     if (system(rm.c_str()) != 0) fprintf(stderr, "could not remove %s\n", dir);
 }
 
+// core::restore::should_restore_batch (restore.rs:231-405) against the per-file rules spelled out here
+static void restore_checks() {
+    namespace rs = liboxen::core::restore;
+    char tmpl[] = "/tmp/oxh_restore_XXXXXX";
+    const char* dir = mkdtemp(tmpl);
+    CHECK(dir != nullptr);
+    if (!dir) return;
+    auto put = [&](const std::string& name, const std::string& data) {
+        const std::string p = std::string(dir) + "/" + name;
+        if (FILE* f = fopen(p.c_str(), "wb")) {
+            fwrite(data.data(), 1, data.size(), f);
+            fclose(f);
+        }
+        return p;
+    };
+    const std::string oldv = "line one\nline two\n", newv = "line one\nline two\nchanged\n", other = "something else";
+    auto text_meta = [](const std::string& d) {
+        uint64_t lines = 1, chars = 0;
+        for (unsigned char c : d) lines += c == '\n', chars += (c & 0xC0) != 0x80;
+        return hasher::get_metadata_hash(std::string("{\"text\":{\"num_lines\":") + std::to_string(lines) +
+                                         ",\"num_chars\":" + std::to_string(chars) + "}}");
+    };
+    auto node = [&](const std::string& d, bool meta) {
+        rs::NodeHashes h;
+        h.hash = hasher::hash_buffer_128bit(d);
+        h.num_bytes = d.size();
+        h.combined_hash = meta ? hasher::get_combined_hash(text_meta(d), h.hash) : h.hash;
+        return h;
+    };
+    for (bool combined : {false, true}) {
+        std::vector<rs::RestoreCheck> v;
+        std::vector<bool> want;
+        auto add = [&](const std::string& path, bool has_base, bool mtime_ok, bool expect) {
+            rs::RestoreCheck c;
+            c.working_path = path;
+            c.target = node(newv, combined);
+            if (has_base) c.base = node(oldv, combined);
+            c.mtime_matched = mtime_ok;
+            if (combined) c.file_metadata.kind = liboxen::util::fs::FileMetadataHash::Text;
+            v.push_back(c);
+            want.push_back(expect);
+        };
+        const std::string p_new = put("new.txt", newv), p_old = put("old.txt", oldv), p_other = put("other.txt", other);
+        add(std::string(dir) + "/missing", true, false, true);  // nothing to lose
+        add(p_new, true, false, true);                          // already the target
+        add(p_old, true, false, true);                          // unchanged since the base
+        add(p_other, true, false, false);                       // modified: keep it
+        add(p_other, false, false, false);                      // untracked and different
+        add(p_new, false, false, true);                         // untracked and equal to the target
+        add(put("short.txt", std::string(oldv.size(), 'z')), true, true, true);  // mtime + size short cut: no read
+        CHECK(rs::should_restore_batch(v, combined) == want);
+    }
+    rs::RestoreCheck d;
+    d.working_path = dir;  // a directory: the hash's read fails (EISDIR) and the call throws
+    d.target = node(newv, false);
+    CHECK(throws_oxen([&] { rs::should_restore_batch({d}, false); }, "Could not read file for hashing"));
+    const std::string rm = std::string("rm -rf ") + dir;
+    if (system(rm.c_str()) != 0) fprintf(stderr, "could not remove %s\n", dir);
+}
+
 int main(int argc, char** argv) {
     const std::string golden = argc > 1 ? argv[1] : "tests/golden";
     try {
@@ -550,6 +610,7 @@ int main(int argc, char** argv) {
         long_stream();
         modified_check(golden);
         dedup_chunks(golden);
+        restore_checks();
         char tmpl[] = "/tmp/oxh_native_XXXXXX";
         const char* scratch = mkdtemp(tmpl);
         if (!scratch) throw std::runtime_error("mkdtemp failed");
