@@ -259,6 +259,7 @@ struct oxh_ctx {
     hipStream_t stream = nullptr, copy_stream = nullptr;
     hipStream_t copy_stream2 = nullptr;  // large items: every other bounce window's H2D (created on first use)
     hipEvent_t ev_copy2_join = nullptr;  // copy_stream waits for copy_stream2's windows of a piece
+    std::atomic<const char*> where{"-"};  // where the engine / large-item path last blocked (stall reports)
     uint64_t stage_bytes = 0, max_items = 0;
     uint8_t* h_stage[NSLOT] = {};
     uint8_t* d_stage[NSLOT] = {};
@@ -589,6 +590,15 @@ int big_windows() {
     return v;
 }
 
+// H2D copy streams a large item's bounce windows alternate over (OXH_BIG_COPY_STREAMS, 1 or 2; default 2)
+int big_copy_streams() {
+    static const int v = [] {
+        const char* e = getenv("OXH_BIG_COPY_STREAMS");
+        return e && atoi(e) == 1 ? 1 : 2;
+    }();
+    return v;
+}
+
 // Where a large item's bytes come from.
 struct LargeSource {
     virtual ~LargeSource() = default;
@@ -771,7 +781,9 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
     if (!c->copy_stream2) HIP_TRY(hipStreamCreateWithFlags(&c->copy_stream2, hipStreamNonBlocking));
     if (!c->ev_copy2_join) HIP_TRY(hipEventCreateWithFlags(&c->ev_copy2_join, hipEventDisableTiming));
     uint64_t* sums = nullptr;
+    c->where.store("large_items: scratch lease");
     oxh::ScratchLease lease(c->stream);  // block sums of the two rounds in flight
+    c->where.store("large_items: scratch get");
     const uint64_t sums_per = (cap >> 10) * 8;
     if (lease.get(2 * sums_per * 8 * (uint64_t)n, (void**)&sums) != hipSuccess) return nomem();
     HIP_TRY(hipMemcpyAsync(d_res_all, h_res.data(), h_res.size(), hipMemcpyHostToDevice, c->stream));
@@ -822,12 +834,14 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
         std::deque<Window*> inflight;
         bool ok = true;
         auto finish = [&](Window& W) {
+            c->where.store("copy_piece: window reads");
             W.grp.wait();
+            c->where.store("copy_piece: window H2D");
             if (W.bad.load()) ok = false;
             if (!ok) return;
             // windows alternate over two copy streams: two DMA queues keep the PCIe link busier (the
             // FastCDC host pipeline measured 53.5 vs 47 GB/s)
-            hipStream_t cs = ((W.o / kBounce) & 1) ? c->copy_stream2 : c->copy_stream;
+            hipStream_t cs = (big_copy_streams() == 2 && ((W.o / kBounce) & 1)) ? c->copy_stream2 : c->copy_stream;
             if (hipMemcpyAsync(d + W.o, c->h_bounce[W.bb], W.m, hipMemcpyHostToDevice, cs) != hipSuccess ||
                 hipEventRecord(c->ev_bounce[W.bb], cs) != hipSuccess) {
                 ok = false;
@@ -841,10 +855,12 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
             W.bb = (int)(c->bounce_next++ % kNBounce);
             W.o = o;
             W.m = std::min(kBounce, plen - o);
+            c->where.store("copy_piece: bounce event");
             if (c->bounce_used[W.bb] && hipEventSynchronize(c->ev_bounce[W.bb]) != hipSuccess) {
                 ok = false;
                 break;
             }
+            c->where.store("copy_piece: start window");
             c->bounce_used[W.bb] = false;
             src.will_need(off + o + W.m, 2 * kBounce);  // two windows ahead of the ones being read
             uint8_t* buf = c->h_bounce[W.bb];
@@ -915,6 +931,7 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
         const int b = (int)(r & 1);
         pinned.swap(next_pin);
         // the chains of round r-2 (which read buffers b and their block sums) are done
+        c->where.store("large_items: piece free");
         if (round_used[b] && hipEventSynchronize(c->ev_piece_free[b]) != hipSuccess) {
             rc = fail(OXH_ERR_HIP, "large-item piece wait");
             break;
@@ -988,6 +1005,7 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
         }
     }
     // a failure mid-way: release what is still pinned
+    c->where.store("large_items: final copy sync");
     if (hipStreamSynchronize(c->copy_stream) != hipSuccess && rc == OXH_OK) rc = fail(OXH_ERR_HIP, "large-item copy");
     if (hipStreamSynchronize(c->copy_stream2) != hipSuccess && rc == OXH_OK) rc = fail(OXH_ERR_HIP, "large-item copy");
     for (int q = 0; q < n; ++q) {
@@ -998,7 +1016,9 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
     if (rc == OXH_OK && hipMemcpyAsync(h_res.data(), d_res_all, h_res.size(), hipMemcpyDeviceToHost, c->stream) != hipSuccess)
         rc = fail(OXH_ERR_HIP, "large-item results D2H");
     const double t_tail0 = Trace::now();
+    c->where.store("large_items: results sync");
     if (hipStreamSynchronize(c->stream) != hipSuccess && rc == OXH_OK) rc = fail(OXH_ERR_HIP, "large-item sync");
+    c->where.store("large_items: publish");
     if (tr.on)
         fprintf(stderr, "[oxh] large_items n=%d rounds=%llu piece=%llu MiB: total %.1f ms, pin %.1f, copy wait %.1f, unpin %.1f, "
                 "bounce %.1f, chain tail %.1f\n", n, (unsigned long long)rounds, (unsigned long long)(P >> 20),
@@ -2188,7 +2208,9 @@ void run_stream(oxh_ctx* c) {
                 fs.changed.pop_back();
             }
             fs.n_changed.fetch_sub(1);
+            c->where.store("engine: refresh_file");
             rc = refresh_file(fs, it.first, it.second);
+            c->where.store("engine: loop");
             continue;
         }
         if (const uint64_t no = fs.n_oversize.load(std::memory_order_acquire)) {
@@ -2208,7 +2230,9 @@ void run_stream(oxh_ctx* c) {
                 }
                 fs.n_oversize.fetch_sub(items.size());
                 big_wait_since = 0;
+                c->where.store("engine: big_files");
                 rc = big_files(fs, items);
+                c->where.store("engine: loop");
                 continue;
             }
         }
@@ -2243,7 +2267,9 @@ void run_stream(oxh_ctx* c) {
             pend[s].text = fs.want_text.load();
             pend[s].utf8 = fs.want_utf8.load();
             sl.state.store(2, std::memory_order_release);
+            c->where.store("engine: submit_slot");
             rc = submit_slot(c, s, bytes, cnt, false, bytes / cnt <= kShortItemBytes, pend[s].text, pend[s].utf8);
+            c->where.store("engine: loop");
             if (nbusy == 0) last_progress = Trace::now();
             tr.submit += Trace::now() - t0;
             tr.batches++;
@@ -2335,6 +2361,10 @@ static void dump_engine(oxh_ctx* c, const FileRequest& r) {
     fprintf(stderr, "[oxh] request stalled: n=%llu claimed=%llu remaining=%llu queue=%zu live=%d\n",
             (unsigned long long)r.n, (unsigned long long)r.next, (unsigned long long)r.remaining.load(), c->queue.size(),
             c->live != nullptr);
+    // where the context's engine thread last blocked, and which of its streams still hold work
+    fprintf(stderr, "[oxh]   ctx %p at \"%s\": stream=%s copy_stream=%s copy_stream2=%s\n", (void*)c, c->where.load(),
+            hipGetErrorName(hipStreamQuery(c->stream)), hipGetErrorName(hipStreamQuery(c->copy_stream)),
+            c->copy_stream2 ? hipGetErrorName(hipStreamQuery(c->copy_stream2)) : "-");
     if (FileStream* fs = static_cast<FileStream*>(c->live)) {
         fprintf(stderr, "[oxh]   run: readers=%d left=%d idle=%d closing=%d abort=%d cur=%d reqs=%zu cur_req=%zu oversize=%llu changed=%llu\n",
                 fs->nreaders, fs->readers_left.load(), fs->idle.load(), (int)fs->closing, (int)fs->abort.load(), fs->cur.load(),

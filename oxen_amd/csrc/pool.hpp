@@ -128,8 +128,13 @@ class Pool {
                 std::unique_lock<std::mutex> lk(mu_);
                 cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
                 if (stop_ && q_.empty()) return;
-                job = std::move(q_.front());  // first in, first out: a caller waiting on its oldest
-                q_.pop_front();               // group (the bounce windows) gets it done first
+                if (lifo_) {  // OXH_POOL_LIFO=1: last in, first out (the r04 order; for A/Bs)
+                    job = std::move(q_.back());
+                    q_.pop_back();
+                } else {
+                    job = std::move(q_.front());  // first in, first out: a caller waiting on its oldest
+                    q_.pop_front();               // group (the bounce windows) gets it done first
+                }
                 ++busy_;
             }
             job();
@@ -140,6 +145,7 @@ class Pool {
             idle_cv_.notify_all();
         }
     }
+    const bool lifo_ = getenv("OXH_POOL_LIFO") && atoi(getenv("OXH_POOL_LIFO")) != 0;
     std::vector<std::thread> th_;
     std::deque<std::function<void()>> q_;
     std::mutex mu_;
