@@ -408,12 +408,16 @@ int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_
     const uint64_t M = c->max_items;
     STEP("submit s=%d bytes=%llu cnt=%llu lane=%d short=%d", s, (unsigned long long)bytes, (unsigned long long)cnt,
          (int)any_short_only, (int)short_items);
+    c->where.store("submit_slot: H2D stage");
     HIP_TRY(hipMemcpyAsync(c->d_stage[s], c->h_stage[s], bytes, hipMemcpyHostToDevice, c->copy_stream));
+    c->where.store("submit_slot: H2D desc");
     HIP_TRY(hipMemcpyAsync(c->d_desc[s], c->h_desc[s], cnt * 8, hipMemcpyHostToDevice, c->copy_stream));
     HIP_TRY(hipMemcpyAsync(c->d_desc[s] + M, c->h_desc[s] + M, cnt * 8, hipMemcpyHostToDevice, c->copy_stream));
+    c->where.store("submit_slot: record / wait");
     HIP_TRY(hipEventRecord(c->ev_copied[s], c->copy_stream));
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[s], 0));
     STEP("copies queued s=%d", s);
+    c->where.store("submit_slot: launch");
     int rc = text ? launch_text(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->d_cnt[s], c->stream,
                                 short_items)
              : any_short_only ? launch_lane(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->stream)
@@ -421,6 +425,7 @@ int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_
                                             short_items ? ItemShape::Short : ItemShape::Long);
     if (rc) return rc;
     STEP("launched s=%d", s);
+    c->where.store("submit_slot: D2H");
     HIP_TRY(hipMemcpyAsync(c->h_out[s], c->d_out[s], cnt * 16, hipMemcpyDeviceToHost, c->stream));
     if (text) HIP_TRY(hipMemcpyAsync(c->h_cnt[s], c->d_cnt[s], cnt * 16, hipMemcpyDeviceToHost, c->stream));
     if (utf8) {  // is_utf8 sniff of the same staged bytes
@@ -429,6 +434,7 @@ int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(c->h_utf8[s], c->d_utf8[s], cnt * 4, hipMemcpyDeviceToHost, c->stream));
     }
+    c->where.store("submit_slot: record done");
     HIP_TRY(hipEventRecord(c->ev_done[s], c->stream));
     STEP("submitted s=%d", s);
     return OXH_OK;
@@ -577,6 +583,12 @@ int oversize_item(oxh_ctx* c, const uint8_t* src, uint64_t len, uint64_t* out2, 
 // counts accumulate over the pieces; is_utf8 reads the first 4 KiB of piece 0. With a sink (fused
 // add) every bounce part is also written to the sink's temp as it is read, and the temp is published
 // once the digest is known: the item never has to fit in host memory.
+// Stall reports (dump_engine): the live contexts, and where context creation / destruction and the
+// streaming Xxh3 last were -- the threads that call those are not engine threads.
+std::mutex g_live_mu;
+std::vector<oxh_ctx*> g_live;
+std::atomic<const char*> g_life{"-"}, g_stream_where{"-"};
+
 constexpr uint64_t kBounce = 64ull << 20, kBigRead = 4ull << 20;
 constexpr int kNBounce = 8;  // bounce buffers in the ring: up to 7 windows read while earlier H2Ds drain
 
@@ -727,26 +739,23 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
         return OXH_OK;
     };
     const uint64_t need = (uint64_t)n * (2 * slot + kRes) + 4096;
+    c->where.store("large_items: d_big");
     if (c->d_big_size < need) {
-        // Regrow without a device-wide sync: every earlier large_items call on this context finished
-        // its work on d_big before it returned (both of its streams are synchronised at the end), and
-        // the buffer is stream-ordered memory of c->stream (hipMallocAsync / hipFreeAsync), so other
-        // contexts and device-resident callers on their own streams never wait for the regrowth.
+        // Regrow: every earlier large_items call on this context finished its work on d_big before it
+        // returned (its streams are synchronised at the end), so the old buffer is idle. Plain
+        // hipFree / hipMalloc: the stream-ordered allocator (hipMallocAsync / hipFreeAsync on
+        // c->stream, r04) deadlocked inside the runtime under concurrent contexts -- threads stuck
+        // in hipMallocAsync beside others in hipEventRecord / hipHostMalloc with every stream idle
+        // (tools/engine_soak.py --regrow with a device soak beside it, profiles/r05/r05s6_*).
         if (c->d_big) {
-            (void)hipFreeAsync(c->d_big, c->stream);
+            (void)hipFree(c->d_big);
             c->d_big = nullptr;
             c->d_big_size = 0;
         }
         void* m = nullptr;
-        const bool ok = hipMallocAsync(&m, need, c->stream) == hipSuccess && m != nullptr;
-        // the copy stream's first piece must not run ahead of the allocation
-        if (!ok || hipStreamSynchronize(c->stream) != hipSuccess) {
+        const bool ok = hipMalloc(&m, need) == hipSuccess && m != nullptr;
+        if (!ok) {
             (void)hipGetLastError();
-            if (ok) {
-                (void)hipFreeAsync(m, c->stream);
-                (void)hipStreamSynchronize(c->stream);
-                (void)hipGetLastError();
-            }
             // 2 piece buffers per file side by side did not fit: fewer files at a time (each item's
             // result does not depend on its batch), down to one before the items fail with NOMEM
             if (n > 1) {
@@ -769,6 +778,7 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
     static_assert(sizeof(Res) + 64 <= kRes, "results area");
     std::vector<uint8_t> h_res((size_t)n * kRes, 0);
     for (int q = 0; q < n; ++q) reinterpret_cast<Res*>(h_res.data() + (size_t)q * kRes)->len = jobs[q].L;
+    c->where.store("large_items: bounce alloc");
     for (int b = 0; b < kNBounce; ++b) {
         if (!c->h_bounce[b] && hipHostMalloc(&c->h_bounce[b], kBounce, hipHostMallocDefault) != hipSuccess) {
             c->h_bounce[b] = nullptr;
@@ -778,6 +788,7 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
     }
     for (int b = 0; b < 2; ++b)
         if (!c->ev_piece_free[b]) HIP_TRY(hipEventCreateWithFlags(&c->ev_piece_free[b], hipEventDisableTiming));
+    c->where.store("large_items: events / copy_stream2");
     if (!c->copy_stream2) HIP_TRY(hipStreamCreateWithFlags(&c->copy_stream2, hipStreamNonBlocking));
     if (!c->ev_copy2_join) HIP_TRY(hipEventCreateWithFlags(&c->ev_copy2_join, hipEventDisableTiming));
     uint64_t* sums = nullptr;
@@ -1103,11 +1114,17 @@ int oxh_ctx_create(int device, uint64_t staging_bytes, oxh_ctx** out) {
     HIP_TRY(hipSetDevice(device));
     oxh_ctx* c = new oxh_ctx();
     c->device = device;
+    {
+        std::lock_guard<std::mutex> g(g_live_mu);
+        g_live.push_back(c);
+    }
+    g_life.store("create: streams");
     c->stage_bytes = align_up(staging_bytes ? staging_bytes : (256ull << 20));
     c->max_items = std::max<uint64_t>(1024, c->stage_bytes / 4096);
     auto cleanup = [&](int code, const char* m) { oxh_ctx_destroy(c); return fail(code, m); };
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return cleanup(OXH_ERR_HIP, "stream");
     if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) return cleanup(OXH_ERR_HIP, "copy stream");
+    g_life.store("create: slot buffers");
     for (int s = 0; s < NSLOT; ++s) {
         if (hipHostMalloc(&c->h_stage[s], c->stage_bytes, hipHostMallocDefault) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "pinned staging");
         if (hipMalloc(&c->d_stage[s], c->stage_bytes) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "device staging");
@@ -1131,12 +1148,18 @@ int oxh_ctx_create(int device, uint64_t staging_bytes, oxh_ctx** out) {
     c->pool = new oxh::Pool(default_threads());
     c->rpool = new oxh::Pool(default_threads(), /*private_fds=*/true);  // readers use only their own fds
     c->engine = std::thread(engine_main, c);
+    g_life.store("create: done");
     *out = c;
     return OXH_OK;
 }
 
 int oxh_ctx_destroy(oxh_ctx* c) {
     if (!c) return OXH_OK;
+    {
+        std::lock_guard<std::mutex> g(g_live_mu);
+        g_live.erase(std::remove(g_live.begin(), g_live.end(), c), g_live.end());
+    }
+    g_life.store("destroy: engine join");
     if (c->engine.joinable()) {  // finishes what is queued, then exits
         {
             std::lock_guard<std::mutex> g(c->qmu);
@@ -1146,6 +1169,7 @@ int oxh_ctx_destroy(oxh_ctx* c) {
         c->engine.join();
     }
     (void)hipSetDevice(c->device);
+    g_life.store("destroy: buffers");
     if (c->cdc && c->cdc_free) c->cdc_free(c->cdc);
     c->cdc = nullptr;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
@@ -1164,10 +1188,12 @@ int oxh_ctx_destroy(oxh_ctx* c) {
         if (c->ev_copied[s]) (void)hipEventDestroy(c->ev_copied[s]);
         if (c->ev_done[s]) (void)hipEventDestroy(c->ev_done[s]);
     }
-    if (c->d_big) {  // stream-ordered memory (large_items)
-        (void)hipFreeAsync(c->d_big, c->stream);
+    g_life.store("destroy: d_big");
+    if (c->d_big) {  // large_items' piece buffers
         (void)hipStreamSynchronize(c->stream);
+        (void)hipFree(c->d_big);
     }
+    g_life.store("destroy: bounce / streams");
     for (int b = 0; b < kNBounce; ++b) {
         if (c->h_bounce[b]) (void)hipHostFree(c->h_bounce[b]);
         if (c->ev_bounce[b]) (void)hipEventDestroy(c->ev_bounce[b]);
@@ -1181,10 +1207,12 @@ int oxh_ctx_destroy(oxh_ctx* c) {
         (void)hipStreamDestroy(c->copy_stream2);
     }
     if (c->ev_copy2_join) (void)hipEventDestroy(c->ev_copy2_join);
+    g_life.store("destroy: pools");
     delete c->pool;
     delete c->wpool;
     delete c->rpool;
     delete c;
+    g_life.store("destroy: done");
     return OXH_OK;
 }
 
@@ -1380,22 +1408,29 @@ int oxh_xxh3_stream_update(oxh_xxh3_stream* s, const void* data, uint64_t len) {
     const uint64_t cap = s->piece + 1025;
     while (len) {
         const uint64_t take = std::min(len, cap - s->fill);
+        g_stream_where.store("update: reserve");
         if (int rc = stream_reserve(s, s->fill + take)) return rc;
+        g_stream_where.store("update: copy");
         memcpy(s->h_pend + s->fill, p, take);
         s->fill += take;
         s->total += take;
         p += take;
         len -= take;
-        if (s->fill == cap)
+        if (s->fill == cap) {
+            g_stream_where.store("update: flush");
             if (int rc = stream_flush(s)) return rc;
+        }
     }
+    g_stream_where.store("update: done");
     return OXH_OK;
 }
 
 int oxh_xxh3_stream_digest(oxh_xxh3_stream* s, uint64_t* out2) {
     if (!s || !out2) return fail(OXH_ERR_INVALID, "bad stream digest");
     HIP_TRY(hipSetDevice(s->device));
+    g_stream_where.store("digest: queue");
     if (int rc = stream_queue(s)) return rc;
+    g_stream_where.store("digest: final piece");
     uint64_t* d_out = nullptr;
     if (s->pieces == 0) {  // the whole stream is pending: a one-shot digest (K1, or K1L above 1 MiB)
         const uint64_t need = align_up(s->fill + 1) + 256;
@@ -1441,7 +1476,9 @@ int oxh_xxh3_stream_reset(oxh_xxh3_stream* s) {
 int oxh_xxh3_stream_destroy(oxh_xxh3_stream* s) {
     if (!s) return OXH_OK;
     (void)hipSetDevice(s->device);
+    g_stream_where.store("destroy: sync");
     if (s->st) (void)hipStreamSynchronize(s->st);
+    g_stream_where.store("destroy: free");
     if (s->d_mem) (void)hipFree(s->d_mem);
     if (s->d_one) (void)hipFree(s->d_one);
     if (s->h_pend) (void)hipHostFree(s->h_pend);
@@ -1450,6 +1487,7 @@ int oxh_xxh3_stream_destroy(oxh_xxh3_stream* s) {
         if (e) (void)hipEventDestroy(e);
     if (s->st) (void)hipStreamDestroy(s->st);
     delete s;
+    g_stream_where.store("destroy: done");
     return OXH_OK;
 }
 
@@ -2361,10 +2399,18 @@ static void dump_engine(oxh_ctx* c, const FileRequest& r) {
     fprintf(stderr, "[oxh] request stalled: n=%llu claimed=%llu remaining=%llu queue=%zu live=%d\n",
             (unsigned long long)r.n, (unsigned long long)r.next, (unsigned long long)r.remaining.load(), c->queue.size(),
             c->live != nullptr);
-    // where the context's engine thread last blocked, and which of its streams still hold work
-    fprintf(stderr, "[oxh]   ctx %p at \"%s\": stream=%s copy_stream=%s copy_stream2=%s\n", (void*)c, c->where.load(),
-            hipGetErrorName(hipStreamQuery(c->stream)), hipGetErrorName(hipStreamQuery(c->copy_stream)),
-            c->copy_stream2 ? hipGetErrorName(hipStreamQuery(c->copy_stream2)) : "-");
+    // where each live context's engine thread last blocked, and which of its streams still hold work;
+    // where context creation / destruction and the streaming Xxh3 last were
+    fprintf(stderr, "[oxh]   this ctx %p; ctx create/destroy at \"%s\", Xxh3 stream at \"%s\"\n", (void*)c, g_life.load(),
+            g_stream_where.load());
+    {
+        std::lock_guard<std::mutex> g(g_live_mu);
+        for (oxh_ctx* x : g_live)
+            fprintf(stderr, "[oxh]   ctx %p at \"%s\": stream=%s copy_stream=%s copy_stream2=%s\n", (void*)x, x->where.load(),
+                    x->stream ? hipGetErrorName(hipStreamQuery(x->stream)) : "-",
+                    x->copy_stream ? hipGetErrorName(hipStreamQuery(x->copy_stream)) : "-",
+                    x->copy_stream2 ? hipGetErrorName(hipStreamQuery(x->copy_stream2)) : "-");
+    }
     if (FileStream* fs = static_cast<FileStream*>(c->live)) {
         fprintf(stderr, "[oxh]   run: readers=%d left=%d idle=%d closing=%d abort=%d cur=%d reqs=%zu cur_req=%zu oversize=%llu changed=%llu\n",
                 fs->nreaders, fs->readers_left.load(), fs->idle.load(), (int)fs->closing, (int)fs->abort.load(), fs->cur.load(),
