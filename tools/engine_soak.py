@@ -16,6 +16,8 @@ seals early and takes the large-file path), one default. Requests, picked at ran
   modified   oxh_files_modified: equal sizes, drifted mtimes, node hashes right or off by one
   utf8       oxh_hash_files_text_utf8 (digests, counts and the is_utf8 sniff)
   pool       the reader-process pool (oxh_pool, 2 helpers) over a random subset
+  cdc        oxh_fastcdc_files (8 KiB FastCDC) on the same contexts, every table against the oracle
+  fixed      oxh_chunk_digests_files (4 KiB / 64 KiB / 1 MiB chunks), against the oracle
 --regrow: a thread keeps creating a context with 1 MiB staging slots, hashing 1, 2, then 4 of the
 corpus's large files side by side (each step regrows the context's large-file piece buffers:
 stream-ordered, no device-wide sync) and destroying it again -- while the other threads (and any
@@ -97,7 +99,10 @@ def main():
 
         ctxs = [_capi.Context(0, staging_bytes=1 << 20), _capi.Context(0)]
         lock = threading.Lock()
-        counts = {k: 0 for k in ("files", "text", "add", "buffers", "stream", "meta", "streams", "modified", "utf8", "pool")}
+        counts = {k: 0 for k in ("files", "text", "add", "buffers", "stream", "meta", "streams", "modified", "utf8", "pool",
+                                 "cdc", "fixed")}
+        from oracle import fastcdc as F
+        from oxen_amd import dedup
         from oxen_amd.procpool import ShardedFileHasher
 
         pool = ShardedFileHasher(procs=2, devices=(0,), threads=4)
@@ -211,6 +216,32 @@ def main():
                     for p, o, s_ in zip(sub, out, st):
                         if s_ != 0 or version(p, int(o[1]) << 64 | int(o[0])) is None:
                             fail(f"pool: {p} status {s_}")
+                        else:
+                            n_ok += 1
+                elif kind in ("cdc", "fixed"):  # the host chunk entries on the same contexts (stable files)
+                    sub = [r.choice(stable) for _ in sub[:64]]
+                    datas = []
+                    for p in sub:
+                        with open(p, "rb") as f:
+                            datas.append(np.frombuffer(f.read(), dtype=np.uint8))
+                    if kind == "cdc":
+                        tab = dedup.fastcdc_files(sub, 4096, 8192, 16384, ctx=ctx)
+                    else:
+                        chunk = r.choice((4096, 65536, 1 << 20))
+                        tab = dedup.chunk_digests_files(sub, chunk, ctx=ctx)
+                    for i, (p, d) in enumerate(zip(sub, datas)):
+                        if int(tab.status[i]) != 0:
+                            fail(f"{kind}: {p} status {int(tab.status[i])}")
+                            continue
+                        if kind == "cdc":
+                            off, ln, dig = tab.file(i)
+                            w = F.chunks(d, 4096, 8192, 16384)
+                            ok = np.array_equal(off, w[:, 0]) and np.array_equal(ln, w[:, 1]) and \
+                                (len(w) == 0 or np.array_equal(dig, oracle.batch(d, w[:, 0], w[:, 1])))
+                        else:
+                            ok = np.array_equal(tab.file(i), oracle.chunk_digests(d, chunk))
+                        if not ok:
+                            fail(f"{kind}: {p} table differs from the oracle")
                         else:
                             n_ok += 1
                 else:  # stream
