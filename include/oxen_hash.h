@@ -338,6 +338,13 @@ int oxh_fastcdc_files_multi(oxh_ctx* const* ctxs, int nctx, const char* const* p
 int oxh_chunk_digests_files_multi(oxh_ctx* const* ctxs, int nctx, const char* const* paths, uint64_t n,
                                   uint64_t chunk_size, uint64_t* digests, uint64_t capacity, uint64_t* first_chunk,
                                   uint64_t* sizes, int32_t* status, int32_t* os_error);
+/* ... and the host-buffer entries (oxh_fastcdc_host / oxh_chunk_digests_host) the same way, the shares
+ * balanced by the buffers' lengths. */
+int oxh_fastcdc_host_multi(oxh_ctx* const* ctxs, int nctx, const uint8_t* const* bufs, const uint64_t* lens, uint64_t n,
+                           uint32_t min_size, uint32_t avg_size, uint32_t max_size, uint32_t level, uint64_t* chunk_offsets,
+                           uint64_t* chunk_lens, uint64_t* digests, uint64_t capacity, uint64_t* first_chunk);
+int oxh_chunk_digests_host_multi(oxh_ctx* const* ctxs, int nctx, const uint8_t* const* bufs, const uint64_t* lens, uint64_t n,
+                                 uint64_t chunk_size, uint64_t* digests, uint64_t capacity, uint64_t* first_chunk);
 /* The compiled-in GEAR table (256 u64) and the (mask_s, mask_l) pair for an average size and
  * normalization level (fastcdc v2020 MASKS[bits +/- level], bits = round(log2(avg))). Host only. */
 int oxh_fastcdc_gear(uint64_t* out256);

@@ -98,6 +98,10 @@ SIGNATURES = {
                                        _u32, _u64p, _u64p, _u64p, _u64, _u64p, _u64p, _i32p, _i32p]),
     "oxh_chunk_digests_files_multi": (_int, [ctypes.POINTER(_vp), _int, ctypes.POINTER(ctypes.c_char_p), _u64, _u64, _u64p,
                                              _u64, _u64p, _u64p, _i32p, _i32p]),
+    "oxh_fastcdc_host_multi": (_int, [ctypes.POINTER(_vp), _int, ctypes.POINTER(ctypes.c_char_p), _u64p, _u64, _u32, _u32,
+                                      _u32, _u32, _u64p, _u64p, _u64p, _u64, _u64p]),
+    "oxh_chunk_digests_host_multi": (_int, [ctypes.POINTER(_vp), _int, ctypes.POINTER(ctypes.c_char_p), _u64p, _u64, _u64,
+                                            _u64p, _u64, _u64p]),
     "oxh_fastcdc_gear": (_int, [_u64p]),
     "oxh_fastcdc_masks": (_int, [_u32, _u32, _u64p, _u64p]),
     "oxh_comm_unique_id": (_int, [ctypes.c_char_p]),

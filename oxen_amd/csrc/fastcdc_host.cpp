@@ -754,26 +754,41 @@ int run(oxh_ctx* ctx, CdcSource& src, uint64_t n, uint32_t mn, uint32_t av, uint
 // files split into nctx contiguous shares balanced by bytes, the shares run side by side, and their
 // tables are concatenated in file order -- the multi-GPU form of SURVEY §8e for files in host memory,
 // no collective (the tables meet in host memory).
-int run_sharded(oxh_ctx* const* ctxs, int nctx, const char* const* paths, uint64_t n, uint32_t mn, uint32_t av, uint32_t mx,
-                uint32_t lv, uint64_t fixed, uint64_t* c_off, uint64_t* c_len, uint64_t* dig, uint64_t capacity,
-                uint64_t* first_chunk, uint64_t* sizes, int32_t* status, int32_t* os_error) {
+// (files: paths; host buffers: paths == nullptr, bufs / lens)
+int run_sharded(oxh_ctx* const* ctxs, int nctx, const char* const* paths, const uint8_t* const* bufs, const uint64_t* lens,
+                uint64_t n, uint32_t mn, uint32_t av, uint32_t mx, uint32_t lv, uint64_t fixed, uint64_t* c_off,
+                uint64_t* c_len, uint64_t* dig, uint64_t capacity, uint64_t* first_chunk, uint64_t* sizes, int32_t* status,
+                int32_t* os_error) {
     if (!ctxs || nctx < 1) return oxh::set_error(OXH_ERR_INVALID, "no contexts");
     for (int k = 0; k < nctx; ++k)
         if (!ctxs[k]) return oxh::set_error(OXH_ERR_INVALID, "null context");
     if (!first_chunk) return oxh::set_error(OXH_ERR_INVALID, "null first_chunk");
-    if (n && !paths) return oxh::set_error(OXH_ERR_INVALID, "null paths");
-    for (uint64_t i = 0; i < n; ++i)
-        if (!paths[i]) return oxh::set_error(OXH_ERR_INVALID, "null path");
+    const bool files = paths != nullptr || bufs == nullptr;
+    if (files) {
+        if (n && !paths) return oxh::set_error(OXH_ERR_INVALID, "null paths");
+        for (uint64_t i = 0; i < n; ++i)
+            if (!paths[i]) return oxh::set_error(OXH_ERR_INVALID, "null path");
+    } else {
+        if (n && !lens) return oxh::set_error(OXH_ERR_INVALID, "null buffers");
+        for (uint64_t i = 0; i < n; ++i)
+            if (lens[i] && !bufs[i]) return oxh::set_error(OXH_ERR_INVALID, "null buffer");
+    }
     if (int rc = check_params(mn, av, mx, lv, fixed)) return rc;
     if (capacity && !fixed && (!c_off || !c_len)) return oxh::set_error(OXH_ERR_INVALID, "null chunk table");
     if (capacity && fixed && !dig) return oxh::set_error(OXH_ERR_INVALID, "null digests");
+    auto source = [&](uint64_t a, uint64_t m) -> std::unique_ptr<CdcSource> {
+        if (files) return std::unique_ptr<CdcSource>(new FileSrc(paths + a, m));
+        return std::unique_ptr<CdcSource>(new MemSrc(bufs + a, lens + a));
+    };
     if (nctx == 1 || n <= 1) {
-        FileSrc src(paths, n);
-        return run(ctxs[0], src, n, mn, av, mx, lv, fixed, c_off, c_len, dig, capacity, first_chunk, sizes, status, os_error);
+        auto src = source(0, n);
+        return run(ctxs[0], *src, n, mn, av, mx, lv, fixed, c_off, c_len, dig, capacity, first_chunk, sizes, status, os_error);
     }
     // sizes for the split (a file that cannot be stat'ed weighs nothing; its share reports it)
     std::vector<uint64_t> sz(n, 0);
-    {
+    if (!files) {
+        for (uint64_t i = 0; i < n; ++i) sz[i] = lens[i];
+    } else {
         std::vector<std::thread> th;
         const int nt = std::min<int>(nctx * 2, 16);
         for (int t = 0; t < nt; ++t)
@@ -821,9 +836,9 @@ int run_sharded(oxh_ctx* const* ctxs, int nctx, const char* const* paths, uint64
             if (!fixed) S.off.assign(cap, 0), S.len.assign(cap, 0);
             if (dig) S.dig.assign(2 * cap, 0);
             S.first.assign(m + 1, 0), S.sizes.assign(m, 0), S.st.assign(m, 0), S.oe.assign(m, 0);
-            FileSrc src(paths + a, m);
+            auto src = source(a, m);
             S.total = 0;
-            S.rc = run(ctxs[k], src, m, mn, av, mx, lv, fixed, fixed ? nullptr : S.off.data(), fixed ? nullptr : S.len.data(),
+            S.rc = run(ctxs[k], *src, m, mn, av, mx, lv, fixed, fixed ? nullptr : S.off.data(), fixed ? nullptr : S.len.data(),
                        dig ? S.dig.data() : nullptr, cap, S.first.data(), S.sizes.data(), S.st.data(), S.oe.data(), &S.total);
             if (S.rc == OXH_ERR_INVALID && S.total > cap) {
                 cap = S.total;
@@ -923,16 +938,32 @@ int oxh_fastcdc_files_multi(oxh_ctx* const* ctxs, int nctx, const char* const* p
                             uint32_t avg_size, uint32_t max_size, uint32_t level, uint64_t* chunk_offsets,
                             uint64_t* chunk_lens, uint64_t* digests, uint64_t capacity, uint64_t* first_chunk,
                             uint64_t* sizes, int32_t* status, int32_t* os_error) {
-    return run_sharded(ctxs, nctx, paths, n, min_size, avg_size, max_size, level, 0, chunk_offsets, chunk_lens, digests,
-                       capacity, first_chunk, sizes, status, os_error);
+    return run_sharded(ctxs, nctx, paths, nullptr, nullptr, n, min_size, avg_size, max_size, level, 0, chunk_offsets,
+                       chunk_lens, digests, capacity, first_chunk, sizes, status, os_error);
+}
+
+int oxh_fastcdc_host_multi(oxh_ctx* const* ctxs, int nctx, const uint8_t* const* bufs, const uint64_t* lens, uint64_t n,
+                           uint32_t min_size, uint32_t avg_size, uint32_t max_size, uint32_t level, uint64_t* chunk_offsets,
+                           uint64_t* chunk_lens, uint64_t* digests, uint64_t capacity, uint64_t* first_chunk) {
+    if (n && !bufs) return oxh::set_error(OXH_ERR_INVALID, "null buffers");
+    return run_sharded(ctxs, nctx, nullptr, bufs, lens, n, min_size, avg_size, max_size, level, 0, chunk_offsets, chunk_lens,
+                       digests, capacity, first_chunk, nullptr, nullptr, nullptr);
 }
 
 int oxh_chunk_digests_files_multi(oxh_ctx* const* ctxs, int nctx, const char* const* paths, uint64_t n,
                                   uint64_t chunk_size, uint64_t* digests, uint64_t capacity, uint64_t* first_chunk,
                                   uint64_t* sizes, int32_t* status, int32_t* os_error) {
     if (chunk_size == 0) return oxh::set_error(OXH_ERR_INVALID, "Chunk size cannot be zero");
-    return run_sharded(ctxs, nctx, paths, n, 0, 0, 0, 0, chunk_size, nullptr, nullptr, digests, capacity, first_chunk, sizes,
-                       status, os_error);
+    return run_sharded(ctxs, nctx, paths, nullptr, nullptr, n, 0, 0, 0, 0, chunk_size, nullptr, nullptr, digests, capacity,
+                       first_chunk, sizes, status, os_error);
+}
+
+int oxh_chunk_digests_host_multi(oxh_ctx* const* ctxs, int nctx, const uint8_t* const* bufs, const uint64_t* lens, uint64_t n,
+                                 uint64_t chunk_size, uint64_t* digests, uint64_t capacity, uint64_t* first_chunk) {
+    if (chunk_size == 0) return oxh::set_error(OXH_ERR_INVALID, "Chunk size cannot be zero");
+    if (n && !bufs) return oxh::set_error(OXH_ERR_INVALID, "null buffers");
+    return run_sharded(ctxs, nctx, nullptr, bufs, lens, n, 0, 0, 0, 0, chunk_size, nullptr, nullptr, digests, capacity,
+                       first_chunk, nullptr, nullptr, nullptr);
 }
 
 }  // extern "C"

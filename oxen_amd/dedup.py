@@ -199,11 +199,12 @@ def fastcdc_files(paths, min_size: int, avg_size: int, max_size: int, level: int
 
 
 def fastcdc_host(buffers, min_size: int, avg_size: int, max_size: int, level: int = 1, digests: bool = True,
-                 ctx: Optional[_capi.Context] = None) -> FastCdcTable:
-    """oxh_fastcdc_host: the same over host buffers (bytes / numpy uint8 arrays)."""
+                 ctx: Optional[_capi.Context] = None, ctxs=None) -> FastCdcTable:
+    """oxh_fastcdc_host: the same over host buffers (bytes / numpy uint8 arrays); ctxs: over several
+    contexts (oxh_fastcdc_host_multi)."""
     from .hasher import default_context
 
-    ctx = ctx or default_context()
+    ctx = ctx or (None if ctxs else default_context())
     arrs = [np.frombuffer(b, dtype=np.uint8) if isinstance(b, (bytes, bytearray, memoryview)) else np.ascontiguousarray(b, dtype=np.uint8)
             for b in buffers]
     n = len(arrs)
@@ -215,10 +216,13 @@ def fastcdc_host(buffers, min_size: int, avg_size: int, max_size: int, level: in
     ln = np.zeros(cap, dtype=np.uint64)
     dig = np.zeros((cap, 2), dtype=np.uint64) if digests else None
     first = np.zeros(n + 1, dtype=np.uint64)
-    _capi.check(L.oxh_fastcdc_host(ctx.handle, ptrs, lens_in.ctypes.data_as(_capi._u64p), n, int(min_size), int(avg_size),
-                                   int(max_size), int(level), off.ctypes.data_as(_capi._u64p), ln.ctypes.data_as(_capi._u64p),
-                                   dig.ctypes.data_as(_capi._u64p) if dig is not None else None, cap,
-                                   first.ctypes.data_as(_capi._u64p)), "oxh_fastcdc_host")
+    tail = (lens_in.ctypes.data_as(_capi._u64p), n, int(min_size), int(avg_size), int(max_size), int(level),
+            off.ctypes.data_as(_capi._u64p), ln.ctypes.data_as(_capi._u64p),
+            dig.ctypes.data_as(_capi._u64p) if dig is not None else None, cap, first.ctypes.data_as(_capi._u64p))
+    if ctxs:
+        _capi.check(L.oxh_fastcdc_host_multi(_ctx_array(ctxs), len(ctxs), ptrs, *tail), "oxh_fastcdc_host_multi")
+    else:
+        _capi.check(L.oxh_fastcdc_host(ctx.handle, ptrs, *tail), "oxh_fastcdc_host")
     total = int(first[n])
     return FastCdcTable(off[:total], ln[:total], dig[:total] if dig is not None else None, first)
 
@@ -282,13 +286,14 @@ def chunk_digests_files(paths, chunk_size: int, ctx: Optional[_capi.Context] = N
     raise _capi.OxenError("oxh_chunk_digests_files: the files keep growing", _capi.OXH_ERR_INVALID)
 
 
-def chunk_digests_host(buffers, chunk_size: int, ctx: Optional[_capi.Context] = None) -> FixedChunkTable:
-    """oxh_chunk_digests_host: the same over host buffers (bytes / numpy uint8 arrays)."""
+def chunk_digests_host(buffers, chunk_size: int, ctx: Optional[_capi.Context] = None, ctxs=None) -> FixedChunkTable:
+    """oxh_chunk_digests_host: the same over host buffers (bytes / numpy uint8 arrays); ctxs: over
+    several contexts (oxh_chunk_digests_host_multi)."""
     from .hasher import default_context
 
     if chunk_size <= 0:
         raise _capi.OxenError("Chunk size cannot be zero", _capi.OXH_ERR_INVALID)
-    ctx = ctx or default_context()
+    ctx = ctx or (None if ctxs else default_context())
     arrs = [np.frombuffer(b, dtype=np.uint8) if isinstance(b, (bytes, bytearray, memoryview)) else np.ascontiguousarray(b, dtype=np.uint8)
             for b in buffers]
     n = len(arrs)
@@ -297,9 +302,13 @@ def chunk_digests_host(buffers, chunk_size: int, ctx: Optional[_capi.Context] = 
     cap = max(1, _fixed_count(lens_in, chunk_size))
     dig = np.zeros((cap, 2), dtype=np.uint64)
     first = np.zeros(n + 1, dtype=np.uint64)
-    _capi.check(_capi.lib().oxh_chunk_digests_host(ctx.handle, ptrs, lens_in.ctypes.data_as(_capi._u64p), n, int(chunk_size),
-                                                   dig.ctypes.data_as(_capi._u64p), cap, first.ctypes.data_as(_capi._u64p)),
-                "oxh_chunk_digests_host")
+    tail = (lens_in.ctypes.data_as(_capi._u64p), n, int(chunk_size), dig.ctypes.data_as(_capi._u64p), cap,
+            first.ctypes.data_as(_capi._u64p))
+    if ctxs:
+        _capi.check(_capi.lib().oxh_chunk_digests_host_multi(_ctx_array(ctxs), len(ctxs), ptrs, *tail),
+                    "oxh_chunk_digests_host_multi")
+    else:
+        _capi.check(_capi.lib().oxh_chunk_digests_host(ctx.handle, ptrs, *tail), "oxh_chunk_digests_host")
     return FixedChunkTable(dig[:int(first[n])], first)
 
 

@@ -471,6 +471,13 @@ def test_files_multi_contexts(cuda, oracle_lib, tmp_path, monkeypatch, nctx):
             if len(want):
                 assert np.array_equal(dig, oracle_lib.batch(datas[k], want[:, 0], want[:, 1], threads=8)), i
             k += 1
+        # the host-buffer forms over the same contexts (shares balanced by length)
+        hone = dedup.fastcdc_host(datas, 4096, 8192, 16384, ctx=own[0])
+        hmany = dedup.fastcdc_host(datas, 4096, 8192, 16384, ctxs=ctxs)
+        for f in ("offsets", "lens", "digests", "first"):
+            assert np.array_equal(getattr(hone, f), getattr(hmany, f)), f
+        assert np.array_equal(dedup.chunk_digests_host(datas, 4096, ctx=own[0]).digests,
+                              dedup.chunk_digests_host(datas, 4096, ctxs=ctxs).digests)
         fone = dedup.chunk_digests_files(paths, 65_536, ctx=own[0])
         fmany = dedup.chunk_digests_files(paths, 65_536, ctxs=ctxs)
         for f in ("digests", "first", "sizes", "status", "os_error"):
