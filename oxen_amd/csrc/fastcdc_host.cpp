@@ -143,7 +143,7 @@ struct CdcHost {
         if (!ok) {
             (void)hipGetLastError();
             free_tables();
-            return oxh::set_error(OXH_ERR_NOMEM, "FastCDC chunk-table buffers");
+            return oxh::set_error(OXH_ERR_NOMEM, "host chunk pipeline: chunk-table buffers");
         }
         tab_cap = cap;
         return OXH_OK;
