@@ -13,7 +13,7 @@ if [ "${DEV:-0}" = 1 ]; then
     > gpurun_out/${T}_device_soak.json 2> gpurun_out/${T}_device_soak.err &
   DP=$!
 fi
-timeout -k 10 ${LIMIT:-150} env ${VARIANT_ENV:-OXH_NONE=0} python -u tools/engine_soak.py --seconds ${SECS:-60} --regrow ${SEED:+--seed $SEED} \
+timeout -k 10 ${LIMIT:-150} env ${VARIANT_ENV:-OXH_NONE=0} python -u tools/engine_soak.py --seconds ${SECS:-60} --regrow ${MUTATE:+--mutate} ${SEED:+--seed $SEED} \
   > gpurun_out/${T}_engine_soak.json 2> gpurun_out/${T}_engine_soak.err
 rc=$?
 echo "engine_soak rc=$rc"
