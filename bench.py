@@ -224,6 +224,9 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm); gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--gather", choices=["abi", "torch"], default="abi",
+                    help="N > 1 on RCCL: the digest gather through the C ABI (oxh_gather_digests, default) or "
+                         "torch.distributed's all-gather (the fallback when the ABI gather cannot come up)")
     ap.add_argument("--dist", action="store_true",
                     help="take the N>1 path (process group, pipelined RCCL gather) even at WORLD_SIZE=1: "
                          "rehearses the multi-GPU step on a one-GPU box under torch.distributed.run")
@@ -286,11 +289,33 @@ def main() -> None:
     # The gather is the C ABI's oxh_gather_digests (comm.py / csrc/comm.cpp: RCCL all-gather over xGMI),
     # the call a Rust host links; rank 0's communicator id travels over the process group.
     comm = None
+    gather_via = "none"
     if multi and args.backend == "nccl":
         from oxen_amd.comm import comm_from_process_group
 
-        comm = comm_from_process_group(rank, world, dev.index)
-    pipe = PipelinedGather(n_items, world, dev, comm=comm) if comm is not None else None
+        err = None
+        try:
+            if args.gather == "torch":
+                raise RuntimeError("--gather torch")
+            comm = comm_from_process_group(rank, world, dev.index)
+        except Exception as e:  # noqa: BLE001 -- decided below, by every rank together
+            err = e
+        # every rank takes the same path: the ABI gather only if it came up on all of them
+        ok = torch.tensor([0 if err is None else 1], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok)
+        if int(ok.item()):
+            if err is not None:
+                log(f"[bench] rank {rank}: oxh_comm_create failed ({err})")
+            if comm is not None:
+                comm.close()
+                comm = None
+            why = "--gather torch" if args.gather == "torch" else "the ABI gather failed to come up"
+            if args.gather != "torch":
+                log("[bench] the ABI gather is unavailable on some rank: torch's all-gather over the process group instead")
+            gather_via = f"torch.distributed all_gather_into_tensor (RCCL; {why})"
+        else:
+            gather_via = "oxh_gather_digests"
+    pipe = PipelinedGather(n_items, world, dev, comm=comm) if (comm is not None or gather_via.startswith("torch")) else None
 
     def step():
         if pipe is not None:
@@ -407,7 +432,7 @@ def main() -> None:
             "data": "synthetic (splitmix64 byte stream, seed %d+rank), device-resident in HBM" % args.seed,
             "config": {"workload": desc, "items_per_gpu": n_items, "item_bytes": item_len,
                        "bytes_per_gpu": bytes_per_rank, "parallelism": (f"files sharded x{world}, one RCCL all-gather of the digests per step "
-                                               f"({'oxh_gather_digests' if comm is not None else 'torch gloo rehearsal'})")
+                                               f"({gather_via if gather_via != 'none' else 'torch gloo rehearsal'})")
                        if multi else "single GPU",
                        "kernel_variant": args.variant or "auto (8: 2-round ring, items > 16 KiB)"},
             "roofline": roofline,
