@@ -113,3 +113,22 @@ def test_should_restore_errors(cuda, oracle_lib, tmp_path):
     assert restore.should_restore([str(f)], [n], [None], [True]) == [True]  # short cut: no read
     with pytest.raises(_capi.OxenError, match="lengths differ"):
         restore.should_restore([str(f)], [n, n], [None], [True])
+
+
+def test_should_restore_short_cuts_need_no_device(tmp_path):
+    """Missing working files and the mtime + size short cut decide without reading anything (no GPU
+    call is made: this runs on the CPU), and argument lengths are checked first."""
+    from oxen_amd import _capi, restore
+    from oxen_amd.restore import NodeHashes
+
+    f = tmp_path / "same_size.txt"
+    f.write_bytes(b"12345")
+    t = NodeHashes(hash=1, num_bytes=5, combined_hash=1)
+    b = NodeHashes(hash=2, num_bytes=5, combined_hash=2)
+    got = restore.should_restore([str(tmp_path / "missing"), str(f), str(f)], [t, t, t], [None, b, None],
+                                 [False, True, True])
+    assert got == [True, True, True]
+    for combined in (False, True):
+        assert restore.should_restore([], [], [], [], combined=combined) == []
+    with pytest.raises(_capi.OxenError, match="lengths differ"):
+        restore.should_restore([str(f)], [t], [None, None], [True])
