@@ -218,6 +218,8 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--prewarm-s", type=float, default=0.5,
+                    help="seconds of untimed hashing before the warmup steps (clock ramp); 0 = off")
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
@@ -331,6 +333,18 @@ def main() -> None:
         if pipe is not None:
             pipe.drain()
 
+    # Clock ramp: the first bench process on a fresh box ran K1 2-4 % slow when only the W warmup steps
+    # (a few ms of work) came before the timed region (profiles/r05/r05v_*, r05u_*). Hash the same
+    # tables for prewarm_s seconds first (untimed; its launch count goes into the JSON line so the
+    # profile summary can find the timed launches), then the W warmup steps and the K timed steps.
+    t_pre = time.perf_counter()
+    prewarm_launches = 0
+    while time.perf_counter() - t_pre < args.prewarm_s:
+        for _ in range(8):
+            da.hash(out)
+        prewarm_launches += 8
+        torch.cuda.synchronize()
+    prewarm_s = time.perf_counter() - t_pre
     for _ in range(args.warmup):
         step()
     drain()
@@ -436,6 +450,8 @@ def main() -> None:
                        if multi else "single GPU",
                        "kernel_variant": args.variant or "auto (8: 2-round ring, items > 16 KiB)"},
             "roofline": roofline,
+            "prewarm": {"seconds": round(prewarm_s, 3), "launches": prewarm_launches,
+                        "what": "untimed K1 launches over the same tables before the warmup steps (clock ramp)"},
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)

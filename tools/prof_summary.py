@@ -8,8 +8,9 @@ call dropped), the bench line that same profiled process printed (its ms_per_ste
 tracer's overhead, so avg_ms <= ms_per_step holds for the same invocation), and the roofline fraction
 bytes / avg / 8 TB/s. bench.py reads the newest such file and reports it next to its HIP-event figure.
 With --trace (the same run's kernel_trace.csv) it also reports the launches of the timed region alone:
-bench.py dispatches W warm-up launches, then the K timed ones (then the per-launch probes), so
-launches W .. W+K-1 in dispatch order are the ones ms_per_step covers; the process's first launch
+bench.py dispatches its pre-warm launches (their count is in its JSON line), W warm-up launches, then
+the K timed ones (then the per-launch probes), so
+launches P+W .. P+W+K-1 in dispatch order (P pre-warm) are the ones ms_per_step covers; the process's first launch
 (cold code and TLB) is the slowest of all and is not among them.
 """
 from __future__ import annotations
@@ -56,10 +57,12 @@ def main():
     if a.trace:
         tr = sorted((int(r["Dispatch_Id"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
                     for r in csv.DictReader(open(a.trace)) if a.kernel in r["Kernel_Name"])
-        timed = [d for _, d in tr[a.warmup:a.warmup + a.steps]]
-        assert len(timed) == a.steps, "trace holds fewer launches than warm-up + steps"
+        # bench.py's untimed pre-warm launches (r05) come first, then W warm-up, then the K timed ones
+        skip = int(bench.get("prewarm", {}).get("launches", 0)) + a.warmup
+        timed = [d for _, d in tr[skip:skip + a.steps]]
+        assert len(timed) == a.steps, "trace holds fewer launches than pre-warm + warm-up + steps"
         t_ms = sum(timed) / len(timed) / 1e6
-        res["timed_region"] = {"launches": f"{a.warmup}..{a.warmup + a.steps - 1} in dispatch order",
+        res["timed_region"] = {"launches": f"{skip}..{skip + a.steps - 1} in dispatch order",
                                "avg_ms": round(t_ms, 5), "frac": round(nbytes / (t_ms / 1e3) / 1e9 / 8000.0, 4),
                                "avg_le_ms_per_step": t_ms <= bench["ms_per_step"],
                                "first_launch_ms": round(tr[0][1] / 1e6, 5)}
