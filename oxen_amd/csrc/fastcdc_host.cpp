@@ -595,6 +595,11 @@ int run(oxh_ctx* ctx, CdcSource& src, uint64_t n, uint32_t mn, uint32_t av, uint
     if (capacity && !fixed && (!c_off || !c_len)) return oxh::set_error(OXH_ERR_INVALID, "null chunk table");
     if (capacity && fixed && !dig) return oxh::set_error(OXH_ERR_INVALID, "null digests");
     if (int rc = check_params(mn, av, mx, lv, fixed)) return rc;
+    if (n == 0) {  // nothing to read: no pipeline buffers for an empty call
+        first_chunk[0] = 0;
+        if (total_out) *total_out = 0;
+        return OXH_OK;
+    }
     uint64_t min_seg = 0;
     if (fixed) {
         // a segment is whole chunks: at least one, and 16 MiB when the chunks are smaller (within the

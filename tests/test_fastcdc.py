@@ -677,3 +677,21 @@ def test_fastcdc_host_levels(cuda, oracle_lib, monkeypatch, level):
     for mn, av, mx in [(4096, 8192, 16384), (4096, 65536, 131072)]:
         tab = dedup.fastcdc_host(datas, mn, av, mx, level=level)
         _check_table(oracle_lib, tab, datas, mn, av, mx, level=level)
+
+
+@pytest.mark.gpu
+def test_host_chunk_entries_empty_calls(cuda):
+    """n = 0 on every host chunk entry (one context and several): first_chunk = [0], nothing read and
+    no pipeline buffers made."""
+    from oxen_amd import _capi, dedup
+
+    ctxs = [_capi.Context(0), _capi.Context(0)]
+    try:
+        for kw in ({"ctx": ctxs[0]}, {"ctxs": ctxs}):
+            assert list(dedup.fastcdc_files([], 4096, 8192, 16384, **kw).first) == [0]
+            assert list(dedup.fastcdc_host([], 4096, 8192, 16384, **kw).first) == [0]
+            assert list(dedup.chunk_digests_files([], 4096, **kw).first) == [0]
+            assert list(dedup.chunk_digests_host([], 4096, **kw).first) == [0]
+    finally:
+        for c in ctxs:
+            c.close()
