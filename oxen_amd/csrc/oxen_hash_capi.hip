@@ -116,6 +116,8 @@ WaveKernel wave_kernel_for(int variant) {
         case 768: return oxh::xxh3_wave_kernel<DESC, 768>;
         case 772: return oxh::xxh3_wave_kernel<DESC, 772>;
         case 776: return oxh::xxh3_wave_kernel<DESC, 776>;
+        case 1032: return oxh::xxh3_wave_kernel<DESC, 1032>;
+        case 1024: return oxh::xxh3_wave_kernel<DESC, 1024>;
 #endif
         default: return oxh::xxh3_wave_kernel<DESC, 0>;
     }
@@ -158,7 +160,7 @@ int known_variant(int v) {
         case 8: case 72: case 104: case 264: return v;
 #ifdef OXH_PROBE_VARIANTS
         case 1: case 2: case 4: case 12: case 40: case 64: case 74:
-        case 256: case 260: case 768: case 772: case 776: return v;
+        case 256: case 260: case 768: case 772: case 776: case 1024: case 1032: return v;
 #endif
         default: return 0;
     }

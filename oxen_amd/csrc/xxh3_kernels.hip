@@ -99,6 +99,10 @@ __device__ __forceinline__ void bcast_rows64(uint64_t x, uint64_t t[4], int lane
 //   bit 8     1 = K1R, one 16-lane row per item and four items per wave (rows_item below; bits 1-3
 //             as above, the others unused)
 //   bit 9     K1R only: 1 = K1H, two rows per item and two items per wave
+//   bit 10    1 = rotated start (K1 only): item i visits its first min(nr, 16) full rounds starting at
+//             round i % 16, stashing the block sums of the rounds it reads before round 0 in LDS and
+//             replaying them into the chain in order -- so the waves in flight, whose items all start
+//             on 64 KiB boundaries in C2's arena, read at addresses 4 KiB apart instead of in lockstep
 // Measured on MI355X (C2, tools/readbw.py, profiles/r01_readbw*.json): nt loads ~+11 % over
 // default-policy loads; 4 rounds in flight (2 waves/SIMD at 180 VGPRs) ~+4 % over 2 rounds (5 waves/SIMD).
 template <int V>
@@ -111,6 +115,7 @@ struct Cfg {
     static constexpr bool BLOCKWISE = ((V >> 5) & 1) != 0;
     static constexpr bool ROWS = ((V >> 8) & 1) != 0;
     static constexpr bool ROWS2 = ((V >> 9) & 1) != 0;
+    static constexpr bool ROT = ((V >> 10) & 1) != 0;
 };
 
 template <bool ALIGNED, bool NT = false>
@@ -225,7 +230,8 @@ __device__ __forceinline__ uint4 bload16(__amdgpu_buffer_rsrc_t rsrc, uint32_t v
 template <int VARIANT, bool TEXT, bool BS>
 __device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_t len,
                                           uint64_t* __restrict__ out, int lane, const uint64_t* lds_sec,
-                                          uint64_t* __restrict__ counts, uint32_t bs = 0) {
+                                          uint64_t* __restrict__ counts, uint32_t bs = 0, uint64_t* stash = nullptr,
+                                          uint64_t phase = 0) {
     constexpr bool BW = Cfg<VARIANT>::BLOCKWISE;
     constexpr uint32_t JSTRIDE = BW ? 1024u : 256u;  // bytes between a lane's loads j and j+1
     const int g = lane >> 4, q = (lane >> 2) & 3, k = lane & 3;
@@ -339,6 +345,56 @@ __device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_
         }
         fold_round<Cfg<VARIANT>::BCAST>(s0, s1, a0, a1, sk0, sk1, partial ? (int)(nb - nr * 4) : 4, lane);
     };
+    // ROT: visit v of the full rounds reads round seq(v). With phi > 0 the first wr - phi visits read
+    // rounds phi .. wr-1 and stash their block sums (slot v), the next phi read rounds 0 .. phi-1 into
+    // the chain, and the stash is then replayed in order; visits from wr on read round v.
+    constexpr bool ROT = Cfg<VARIANT>::ROT && !BW;
+    const uint64_t wr = ROT ? (nr < 16 ? nr : 16) : 0;
+    const uint64_t phi = (ROT && wr >= 2) ? phase % wr : 0;
+    auto seq = [&](uint64_t v) -> uint64_t {
+        if (!ROT || phi == 0 || v >= wr) return v;
+        return v < wr - phi ? phi + v : v - (wr - phi);
+    };
+    // a full round's block sums: row g's lanes q == 0 hold block g's, accumulators (2k, 2k + 1)
+    auto stash4 = [&](uint4 (&src)[4], uint32_t ext, uint64_t slot) {
+        realign(src, ext);
+        uint64_t s0 = 0, s1 = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint64_t k0, k1;
+            keys(j, k0, k1);
+            accum16(src[j], k0, k1, s0, s1);
+            if constexpr (TEXT) count16(src[j], n_nl, n_cont);
+        }
+        s0 += dpp64<DPP_ROW_ROR4>(s0);
+        s1 += dpp64<DPP_ROW_ROR4>(s1);
+        s0 += dpp64<DPP_ROW_ROR8>(s0);
+        s1 += dpp64<DPP_ROW_ROR8>(s1);
+        if (q == 0) {
+            const uint32_t at = (uint32_t)(((slot * 4 + (uint64_t)g) * 4 + (uint64_t)k) * 2);
+            stash[at] = s0;
+            stash[at + 1] = s1;
+        }
+    };
+    auto replay = [&]() {
+        for (uint64_t slot = 0; slot < wr - phi; ++slot) {
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg) {
+                const uint32_t at = (uint32_t)(((slot * 4 + (uint64_t)gg) * 4 + (uint64_t)k) * 2);
+                a0 = scramble1(a0 + stash[at], sk0);
+                a1 = scramble1(a1 + stash[at + 1], sk1);
+            }
+        }
+    };
+    // fold visit v (a full round), replaying the stash after the window's last visit
+    auto visit = [&](uint4 (&src)[4], uint32_t ext, uint64_t v) {
+        if (ROT && phi != 0 && v < wr - phi) {
+            stash4(src, ext, v);
+        } else {
+            fold4(src, ext, seq(v), false);
+            if (ROT && phi != 0 && v == wr - 1) replay();
+        }
+    };
     // the last stripe (at len - 64, secret offset 121) is fetched up front with the first rounds
     const __amdgpu_buffer_rsrc_t rsrc_last =
         __builtin_amdgcn_make_buffer_rsrc((void*)(p + len - 64), (short)0, 64, kRsrcFlags);
@@ -352,13 +408,14 @@ __device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_
         uint4 ring[D][4];
         uint32_t ext[D];
 #pragma unroll
-        for (int d = 0; d < D; ++d) load_round((uint64_t)d, ring[d], ext[d]);
+        for (int d = 0; d < D; ++d) load_round(seq((uint64_t)d), ring[d], ext[d]);
         uint64_t r = 0;
         for (; r + D <= nr; r += D) {  // every slot holds a full round
 #pragma unroll
             for (int d = 0; d < D; ++d) {
-                fold4(ring[d], ext[d], r + d, false);
-                load_round(r + d + D, ring[d], ext[d]);
+                if constexpr (ROT) visit(ring[d], ext[d], r + d);
+                else fold4(ring[d], ext[d], r + d, false);
+                load_round(seq(r + d + D), ring[d], ext[d]);
                 // keep slot d+1's arithmetic below this point: otherwise the scheduler hoists its
                 // data-only adds above the refill and hipcc has to drain every load (vmcnt(0))
                 __builtin_amdgcn_sched_barrier(0);
@@ -367,8 +424,12 @@ __device__ __forceinline__ void wave_long(const uint8_t* __restrict__ p, uint64_
         // rounds r .. nr (at most D, the last one partial) are already in slots 0 .. nr - r
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            if (r + d < nr) fold4(ring[d], ext[d], r + d, false);
-            else if (r + d == nr) fold4(ring[d], ext[d], r + d, true);
+            if (r + d < nr) {
+                if constexpr (ROT) visit(ring[d], ext[d], r + d);
+                else fold4(ring[d], ext[d], r + d, false);
+            } else if (r + d == nr) {
+                fold4(ring[d], ext[d], r + d, true);
+            }
         }
     }
     // last stripe, at len - 64, with the secret shifted to offset 121
@@ -432,6 +493,8 @@ __device__ __forceinline__ void wave_item(const uint8_t* __restrict__ arena, con
                                           const uint64_t* __restrict__ lens, uint64_t n, uint64_t chunk,
                                           uint64_t total, uint64_t* __restrict__ out, uint64_t* __restrict__ counts) {
     __shared__ uint64_t lds_sec[24];
+    // ROT: 16 rounds x 4 blocks x 8 accumulators per wave (4 waves per workgroup at most)
+    __shared__ uint64_t rot_stash[Cfg<VARIANT>::ROT ? 4 * 16 * 32 : 1];
     if constexpr (Cfg<VARIANT>::KEYS_LDS) {
         if (threadIdx.x < 24) lds_sec[threadIdx.x] = kSecW[threadIdx.x];
         __syncthreads();
@@ -478,8 +541,11 @@ __device__ __forceinline__ void wave_item(const uint8_t* __restrict__ arena, con
     const uint32_t bs = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
     const uint64_t nb_ = (len - 1) >> 10;
     const uint64_t E = (nb_ << 10) + ((((len - 1) - (nb_ << 10)) >> 6) << 6);
-    if (bs && len - E >= 4) wave_long<VARIANT, TEXT, true>(p, len, o, lane, lds_sec, TEXT ? counts + 2 * item : nullptr, bs);
-    else wave_long<VARIANT, TEXT, false>(p, len, o, lane, lds_sec, TEXT ? counts + 2 * item : nullptr);
+    uint64_t* stash = Cfg<VARIANT>::ROT ? rot_stash + (threadIdx.x >> 6) * (16 * 32) : nullptr;
+    if (bs && len - E >= 4)
+        wave_long<VARIANT, TEXT, true>(p, len, o, lane, lds_sec, TEXT ? counts + 2 * item : nullptr, bs, stash, item);
+    else
+        wave_long<VARIANT, TEXT, false>(p, len, o, lane, lds_sec, TEXT ? counts + 2 * item : nullptr, 0, stash, item);
 }
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
@@ -1100,6 +1166,10 @@ template __global__ void xxh3_wave_kernel<true, 772>(const uint8_t*, const uint6
 template __global__ void xxh3_wave_kernel<false, 772>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 template __global__ void xxh3_wave_kernel<true, 776>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 template __global__ void xxh3_wave_kernel<false, 776>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<true, 1032>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<false, 1032>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<true, 1024>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
+template __global__ void xxh3_wave_kernel<false, 1024>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*);
 #endif
 template __global__ void xxh3_text_wave_kernel<72>(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t*, uint64_t*);
 template __global__ void xxh3_blocksum_kernel<true>(const uint8_t*, uint64_t, uint64_t*);
