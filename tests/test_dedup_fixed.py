@@ -1,6 +1,7 @@
 """The fixed-size dedup chunkers (experiments/block-level-dedup/src/chunker/fixedsize.rs and
 fixedsize_multithreaded.rs) over the GPU chunk-digest kernel, against a restatement of those files'
 pack loops over the oracle: the same chunk files, the same metadata.bin bytes, unpack round trips."""
+import ctypes
 import os
 import struct
 
@@ -254,3 +255,30 @@ def test_chunker_test_command_fixed_size_reads(cuda, tmp_path):
     # fastcdc's unpack is the reference's stub: nothing at unpacked_output, the hash fails (ENOENT)
     with pytest.raises(_capi.OxenError, match="Failed to hash unpacked file"):
         dedup.run_chunker_test("fastcdc", 8192, str(src), str(tmp_path))
+
+
+@pytest.mark.gpu
+def test_chunk_digests_capacity_errors(cuda, tmp_path):
+    """A digest table too small fails the call with OXH_ERR_INVALID and the count it needs (the caller
+    retries with it, as dedup.chunk_digests_files does for a file that grew); no entry past capacity is
+    written."""
+    from oxen_amd import _capi
+    from oxen_amd.hasher import _PathTable, default_context
+
+    data = np.random.default_rng(3).integers(0, 256, 10 * 4096 + 5, dtype=np.uint8).tobytes()
+    p = tmp_path / "f.bin"
+    p.write_bytes(data)
+    L = _capi.lib()
+    ctx = default_context()
+    table = _PathTable([str(p)])
+    dig = np.full((8, 2), 7, dtype=np.uint64)
+    first = np.zeros(2, dtype=np.uint64)
+    rc = L.oxh_chunk_digests_files(ctx.handle, table.arg, 1, 4096, dig.ctypes.data_as(_capi._u64p), 5,
+                                   first.ctypes.data_as(_capi._u64p), None, None, None)
+    assert rc == _capi.OXH_ERR_INVALID and b"need 11 entries" in L.oxh_last_error()
+    assert (dig[5:] == 7).all()  # nothing past the capacity
+    bufs = (ctypes.c_char_p * 1)(data)
+    lens = np.array([len(data)], dtype=np.uint64)
+    rc = L.oxh_chunk_digests_host(ctx.handle, bufs, lens.ctypes.data_as(_capi._u64p), 1, 4096,
+                                  dig.ctypes.data_as(_capi._u64p), 3, first.ctypes.data_as(_capi._u64p))
+    assert rc == _capi.OXH_ERR_INVALID and b"need 11 entries" in L.oxh_last_error()
