@@ -1485,7 +1485,6 @@ uint32_t log2_round(uint32_t v) {
     return (x * x >= 2.0 * lo * lo) ? b + 1 : b;
 }
 
-// stream-ordered scratch, freed on every exit path
 // Per-call scratch (candidate lists, speculative starts, stitch tables) carved out of the device's
 // cached scratch buffer (scratch.hpp).
 struct Scratch {
