@@ -1,8 +1,9 @@
 """Soak of the host chunking entries against the C oracle: FastCDC (oxh_fastcdc_files / _host) and
 fixed-size chunks (oxh_chunk_digests_files / _host) over random file sets (empty, tiny, around min /
 avg / max, a few MiB to 200 MiB, constant runs), random chunk parameters and piece sizes
-(OXH_CDC_PIECE_MIB changes the context's pipeline between iterations), the four entries in turn, half
-the iterations on one long-lived context; every boundary and digest checked. Prints one JSON object.
+(OXH_CDC_PIECE_MIB changes the context's pipeline between iterations), the four entries in turn, a third
+of the iterations on a fresh context, a third on one long-lived context, a third over two contexts
+(the _multi entries); every boundary and digest checked. Prints one JSON object.
 
     python tools/cdc_host_soak.py --seconds 120 [--dir /tmp/oxh_soak]
 """
@@ -44,6 +45,7 @@ def main():
     failures = []
     last = time.time()
     shared = _capi.Context(0)
+    shared2 = _capi.Context(0)  # with `shared`: the _multi entries over two contexts
     while time.time() < t_end:
         entry = ("files", "host", "fixed_files", "fixed_host")[it % 4]
         fixed = int(rng.choice(FIXED))
@@ -71,8 +73,10 @@ def main():
                 lo = int(rng.integers(0, size))
                 d[lo:lo + int(rng.integers(1, 3 * mx))] = int(rng.integers(256))
             datas.append(d)
-        own = (it // 4) % 2 == 0
+        own = (it // 4) % 3 == 0
+        multi = (it // 4) % 3 == 2  # one context per share (oxh_*_multi), both long-lived
         ctx = _capi.Context(0) if own else shared
+        kw = {"ctxs": [shared, shared2]} if multi else {"ctx": ctx}
         try:
             if entry in ("files", "fixed_files"):
                 paths = []
@@ -81,15 +85,15 @@ def main():
                     d.tofile(p)
                     paths.append(p)
                 if entry == "files":
-                    tab = dedup.fastcdc_files(paths, mn, av, mx, ctx=ctx)
+                    tab = dedup.fastcdc_files(paths, mn, av, mx, **kw)
                 else:
-                    tab = dedup.chunk_digests_files(paths, fixed, ctx=ctx)
+                    tab = dedup.chunk_digests_files(paths, fixed, **kw)
                 if not (tab.status == 0).all():
                     failures.append({"it": it, "what": "status", "status": tab.status.tolist()})
             elif entry == "host":
-                tab = dedup.fastcdc_host(datas, mn, av, mx, ctx=ctx)
+                tab = dedup.fastcdc_host(datas, mn, av, mx, **kw)
             else:
-                tab = dedup.chunk_digests_host(datas, fixed, ctx=ctx)
+                tab = dedup.chunk_digests_host(datas, fixed, **kw)
         finally:
             if own:
                 ctx.close()
@@ -106,7 +110,7 @@ def main():
             if ok and len(want):
                 ok = np.array_equal(dig, oracle.batch(d, want[:, 0], want[:, 1], threads=8))
             if not ok:
-                failures.append({"it": it, "file": i, "size": int(d.size), "piece_mib": piece, "entry": entry,
+                failures.append({"it": it, "file": i, "size": int(d.size), "piece_mib": piece, "entry": entry, "multi": multi,
                                  "params": [fixed] if entry.startswith("fixed") else [mn, av, mx]})
             files_checked += 1
             chunks_checked += len(want)
@@ -117,6 +121,7 @@ def main():
                   file=sys.stderr, flush=True)
             last = time.time()
     shared.close()
+    shared2.close()
     shutil.rmtree(a.dir, ignore_errors=True)
     print(json.dumps({"iterations": it, "files_checked": files_checked, "chunks_checked": chunks_checked,
                       "bytes_checked": bytes_checked, "failures": failures[:20], "n_failures": len(failures)}),
