@@ -818,35 +818,56 @@ int run_sharded(oxh_ctx* const* ctxs, int nctx, const char* const* paths, const 
         }
         while (k < nctx) lo[k++] = n;
     }
+    // Each share writes its chunks straight into the caller's arrays, into a region of its own bound
+    // (the same bound the one-context call is sized by), when the capacity holds every share's
+    // bound; the regions are then moved down into one contiguous table. A share whose files grew past
+    // their bound (or a capacity below the bounds' sum) uses tables of its own instead.
     struct Share {
         std::vector<uint64_t> off, len, dig, first, sizes;
         std::vector<int32_t> st, oe;
-        uint64_t total = 0;
+        uint64_t cap = 0, start = 0, total = 0;
+        bool inplace = false;
         int rc = OXH_OK;
         std::string err;
     };
     std::vector<Share> sh(nctx);
+    uint64_t bound_sum = 0;
+    for (int k = 0; k < nctx; ++k) {
+        Share& S = sh[k];
+        const uint64_t a = lo[k], m = lo[k + 1] - a;
+        if (fixed) {
+            for (uint64_t i = a; i < a + m; ++i) S.cap += (sz[i] + fixed - 1) / fixed;
+        } else {
+            S.cap += oxh_fastcdc_max_chunks(sz.data() + a, m, mn);
+        }
+        S.start = bound_sum;
+        bound_sum += S.cap;
+    }
+    const bool inplace = bound_sum <= capacity;
     auto work = [&](int k) {
         Share& S = sh[k];
         const uint64_t a = lo[k], m = lo[k + 1] - a;
         S.first.assign(m + 1, 0);
         if (m == 0) return;  // (more contexts than files)
-        uint64_t cap = 1;
-        if (fixed) {
-            for (uint64_t i = a; i < a + m; ++i) cap += (sz[i] + fixed - 1) / fixed;
-        } else {
-            cap += oxh_fastcdc_max_chunks(sz.data() + a, m, mn);
-        }
+        uint64_t cap = S.cap;
+        S.inplace = inplace;
         for (int attempt = 0; attempt < 3; ++attempt) {  // a file that grew since its stat: retry with the count
-            if (!fixed) S.off.assign(cap, 0), S.len.assign(cap, 0);
-            if (dig) S.dig.assign(2 * cap, 0);
+            uint64_t *o = nullptr, *l = nullptr, *d = nullptr;
+            if (S.inplace) {
+                if (!fixed) o = c_off + S.start, l = c_len + S.start;
+                if (dig) d = dig + 2 * S.start;
+            } else {
+                if (!fixed) S.off.assign(cap, 0), S.len.assign(cap, 0), o = S.off.data(), l = S.len.data();
+                if (dig) S.dig.assign(2 * cap, 0), d = S.dig.data();
+            }
             S.first.assign(m + 1, 0), S.sizes.assign(m, 0), S.st.assign(m, 0), S.oe.assign(m, 0);
             auto src = source(a, m);
             S.total = 0;
-            S.rc = run(ctxs[k], *src, m, mn, av, mx, lv, fixed, fixed ? nullptr : S.off.data(), fixed ? nullptr : S.len.data(),
-                       dig ? S.dig.data() : nullptr, cap, S.first.data(), S.sizes.data(), S.st.data(), S.oe.data(), &S.total);
+            S.rc = run(ctxs[k], *src, m, mn, av, mx, lv, fixed, o, l, d, cap, S.first.data(), S.sizes.data(), S.st.data(),
+                       S.oe.data(), &S.total);
             if (S.rc == OXH_ERR_INVALID && S.total > cap) {
                 cap = S.total;
+                S.inplace = false;  // past its region: tables of its own
                 continue;
             }
             break;
@@ -863,6 +884,20 @@ int run_sharded(oxh_ctx* const* ctxs, int nctx, const char* const* paths, const 
         if (sh[k].rc != OXH_OK)
             return oxh::set_error(sh[k].rc, "share " + std::to_string(k) + " (files " + std::to_string(lo[k]) + ".." +
                                                 std::to_string(lo[k + 1]) + "): " + sh[k].err);
+    // a share that left its region may overrun the next one's while the tables are joined: then every
+    // in-place share's chunks are copied out first
+    bool any_own = false;
+    for (const Share& S : sh) any_own = any_own || (!S.inplace && S.total);
+    if (inplace && any_own)
+        for (Share& S : sh)
+            if (S.inplace && S.total) {
+                if (!fixed) {
+                    S.off.assign(c_off + S.start, c_off + S.start + S.total);
+                    S.len.assign(c_len + S.start, c_len + S.start + S.total);
+                }
+                if (dig) S.dig.assign(dig + 2 * S.start, dig + 2 * (S.start + S.total));
+                S.inplace = false;
+            }
     uint64_t base = 0;
     for (int k = 0; k < nctx; ++k) {
         const Share& S = sh[k];
@@ -874,11 +909,21 @@ int run_sharded(oxh_ctx* const* ctxs, int nctx, const char* const* paths, const 
             if (os_error) os_error[a + i] = S.oe[i];
         }
         const uint64_t keep = base < capacity ? std::min(S.total, capacity - base) : 0;
-        if (keep && !fixed) {
-            memcpy(c_off + base, S.off.data(), keep * 8);
-            memcpy(c_len + base, S.len.data(), keep * 8);
+        if (keep && S.inplace) {  // down to its place in the joined table (base <= start: memmove)
+            if (base != S.start) {
+                if (!fixed) {
+                    memmove(c_off + base, c_off + S.start, keep * 8);
+                    memmove(c_len + base, c_len + S.start, keep * 8);
+                }
+                if (dig) memmove(dig + 2 * base, dig + 2 * S.start, keep * 16);
+            }
+        } else if (keep) {
+            if (!fixed) {
+                memcpy(c_off + base, S.off.data(), keep * 8);
+                memcpy(c_len + base, S.len.data(), keep * 8);
+            }
+            if (dig) memcpy(dig + 2 * base, S.dig.data(), keep * 16);
         }
-        if (keep && dig) memcpy(dig + 2 * base, S.dig.data(), keep * 16);
         base += S.total;
     }
     first_chunk[n] = base;

@@ -471,6 +471,23 @@ def test_files_multi_contexts(cuda, oracle_lib, tmp_path, monkeypatch, nctx):
             if len(want):
                 assert np.array_equal(dig, oracle_lib.batch(datas[k], want[:, 0], want[:, 1], threads=8)), i
             k += 1
+        # a capacity of exactly the chunk count (below the shares' bounds): each share then fills tables
+        # of its own and the call joins them -- the same table as the in-place form above
+        from oxen_amd.hasher import _PathTable
+
+        tot = int(one.first[-1])
+        off = np.zeros(tot, dtype=np.uint64)
+        ln = np.zeros(tot, dtype=np.uint64)
+        dg = np.zeros((tot, 2), dtype=np.uint64)
+        first = np.zeros(len(paths) + 1, dtype=np.uint64)
+        arr = (ctypes.c_void_p * len(ctxs))(*[c.handle.value for c in ctxs])
+        table = _PathTable(paths)
+        _capi.check(_capi.lib().oxh_fastcdc_files_multi(arr, len(ctxs), table.arg, len(paths), 4096, 8192, 16384, 1,
+                                                        off.ctypes.data_as(_capi._u64p), ln.ctypes.data_as(_capi._u64p),
+                                                        dg.ctypes.data_as(_capi._u64p), tot,
+                                                        first.ctypes.data_as(_capi._u64p), None, None, None), "multi exact")
+        assert np.array_equal(first, one.first) and np.array_equal(off, one.offsets)
+        assert np.array_equal(ln, one.lens) and np.array_equal(dg, one.digests)
         # the host-buffer forms over the same contexts (shares balanced by length)
         hone = dedup.fastcdc_host(datas, 4096, 8192, 16384, ctx=own[0])
         hmany = dedup.fastcdc_host(datas, 4096, 8192, 16384, ctxs=ctxs)
