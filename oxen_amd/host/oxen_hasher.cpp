@@ -748,7 +748,13 @@ std::vector<ChunkedFile> fastcdc_files(const std::vector<std::string>& paths, ui
 
 std::vector<std::vector<Chunk>> fastcdc_buffers(const std::vector<std::string_view>& buffers, uint32_t min_size,
                                                 uint32_t avg_size, uint32_t max_size, oxh_ctx* ctx) {
-    ctx = ctx ? ctx : util::hasher::default_context();
+    return fastcdc_buffers(buffers, min_size, avg_size, max_size,
+                           std::vector<oxh_ctx*>{ctx ? ctx : util::hasher::default_context()});
+}
+
+std::vector<std::vector<Chunk>> fastcdc_buffers(const std::vector<std::string_view>& buffers, uint32_t min_size,
+                                                uint32_t avg_size, uint32_t max_size, const std::vector<oxh_ctx*>& ctxs) {
+    if (ctxs.empty()) throw OxenError::basic_str("no contexts", OXH_ERR_INVALID);
     const size_t n = buffers.size();
     std::vector<const uint8_t*> ptrs(n);
     std::vector<uint64_t> lens(n);
@@ -758,9 +764,14 @@ std::vector<std::vector<Chunk>> fastcdc_buffers(const std::vector<std::string_vi
     }
     const uint64_t cap = std::max<uint64_t>(1, oxh_fastcdc_max_chunks(lens.data(), n, min_size));
     std::vector<uint64_t> off(cap), len(cap), dig(2 * cap), first(n + 1);
-    check(oxh_fastcdc_host(ctx, ptrs.data(), lens.data(), n, min_size, avg_size, max_size, 1, off.data(), len.data(),
-                           dig.data(), cap, first.data()),
-          "oxh_fastcdc_host");
+    if (ctxs.size() == 1)
+        check(oxh_fastcdc_host(ctxs[0], ptrs.data(), lens.data(), n, min_size, avg_size, max_size, 1, off.data(),
+                               len.data(), dig.data(), cap, first.data()),
+              "oxh_fastcdc_host");
+    else
+        check(oxh_fastcdc_host_multi(ctxs.data(), (int)ctxs.size(), ptrs.data(), lens.data(), n, min_size, avg_size,
+                                     max_size, 1, off.data(), len.data(), dig.data(), cap, first.data()),
+              "oxh_fastcdc_host_multi");
     return split(first, off, len, dig);
 }
 
@@ -811,7 +822,12 @@ std::vector<ChunkedFile> fixed_chunk_files(const std::vector<std::string>& paths
 
 std::vector<std::vector<Chunk>> fixed_chunk_buffers(const std::vector<std::string_view>& buffers, uint64_t chunk_size,
                                                     oxh_ctx* ctx) {
-    ctx = ctx ? ctx : util::hasher::default_context();
+    return fixed_chunk_buffers(buffers, chunk_size, std::vector<oxh_ctx*>{ctx ? ctx : util::hasher::default_context()});
+}
+
+std::vector<std::vector<Chunk>> fixed_chunk_buffers(const std::vector<std::string_view>& buffers, uint64_t chunk_size,
+                                                    const std::vector<oxh_ctx*>& ctxs) {
+    if (ctxs.empty()) throw OxenError::basic_str("no contexts", OXH_ERR_INVALID);
     const size_t n = buffers.size();
     std::vector<const uint8_t*> ptrs(n);
     std::vector<uint64_t> lens(n);
@@ -822,8 +838,13 @@ std::vector<std::vector<Chunk>> fixed_chunk_buffers(const std::vector<std::strin
         if (chunk_size) cap += (lens[i] + chunk_size - 1) / chunk_size;
     }
     std::vector<uint64_t> dig(2 * cap), first(n + 1);
-    check(oxh_chunk_digests_host(ctx, ptrs.data(), lens.data(), n, chunk_size, dig.data(), cap, first.data()),
-          "oxh_chunk_digests_host");
+    if (ctxs.size() == 1)
+        check(oxh_chunk_digests_host(ctxs[0], ptrs.data(), lens.data(), n, chunk_size, dig.data(), cap, first.data()),
+              "oxh_chunk_digests_host");
+    else
+        check(oxh_chunk_digests_host_multi(ctxs.data(), (int)ctxs.size(), ptrs.data(), lens.data(), n, chunk_size,
+                                           dig.data(), cap, first.data()),
+              "oxh_chunk_digests_host_multi");
     std::vector<std::vector<Chunk>> r(n);
     for (size_t i = 0; i < n; ++i)
         for (uint64_t k = first[i], o = 0; k < first[i + 1]; ++k, o += chunk_size)

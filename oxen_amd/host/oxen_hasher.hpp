@@ -316,6 +316,8 @@ std::vector<ChunkedFile> fastcdc_files(const std::vector<std::string>& paths, ui
                                        uint32_t max_size, const std::vector<oxh_ctx*>& ctxs);
 std::vector<std::vector<Chunk>> fastcdc_buffers(const std::vector<std::string_view>& buffers, uint32_t min_size,
                                                 uint32_t avg_size, uint32_t max_size, oxh_ctx* ctx = nullptr);
+std::vector<std::vector<Chunk>> fastcdc_buffers(const std::vector<std::string_view>& buffers, uint32_t min_size,
+                                                uint32_t avg_size, uint32_t max_size, const std::vector<oxh_ctx*>& ctxs);
 // Fixed-size chunks (fixedsize_multithreaded.rs:78-110: chunk i = [i*chunk_size, min(+chunk_size, size)),
 // xxh3_128 of each) through oxh_chunk_digests_files / _host; offsets and lengths are implied.
 std::vector<ChunkedFile> fixed_chunk_files(const std::vector<std::string>& paths, uint64_t chunk_size,
@@ -324,6 +326,8 @@ std::vector<ChunkedFile> fixed_chunk_files(const std::vector<std::string>& paths
                                            const std::vector<oxh_ctx*>& ctxs);
 std::vector<std::vector<Chunk>> fixed_chunk_buffers(const std::vector<std::string_view>& buffers, uint64_t chunk_size,
                                                     oxh_ctx* ctx = nullptr);
+std::vector<std::vector<Chunk>> fixed_chunk_buffers(const std::vector<std::string_view>& buffers, uint64_t chunk_size,
+                                                    const std::vector<oxh_ctx*>& ctxs);
 // u128::to_string() (fastcdchunker.rs:98, the chunk file name)
 std::string chunk_name(u128 hash);
 }  // namespace dedup

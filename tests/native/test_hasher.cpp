@@ -533,6 +533,19 @@ static void dedup_chunks(const std::string& golden) {
             multi_same = cd2[i].chunks[k].hash == files[i].chunks[k].hash && cd2[i].chunks[k].offset == files[i].chunks[k].offset;
     }
     CHECK(multi_same);
+    // ... and the buffer forms (oxh_*_host_multi)
+    const std::vector<std::string_view> bv{std::string_view(big), std::string_view("hello"), std::string_view()};
+    const auto fb2 = dd::fixed_chunk_buffers(bv, 65536, two);
+    const auto cb2 = dd::fastcdc_buffers(bv, 4096, 8192, 16384, two);
+    bool multi_bufs = fb2.size() == 3 && cb2.size() == 3 && fb2[2].empty() && cb2[2].empty();
+    for (size_t i = 0; multi_bufs && i < 2; ++i) {
+        multi_bufs = fb2[i].size() == fb[i].size() && cb2[i].size() == bufs[i].size();
+        for (size_t k = 0; multi_bufs && k < fb[i].size(); ++k)
+            multi_bufs = fb2[i][k].hash == fb[i][k].hash && fb2[i][k].offset == fb[i][k].offset;
+        for (size_t k = 0; multi_bufs && k < bufs[i].size(); ++k)
+            multi_bufs = cb2[i][k].hash == bufs[i][k].hash && cb2[i][k].length == bufs[i][k].length;
+    }
+    CHECK(multi_bufs);
     (void)oxh_ctx_destroy(c2);
     const std::string rm = std::string("rm -rf ") + dir;
     if (system(rm.c_str()) != 0) fprintf(stderr, "could not remove %s\n", dir);
