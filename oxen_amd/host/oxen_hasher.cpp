@@ -868,12 +868,10 @@ std::vector<bool> should_restore_batch(const std::vector<RestoreCheck>& files, b
     for (size_t i = 0; i < n; ++i) {
         const RestoreCheck& f = files[i];
         struct stat sb;
-        if (stat(f.working_path.c_str(), &sb) != 0) {
-            if (errno == ENOENT || errno == ENOTDIR) continue;  // working_path.exists() is false: restore
-            throw OxenError::basic_str("Could not get file metadata: " + util::hasher::rust_path_debug(f.working_path) +
-                                           " error " + util::hasher::rust_io_error_debug(errno),
-                                       OXH_ERR_IO);
-        }
+        // working_path.exists() is fs::metadata(..).is_ok(): any stat failure (ENOENT, ENOTDIR, EACCES on a
+        // parent, ELOOP ...) reads as "does not exist" -> restore; the reference's metadata(..)? after it
+        // fails only if the file changes between the two calls
+        if (stat(f.working_path.c_str(), &sb) != 0) continue;
         const NodeHashes& ref = f.base ? *f.base : f.target;
         if (f.mtime_matched && (uint64_t)sb.st_size == ref.num_bytes) continue;
         if (combined && f.file_metadata.kind == util::fs::FileMetadataHash::Error)

@@ -348,8 +348,9 @@ struct RestoreCheck {
 };
 // should_restore_partial_node (combined = false) or should_restore_file (combined = true) x n: the
 // existence and mtime + size short cuts, then every remaining file hashed in one pass (oxh_hash_files_ex;
-// its text counts give MetadataText) and compared with the target / base hashes. The first file in
-// order whose stat, read or metadata fails throws OxenError, as the reference's `?` does.
+// its text counts give MetadataText) and compared with the target / base hashes. A path whose stat
+// fails reads as absent (Path::exists()): restore. The first file in order whose read or metadata
+// fails throws OxenError, as the reference's `?` does.
 std::vector<bool> should_restore_batch(const std::vector<RestoreCheck>& files, bool combined, oxh_ctx* ctx = nullptr);
 }  // namespace core::restore
 

@@ -72,7 +72,8 @@ def should_restore(paths: Sequence[str], targets: Sequence[NodeHashes], bases: S
         return [bool(x) for x in out]
     meta = [None] * n if file_metadata is None else list(file_metadata)
     text = [i for i in need if combined and isinstance(meta[i], str) and meta[i] == TEXT]
-    plain = [i for i in need if i not in set(text)]
+    text_set = set(text)
+    plain = [i for i in need if i not in text_set]
     content: dict[int, int] = {}
     meta_hash: dict[int, Optional[int]] = {}
     if plain:
@@ -97,7 +98,7 @@ def should_restore(paths: Sequence[str], targets: Sequence[NodeHashes], bases: S
     for i in need:  # in path order: the first failing file is the error
         h, st, oe = content[i]
         if st != 0:
-            if i in text:  # the K1T pass reports no errno: take the file's error from the plain path
+            if i in text_set:  # the K1T pass reports no errno: take the file's error from the plain path
                 _, _, st2, oe2 = hash_files_with_errors_128bit([paths[i]], ctx=ctx)
                 st, oe = (st2[0], oe2[0]) if st2[0] != 0 else (st, 0)
             raise file_error(paths[i], st, oe)

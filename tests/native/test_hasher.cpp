@@ -601,6 +601,7 @@ static void restore_checks() {
         add(p_other, false, false, false);                      // untracked and different
         add(p_new, false, false, true);                         // untracked and equal to the target
         add(put("short.txt", std::string(oldv.size(), 'z')), true, true, true);  // mtime + size short cut: no read
+        add(p_other + "/x", true, false, true);  // stat fails (ENOTDIR): exists() is false, restore
         CHECK(rs::should_restore_batch(v, combined) == want);
     }
     rs::RestoreCheck d;
