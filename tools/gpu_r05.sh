@@ -23,6 +23,7 @@ step box 30 bash -c 'nproc; free -g; df -h /tmp /dev/shm .; cat /sys/fs/cgroup/m
 step newtests 900 python -u -m pytest tests/test_fastcdc.py tests/test_bench_launch.py tests/test_gpu_file_errors.py -m gpu -q --timeout 300 --timeout-method thread -k "files or host or lds or gather or reference_messages or status_and_errno"
 step pytest 1200 python -u -m pytest tests -m gpu -q --maxfail=20 --timeout 300 --timeout-method thread
 step bench 240 python bench.py --gpus 1 --steps 20 --warmup 5
+step c1 300 python tools/bench_c1.py --reps 5
 step bench_dist_torch 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 1 --dist --gather torch --steps 20 --warmup 5 --no-cpu-baseline
 step bench_dist 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --dist --steps 20 --warmup 5 --no-cpu-baseline
 step c5e2e_small 600 python tools/bench_fastcdc_e2e.py --dir /tmp/oxh_c5s --files 16 --gib 1 --chunk 8192 --reps 3 --cold
