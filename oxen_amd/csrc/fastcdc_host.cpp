@@ -64,6 +64,17 @@ int cdc_copy_streams() {
     }();
     return v;
 }
+// Fixed-size rounds of at most this many segments hash each segment as one implied chunk grid
+// (oxh_chunk_digests_device: no descriptor tables built on the host or copied over the link); more
+// segments (many small files) take one launch over descriptors. OXH_FIXED_IMPLICIT_SEGS, 0 = always
+// descriptors.
+int fixed_implicit_segs() {
+    static const int v = [] {
+        const char* e = getenv("OXH_FIXED_IMPLICIT_SEGS");
+        return e ? std::max(0, atoi(e)) : 8;
+    }();
+    return v;
+}
 int cdc_nbounce() {
     static const int v = [] {
         const char* e = getenv("OXH_CDC_NBOUNCE");
@@ -371,23 +382,33 @@ bool fixed_round(Call& C, const Round& R) {
     }
     const uint64_t m = first.back();
     int rc = h.tables(m);
-    for (size_t j = 0; rc == OXH_OK && j < R.segs.size(); ++j) {
+    // a segment starts on a chunk boundary of its file, so its chunks are the implied grid of ck-byte
+    // chunks over [poff, poff + hi - lo) of the piece: with few segments, one grid launch each
+    size_t live = 0;
+    for (size_t j = 0; j < R.segs.size(); ++j) live += first[j + 1] > first[j];
+    const bool implicit = live <= (size_t)fixed_implicit_segs();
+    for (size_t j = 0; rc == OXH_OK && !implicit && j < R.segs.size(); ++j) {
         const Seg& s = R.segs[j];
         for (uint64_t k = first[j], o = s.lo; k < first[j + 1]; ++k, o += ck) {
             h.h_off[k] = s.poff + (o - s.lo);
             h.h_len[k] = std::min(ck, s.hi - o);
         }
     }
-    if (rc == OXH_OK && m &&
+    if (rc == OXH_OK && m && !implicit &&
         (hipMemcpyAsync(h.d_off, h.h_off, m * 8, hipMemcpyHostToDevice, h.comp) != hipSuccess ||
          hipMemcpyAsync(h.d_len, h.h_len, m * 8, hipMemcpyHostToDevice, h.comp) != hipSuccess))
         rc = oxh::set_error(OXH_ERR_HIP, "chunk descriptors H2D");
     if (rc == OXH_OK && (hipStreamWaitEvent(h.comp, h.ev_copied[R.b], 0) != hipSuccess ||
                          (h.ncopy == 2 && hipStreamWaitEvent(h.comp, h.ev_copied2[R.b], 0) != hipSuccess)))
         rc = oxh::set_error(OXH_ERR_HIP, "wait copies");
-    if (rc == OXH_OK && m)
+    if (rc == OXH_OK && m && !implicit)
         rc = oxh_xxh3_128_batch_device(h.d_piece[R.b], h.d_off, h.d_len, m, h.d_dig,
                                        ck <= 16384 ? OXH_MODE_WAVE_SHORT : OXH_MODE_WAVE, h.comp);
+    for (size_t j = 0; rc == OXH_OK && implicit && j < R.segs.size(); ++j) {
+        const Seg& s = R.segs[j];
+        if (first[j + 1] > first[j])
+            rc = oxh_chunk_digests_device(h.d_piece[R.b] + s.poff, s.hi - s.lo, ck, h.d_dig + 2 * first[j], h.comp);
+    }
     if (rc == OXH_OK && m && hipMemcpyAsync(h.h_dig, h.d_dig, m * 16, hipMemcpyDeviceToHost, h.comp) != hipSuccess)
         rc = oxh::set_error(OXH_ERR_HIP, "digests D2H");
     if (rc == OXH_OK && hipStreamSynchronize(h.comp) != hipSuccess) rc = oxh::set_error(OXH_ERR_HIP, "chunking stream");

@@ -68,5 +68,13 @@ step multi_e2e_2 900 env OXH_TRACE=1 python tools/bench_fastcdc_e2e.py --dir /de
 step multi_e2e_1 900 env OXH_TRACE=1 python tools/bench_fastcdc_e2e.py --dir /dev/shm/oxh_c5 --files 16 --gib 8 --chunk 8192 --reps 3 --keep --cpu none
 step restore 300 python -u -m pytest tests/test_restore.py -m gpu -v --timeout 200 --timeout-method thread
 step fixed_e2e_shm4k 900 env OXH_TRACE=1 python tools/bench_fastcdc_e2e.py --fixed --dir /dev/shm/oxh_c5 --files 16 --gib 8 --chunk 4096 --reps 3 --keep
+step fixedtests 600 python -u -m pytest tests/test_dedup_fixed.py tests/test_fastcdc.py tests/test_native_mirror.py -m gpu -q --timeout 300 --timeout-method thread -k "fixed or chunk_digests or multi or native"
+FX="python tools/bench_fastcdc_e2e.py --fixed --dir /dev/shm/oxh_c5 --files 16 --gib 8 --reps 3 --keep"
+step fx_imp4k 900 env OXH_TRACE=1 $FX --chunk 4096
+step fx_desc4k 900 env OXH_TRACE=1 OXH_FIXED_IMPLICIT_SEGS=0 $FX --chunk 4096 --cpu none
+step fx_imp4k_b 900 env OXH_TRACE=1 $FX --chunk 4096 --cpu none
+step fx_desc4k_b 900 env OXH_TRACE=1 OXH_FIXED_IMPLICIT_SEGS=0 $FX --chunk 4096 --cpu none
+step fx_imp64k 900 env OXH_TRACE=1 $FX --chunk 65536
+step fx_desc64k 900 env OXH_TRACE=1 OXH_FIXED_IMPLICIT_SEGS=0 $FX --chunk 65536 --cpu none
 rm -rf /dev/shm/oxh_c5 /tmp/oxh_c5s /tmp/oxh_c5d /tmp/oxh_big /tmp/oxh_fx
 echo "== done $(date +%T)"
