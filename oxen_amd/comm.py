@@ -74,9 +74,18 @@ class DigestComm:
 
 def comm_from_process_group(rank: int, nranks: int, device: int, group=None) -> DigestComm:
     """A DigestComm for the ranks of a torch.distributed group: rank 0 creates the id, the group
-    broadcasts it (the "out of band" step of the ABI), every rank creates its communicator."""
+    broadcasts it (the "out of band" step of the ABI), every rank creates its communicator. If rank 0
+    cannot create the id (no RCCL), it broadcasts that instead, so every rank raises together rather
+    than the others waiting in the broadcast or in oxh_comm_create for a rank that never comes."""
     import torch.distributed as dist
 
-    obj: list[Optional[bytes]] = [DigestComm.unique_id() if rank == 0 else None]
+    obj: list[Optional[object]] = [None]
+    if rank == 0:
+        try:
+            obj[0] = DigestComm.unique_id()
+        except _capi.OxenError as e:
+            obj[0] = ("error", str(e), e.code)
     dist.broadcast_object_list(obj, src=0, group=group)
+    if isinstance(obj[0], tuple):
+        raise _capi.OxenError(f"rank 0 could not create the comm id: {obj[0][1]}", int(obj[0][2]))
     return DigestComm(obj[0], rank, nranks, device)

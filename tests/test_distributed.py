@@ -114,3 +114,47 @@ def test_pipelined_gather_gloo():
         assert p.exitcode == 0
     res = dict(q.get(timeout=10) for _ in range(world))
     assert res == {0: True, 1: True}
+
+
+def _comm_id_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oxen_amd import _capi, comm
+
+        def no_rccl():
+            raise _capi.OxenError("RCCL unavailable (test)", _capi.OXH_ERR_HIP)
+
+        def never(*a, **k):  # no rank may go on to create a communicator
+            raise AssertionError("DigestComm created after a failed id")
+
+        comm.DigestComm.unique_id = staticmethod(no_rccl)
+        comm.DigestComm.__init__ = never
+        try:
+            comm.comm_from_process_group(rank, world, 0)
+            q.put((rank, "no error"))
+        except _capi.OxenError as e:
+            q.put((rank, e.code, "rank 0 could not create the comm id" in str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_comm_id_failure_raises_on_every_rank():
+    """comm_from_process_group: when rank 0 cannot create the RCCL id, every rank raises the same
+    error (none waits in the broadcast or in oxh_comm_create), so bench.py's collective fallback to
+    torch's all-gather is reached by all of them."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_id_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    from oxen_amd import _capi
+
+    got = sorted(q.get(timeout=10) for _ in range(world))
+    assert got == [(r, _capi.OXH_ERR_HIP, True) for r in range(world)]
