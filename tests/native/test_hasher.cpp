@@ -602,6 +602,9 @@ static void restore_checks() {
         add(p_new, false, false, true);                         // untracked and equal to the target
         add(put("short.txt", std::string(oldv.size(), 'z')), true, true, true);  // mtime + size short cut: no read
         add(p_other + "/x", true, false, true);  // stat fails (ENOTDIR): exists() is false, restore
+        const std::string dangling = std::string(dir) + "/dangling" + (combined ? "1" : "0");
+        CHECK(symlink((std::string(dir) + "/nowhere").c_str(), dangling.c_str()) == 0);
+        add(dangling, false, false, true);  // exists() follows the link: absent, restore
         CHECK(rs::should_restore_batch(v, combined) == want);
     }
     rs::RestoreCheck d;

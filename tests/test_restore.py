@@ -125,9 +125,12 @@ def test_should_restore_short_cuts_need_no_device(tmp_path):
     f.write_bytes(b"12345")
     t = NodeHashes(hash=1, num_bytes=5, combined_hash=1)
     b = NodeHashes(hash=2, num_bytes=5, combined_hash=2)
-    got = restore.should_restore([str(tmp_path / "missing"), str(f), str(f), str(f / "x")], [t, t, t, t],
-                                 [None, b, None, b], [False, True, True, False])
-    assert got == [True, True, True, True]  # a stat that fails (ENOTDIR here) is Path::exists() == false
+    dangling = tmp_path / "dangling"
+    dangling.symlink_to(tmp_path / "nowhere")
+    got = restore.should_restore([str(tmp_path / "missing"), str(f), str(f), str(f / "x"), str(dangling)],
+                                 [t] * 5, [None, b, None, b, None], [False, True, True, False, False])
+    # a stat that fails (ENOTDIR, a dangling symlink: exists() follows links) is Path::exists() == false
+    assert got == [True] * 5
     for combined in (False, True):
         assert restore.should_restore([], [], [], [], combined=combined) == []
     with pytest.raises(_capi.OxenError, match="lengths differ"):
