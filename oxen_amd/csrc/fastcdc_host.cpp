@@ -51,8 +51,19 @@ int default_reader_threads();                               // ... OXH_NUM_THREA
 
 namespace {
 
-constexpr uint64_t kCdcBounce = 64ull << 20;  // one pinned bounce buffer (a window of the piece)
 constexpr int kCdcMaxBounce = 16;
+// one pinned bounce buffer (a window of the piece): OXH_CDC_BOUNCE_MIB, 16..256 (a power of two),
+// default 64
+uint64_t cdc_bounce() {
+    static const uint64_t v = [] {
+        const char* e = getenv("OXH_CDC_BOUNCE_MIB");
+        const long k = e ? atol(e) : 64;
+        uint64_t m = 16;
+        while (m < 256 && (long)m < k) m <<= 1;
+        return m << 20;
+    }();
+    return v;
+}
 // the ring: reads of the next windows run while earlier H2Ds drain (OXH_CDC_NBOUNCE, 2..16, default 8:
 // 47.7 vs 43.6 GiB/s for 4 on 16 x 1 GiB from the page cache, profiles/r05/r05a_e2e_*)
 // H2D copy streams the windows alternate over (OXH_CDC_COPY_STREAMS, 1 or 2; default 2: C5 from the
@@ -194,7 +205,7 @@ int cdc_host(oxh_ctx* ctx, uint64_t piece, CdcHost** out) {
     }
     h->nbounce = cdc_nbounce();
     for (int i = 0; i < h->nbounce; ++i) {
-        if (hipHostMalloc(&h->h_bounce[i], kCdcBounce, hipHostMallocDefault) != hipSuccess)
+        if (hipHostMalloc(&h->h_bounce[i], cdc_bounce(), hipHostMallocDefault) != hipSuccess)
             return bad(OXH_ERR_NOMEM, "pinned bounce buffers");
         if (hipEventCreateWithFlags(&h->ev_bounce[i], hipEventDisableTiming) != hipSuccess) return bad(OXH_ERR_HIP, "events");
     }
@@ -507,7 +518,7 @@ void chunk_rounds(Call& C) {
     }
 }
 
-// Read one round's segments into the piece buffer through the bounce ring (windows of kCdcBounce of
+// Read one round's segments into the piece buffer through the bounce ring (windows of cdc_bounce() of
 // the piece, read by the pool in kCdcPart tasks, each window's H2D once its reads are done; up to
 // kCdcNBounce - 1 windows reading while the oldest one's copy is issued).
 int upload_round(Call& C, const Round& R) {
@@ -523,14 +534,15 @@ int upload_round(Call& C, const Round& R) {
         oxh::Pool::Group grp;
     };
     std::vector<std::unique_ptr<Window>> wins;
+    const uint64_t bounce = cdc_bounce();
     for (const Seg& s : R.segs) {
         if (C.files[s.file].status.load() != OXH_OK) continue;
         for (uint64_t o = s.lo; o < s.hi;) {
-            const uint64_t p = s.poff + (o - s.lo), w = p / kCdcBounce;
-            const uint64_t n = std::min({s.hi - o, kCdcPart, (w + 1) * kCdcBounce - p});
+            const uint64_t p = s.poff + (o - s.lo), w = p / bounce;
+            const uint64_t n = std::min({s.hi - o, kCdcPart, (w + 1) * bounce - p});
             while (wins.size() <= w) {
                 wins.emplace_back(new Window);
-                wins.back()->base = (uint64_t)(wins.size() - 1) * kCdcBounce;
+                wins.back()->base = (uint64_t)(wins.size() - 1) * bounce;
             }
             Window& W = *wins[w];
             W.parts.push_back({s.file, o, n, p - W.base});
@@ -545,7 +557,7 @@ int upload_round(Call& C, const Round& R) {
         W.grp.wait();
         C.t_read_wait += now() - tw;
         if (W.used == 0) return OXH_OK;
-        hipStream_t cs = (h.ncopy == 2 && (W.base / kCdcBounce) % 2) ? h.copy2 : h.copy;
+        hipStream_t cs = (h.ncopy == 2 && (W.base / bounce) % 2) ? h.copy2 : h.copy;
         if (hipMemcpyAsync(h.d_piece[R.b] + W.base, h.h_bounce[W.bb], W.used, hipMemcpyHostToDevice, cs) != hipSuccess ||
             hipEventRecord(h.ev_bounce[W.bb], cs) != hipSuccess)
             return oxh::set_error(OXH_ERR_HIP, "piece H2D");
@@ -597,7 +609,7 @@ int upload_round(Call& C, const Round& R) {
 // fixed-size chunks per round: bounds the descriptor / digest buffers (32 B a chunk) for tiny chunks
 constexpr uint64_t kMaxFixedChunksPerRound = 4ull << 20;
 // largest fixed chunk: a chunk must fit a piece, and pieces stop at 3 GiB
-constexpr uint64_t kMaxFixedChunk = (3ull << 30) - kCdcBounce;
+constexpr uint64_t kMaxFixedChunk = (3ull << 30) - (64ull << 20);
 
 // the crate's asserts (v2020::FastCDC::with_level) or the fixed chunk size's range, before any I/O
 int check_params(uint32_t mn, uint32_t av, uint32_t mx, uint32_t lv, uint64_t fixed) {
@@ -638,7 +650,7 @@ int run(oxh_ctx* ctx, CdcSource& src, uint64_t n, uint32_t mn, uint32_t av, uint
     uint64_t piece = (pe && atoll(pe) > 0 ? (uint64_t)atoll(pe) : 1024ull) << 20;
     piece = std::max<uint64_t>(piece, fixed > (1ull << 30) ? min_seg + kCdcAlign : 2 * min_seg);
     piece = std::min<uint64_t>(piece, 3ull << 30);
-    piece = (piece + kCdcBounce - 1) / kCdcBounce * kCdcBounce;
+    piece = (piece + cdc_bounce() - 1) / cdc_bounce() * cdc_bounce();
     CdcHost* h = nullptr;
     if (int rc = cdc_host(ctx, piece, &h)) return rc;
 
@@ -769,7 +781,7 @@ int run(oxh_ctx* ctx, CdcSource& src, uint64_t n, uint32_t mn, uint32_t av, uint
                 "chunking+D2H+stitch %.1f, waits %.1f (of them: reads %.1f, bounce H2D %.1f), %d bounce x %llu MiB, %d readers\n",
                 (unsigned long long)n, round_no, (unsigned long long)(piece >> 20), (unsigned long long)C.total,
                 1e3 * (now() - t_start), 1e3 * C.t_read, 1e3 * C.t_chunk, 1e3 * C.t_wait, 1e3 * C.t_read_wait,
-                1e3 * C.t_h2d_wait, h->nbounce, (unsigned long long)(kCdcBounce >> 20), h->pool->size());
+                1e3 * C.t_h2d_wait, h->nbounce, (unsigned long long)(cdc_bounce() >> 20), h->pool->size());
     if (total_out) *total_out = C.total;
     if (C.total > capacity)
         return oxh::set_error(OXH_ERR_INVALID, "chunk capacity too small: need " + std::to_string(C.total) + " entries");

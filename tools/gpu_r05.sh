@@ -76,5 +76,12 @@ step fx_imp4k_b 900 env OXH_TRACE=1 $FX --chunk 4096 --cpu none
 step fx_desc4k_b 900 env OXH_TRACE=1 OXH_FIXED_IMPLICIT_SEGS=0 $FX --chunk 4096 --cpu none
 step fx_imp64k 900 env OXH_TRACE=1 $FX --chunk 65536
 step fx_desc64k 900 env OXH_TRACE=1 OXH_FIXED_IMPLICIT_SEGS=0 $FX --chunk 65536 --cpu none
+E8="python tools/bench_fastcdc_e2e.py --dir /dev/shm/oxh_c5 --files 16 --gib 8 --chunk 8192 --reps 3 --keep --cpu none"
+step bw64 900 env OXH_TRACE=1 $E8
+step bw128 900 env OXH_TRACE=1 OXH_CDC_BOUNCE_MIB=128 $E8
+step bw256 900 env OXH_TRACE=1 OXH_CDC_BOUNCE_MIB=256 OXH_CDC_NBOUNCE=6 python tools/bench_fastcdc_e2e.py --dir /dev/shm/oxh_c5 --files 16 --gib 8 --chunk 8192 --reps 3 --keep
+step bw32 900 env OXH_TRACE=1 OXH_CDC_BOUNCE_MIB=32 OXH_CDC_NBOUNCE=16 $E8
+step bw64b 900 env OXH_TRACE=1 $E8
+step bw128b 900 env OXH_TRACE=1 OXH_CDC_BOUNCE_MIB=128 $E8
 rm -rf /dev/shm/oxh_c5 /tmp/oxh_c5s /tmp/oxh_c5d /tmp/oxh_big /tmp/oxh_fx
 echo "== done $(date +%T)"
