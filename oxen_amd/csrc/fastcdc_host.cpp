@@ -380,8 +380,9 @@ void stitch(Call& C, const Round& R, const std::vector<uint64_t>& first, const s
 }
 
 // Fixed-size chunking of one round: every segment starts at a multiple of the chunk size in its file,
-// so its chunks are [poff + k*chunk, + min(chunk, rest)) of the piece. One K1 launch over the round's
-// chunk descriptors, the digests come back, and they are appended per file. false = the call failed.
+// so its chunks are [poff + k*chunk, + min(chunk, rest)) of the piece. A few segments: one implied-grid
+// K1 launch each; many: one K1 launch over the round's chunk descriptors. The digests come back and are
+// appended per file. false = the call failed.
 bool fixed_round(Call& C, const Round& R) {
     CdcHost& h = *C.h;
     const uint64_t ck = C.fixed;
