@@ -83,5 +83,11 @@ step bw256 900 env OXH_TRACE=1 OXH_CDC_BOUNCE_MIB=256 OXH_CDC_NBOUNCE=6 python t
 step bw32 900 env OXH_TRACE=1 OXH_CDC_BOUNCE_MIB=32 OXH_CDC_NBOUNCE=16 $E8
 step bw64b 900 env OXH_TRACE=1 $E8
 step bw128b 900 env OXH_TRACE=1 OXH_CDC_BOUNCE_MIB=128 $E8
+step nb8 900 env OXH_TRACE=1 OXH_CDC_NBOUNCE=8 $E8
+step nb12 900 env OXH_TRACE=1 OXH_CDC_NBOUNCE=12 $E8
+step nb16 900 env OXH_TRACE=1 OXH_CDC_NBOUNCE=16 $E8
+step nb8b 900 env OXH_TRACE=1 OXH_CDC_NBOUNCE=8 $E8
+step nb12b 900 env OXH_TRACE=1 OXH_CDC_NBOUNCE=12 $E8
+step nb16b 900 env OXH_TRACE=1 OXH_CDC_NBOUNCE=16 $E8
 rm -rf /dev/shm/oxh_c5 /tmp/oxh_c5s /tmp/oxh_c5d /tmp/oxh_big /tmp/oxh_fx
 echo "== done $(date +%T)"
