@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define OXH_ABI_VERSION 4
+#define OXH_ABI_VERSION 5
 
 /* status codes (also used per item in status[]) */
 #define OXH_OK 0
@@ -375,9 +375,14 @@ int oxh_hash_streams(oxh_ctx* ctx, const uint8_t* streams, const uint64_t* offse
  * device) receives every rank's table in rank order -- on every rank when root < 0 (all-gather), else on
  * rank `root` only (d_full may be NULL on the others). Equal counts take one ncclAllGather / ncclGather,
  * ragged ones a group of point-to-point transfers. Enqueued on `stream` (hipStream_t, NULL = the null
- * stream); returns without waiting. A communicator is used by one thread at a time. */
+ * stream); returns without waiting. A communicator is used by one thread at a time.
+ * oxh_comm_check: OXH_OK when RCCL loads and `device` is a visible HIP device, else the error
+ * oxh_comm_create would return for that reason (OXH_ERR_NODEVICE / OXH_ERR_INVALID) without joining
+ * anything -- every rank calls it and the job agrees on the result before any rank enters
+ * oxh_comm_create, which would otherwise wait in RCCL's bootstrap for a rank that has already failed. */
 #define OXH_COMM_ID_BYTES 128
 typedef struct oxh_comm oxh_comm;
+int oxh_comm_check(int device);
 int oxh_comm_unique_id(uint8_t* id);
 int oxh_comm_create(const uint8_t* id, int rank, int nranks, int device, oxh_comm** out);
 int oxh_comm_info(oxh_comm* comm, int* rank, int* nranks, int* device);

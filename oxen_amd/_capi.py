@@ -104,6 +104,7 @@ SIGNATURES = {
                                             _u64p, _u64, _u64p]),
     "oxh_fastcdc_gear": (_int, [_u64p]),
     "oxh_fastcdc_masks": (_int, [_u32, _u32, _u64p, _u64p]),
+    "oxh_comm_check": (_int, [_int]),
     "oxh_comm_unique_id": (_int, [ctypes.c_char_p]),
     "oxh_comm_create": (_int, [ctypes.c_char_p, _int, _int, _int, ctypes.POINTER(_vp)]),
     "oxh_comm_info": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int), ctypes.POINTER(_int)]),

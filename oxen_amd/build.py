@@ -47,6 +47,11 @@ COMMIT_CLI_SRC = os.path.join(ROOT, "tests", "native", "commit_tree_cli.cpp")
 COMMIT_CLI = os.path.join(ROOT, "tests", "native", "commit_tree_cli")
 FAKE_HELPER_SRC = os.path.join(ROOT, "tests", "native", "fake_pool_helper.cpp")
 FAKE_HELPER = os.path.join(ROOT, "tests", "native", "fake_pool_helper")  # tests only: the pool without a GPU
+FAKE_RCCL_SRC = os.path.join(ROOT, "tests", "native", "fake_rccl.cpp")
+# tests only: an "RCCL" for N processes on one GPU (OXH_RCCL_LIB), with and without ncclGather
+FAKE_RCCL = os.path.join(ROOT, "tests", "native", "libfake_rccl.so")
+FAKE_RCCL_NOGATHER = os.path.join(ROOT, "tests", "native", "libfake_rccl_nogather.so")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 
 def _stale(target: str, deps: list[str]) -> bool:
@@ -74,6 +79,11 @@ def build_host(force: bool = False, verbose: bool = False) -> str:
          ["g++", "-std=c++17", "-O2", "-Wall", "-o", COMMIT_CLI + ".tmp", COMMIT_CLI_SRC,
           f"-L{HERE}", "-l:liboxen_hasher.so", "-l:liboxen_hash.so", "-Wl,-rpath,$ORIGIN/../../oxen_amd"]),
     ]
+    for target, extra in ((FAKE_RCCL, []), (FAKE_RCCL_NOGATHER, ["-DFAKE_NO_GATHER"])):
+        steps.append((target, [FAKE_RCCL_SRC],
+                      ["g++", "-std=c++17", "-O2", "-Wall", "-shared", "-fPIC", "-fvisibility=hidden",
+                       "-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include", "-o", target + ".tmp", FAKE_RCCL_SRC] + extra +
+                      [f"-L{ROCM}/lib", "-lamdhip64", "-lrt", f"-Wl,-rpath,{ROCM}/lib"]))
     for target, deps, cmd in steps:
         if force or _stale(target, deps):
             if verbose:

@@ -72,13 +72,31 @@ class DigestComm:
         self.close()
 
 
+def comm_check(device: int) -> Optional[_capi.OxenError]:
+    """oxh_comm_check: None when RCCL loads and `device` is visible, else the error oxh_comm_create
+    would fail with (nothing is joined)."""
+    rc = _capi.lib().oxh_comm_check(int(device))
+    if rc == _capi.OXH_OK:
+        return None
+    return _capi.OxenError(f"oxh_comm_check: {_capi.lib().oxh_last_error().decode(errors='replace')}", rc)
+
+
 def comm_from_process_group(rank: int, nranks: int, device: int, group=None) -> DigestComm:
-    """A DigestComm for the ranks of a torch.distributed group: rank 0 creates the id, the group
-    broadcasts it (the "out of band" step of the ABI), every rank creates its communicator. If rank 0
-    cannot create the id (no RCCL), it broadcasts that instead, so every rank raises together rather
-    than the others waiting in the broadcast or in oxh_comm_create for a rank that never comes."""
+    """A DigestComm for the ranks of a torch.distributed group: every rank checks its device and RCCL
+    (oxh_comm_check) and the group agrees on the outcome first; then rank 0 creates the id, the group
+    broadcasts it (the "out of band" step of the ABI), and every rank creates its communicator. A
+    failure on any rank -- a bad device, no RCCL, rank 0 unable to make the id -- is raised on every
+    rank together, rather than the others waiting in the broadcast or in RCCL's bootstrap (inside
+    oxh_comm_create) for a rank that never comes."""
     import torch.distributed as dist
 
+    errs: list[Optional[object]] = [None] * nranks
+    err = comm_check(device)
+    dist.all_gather_object(errs, None if err is None else (str(err), err.code), group=group)
+    bad = [(q, e) for q, e in enumerate(errs) if e is not None]
+    if bad:
+        q, (msg, code) = bad[0]
+        raise _capi.OxenError(f"rank {q} cannot join the digest gather: {msg}", int(code))
     obj: list[Optional[object]] = [None]
     if rank == 0:
         try:

@@ -101,18 +101,23 @@ int oxh_comm_unique_id(uint8_t* id) {
     return OXH_OK;
 }
 
-int oxh_comm_create(const uint8_t* id, int rank, int nranks, int device, oxh_comm** out) {
-    if (!id || !out) return oxh::set_error(OXH_ERR_INVALID, "null argument");
-    *out = nullptr;
-    if (nranks < 1 || rank < 0 || rank >= nranks) return oxh::set_error(OXH_ERR_INVALID, "rank out of range");
+int oxh_comm_check(int device) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
         (void)hipGetLastError();
         return oxh::set_error(OXH_ERR_NODEVICE, "no HIP device visible");
     }
     if (device < 0 || device >= ndev) return oxh::set_error(OXH_ERR_INVALID, "device index out of range");
+    if (!rccl()) return oxh::set_error(OXH_ERR_NODEVICE, "RCCL unavailable");
+    return OXH_OK;
+}
+
+int oxh_comm_create(const uint8_t* id, int rank, int nranks, int device, oxh_comm** out) {
+    if (!id || !out) return oxh::set_error(OXH_ERR_INVALID, "null argument");
+    *out = nullptr;
+    if (nranks < 1 || rank < 0 || rank >= nranks) return oxh::set_error(OXH_ERR_INVALID, "rank out of range");
+    if (const int rc = oxh_comm_check(device); rc != OXH_OK) return rc;
     Rccl* r = rccl();
-    if (!r) return oxh::set_error(OXH_ERR_NODEVICE, "RCCL unavailable");
     int prev = 0;
     (void)hipGetDevice(&prev);
     if (hipSetDevice(device) != hipSuccess) return oxh::set_error(OXH_ERR_HIP, "hipSetDevice failed");

@@ -21,7 +21,9 @@
 #include <hip/hip_runtime_api.h>
 #include <errno.h>
 #include <fcntl.h>
+#include <dirent.h>
 #include <string.h>
+#include <sys/resource.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -96,10 +98,34 @@ int cdc_nbounce() {
 }
 constexpr uint64_t kCdcPart = 4ull << 20;     // one reader task
 constexpr uint64_t kCdcAlign = 256;           // segment placement in a piece
-constexpr uint64_t kProbeWindow = 256;        // files opened (and stat'ed) ahead of the planner
-// files per round: every planned file holds its descriptor until its last segment is read, so a piece
-// of many small files must not need more than a process's descriptor limit (often 1024-20000)
+constexpr uint64_t kProbeWindow = 256;        // files opened (and stat'ed) ahead of the planner, at most
+// segments per round, at most: every planned file holds its descriptor until its last segment is read
 constexpr size_t kMaxSegsPerRound = 2048;
+
+// Descriptors one call may hold at once: files probed ahead of the planner plus the files of the round
+// being read (FileSrc only; host buffers hold none). Half of what the soft RLIMIT_NOFILE leaves free
+// when the call starts, split over the `shares` calls an _multi entry runs side by side -- so a tree of
+// many small (or empty) files never meets EMFILE under a 1024 default limit.
+struct FdBudget {
+    uint64_t window = kProbeWindow;
+    size_t segs = kMaxSegsPerRound;
+};
+FdBudget fd_budget(int shares) {
+    FdBudget b;
+    struct rlimit rl;
+    if (getrlimit(RLIMIT_NOFILE, &rl) != 0 || rl.rlim_cur == RLIM_INFINITY) return b;
+    uint64_t open_now = 0;
+    if (DIR* d = opendir("/proc/self/fd")) {
+        while (readdir(d)) ++open_now;
+        closedir(d);
+    }
+    const uint64_t lim = (uint64_t)rl.rlim_cur;
+    const uint64_t free_fds = lim > open_now ? lim - open_now : 0;
+    const uint64_t mine = std::max<uint64_t>(16, free_fds / 2 / (uint64_t)std::max(1, shares));
+    b.window = std::min<uint64_t>(kProbeWindow, std::max<uint64_t>(4, mine / 8));
+    b.segs = (size_t)std::min<uint64_t>(kMaxSegsPerRound, std::max<uint64_t>(8, mine - b.window));
+    return b;
+}
 
 inline uint64_t align_up(uint64_t x) { return (x + kCdcAlign - 1) & ~(kCdcAlign - 1); }
 
@@ -125,15 +151,14 @@ struct CdcHost {
 
     ~CdcHost() {
         (void)hipSetDevice(device);
-        if (copy) (void)hipStreamSynchronize(copy);
-        if (comp) (void)hipStreamSynchronize(comp);
+        for (hipStream_t st : {copy, copy2, comp})  // every stream that touches d_piece, before it goes
+            if (st) (void)hipStreamSynchronize(st);
         for (auto* p : d_piece)
             if (p) (void)hipFree(p);
         for (auto e : ev_copied)
             if (e) (void)hipEventDestroy(e);
         for (auto e : ev_copied2)
             if (e) (void)hipEventDestroy(e);
-        if (copy2) (void)hipStreamSynchronize(copy2);
         for (int i = 0; i < kCdcMaxBounce; ++i) {
             if (h_bounce[i]) (void)hipHostFree(h_bounce[i]);
             if (ev_bounce[i]) (void)hipEventDestroy(ev_bounce[i]);
@@ -223,6 +248,7 @@ struct CdcSource {
     // [off, off + n) into dst; false with errno (0: the file ended early); called from many threads
     virtual bool read(uint64_t i, uint64_t off, uint64_t n, uint8_t* dst, int& oserr) = 0;
     virtual void close(uint64_t) {}
+    virtual bool holds_fds() const { return false; }  // open() keeps a descriptor until close()
 };
 
 // fs::read(input_file) (fastcdchunker.rs:75): File::open, then the whole file. A directory opens and
@@ -271,6 +297,7 @@ struct FileSrc final : CdcSource {
         if (fds[i] >= 0) ::close(fds[i]);
         fds[i] = -1;
     }
+    bool holds_fds() const override { return true; }
 };
 
 struct MemSrc final : CdcSource {
@@ -623,7 +650,7 @@ int check_params(uint32_t mn, uint32_t av, uint32_t mx, uint32_t lv, uint64_t fi
 
 int run(oxh_ctx* ctx, CdcSource& src, uint64_t n, uint32_t mn, uint32_t av, uint32_t mx, uint32_t lv, uint64_t fixed,
         uint64_t* c_off, uint64_t* c_len, uint64_t* dig, uint64_t capacity, uint64_t* first_chunk, uint64_t* sizes,
-        int32_t* status, int32_t* os_error, uint64_t* total_out = nullptr) {
+        int32_t* status, int32_t* os_error, uint64_t* total_out = nullptr, int shares = 1) {
     if (!ctx) return oxh::set_error(OXH_ERR_INVALID, "null context");
     if (!first_chunk) return oxh::set_error(OXH_ERR_INVALID, "null first_chunk");
     if (capacity && !fixed && (!c_off || !c_len)) return oxh::set_error(OXH_ERR_INVALID, "null chunk table");
@@ -660,6 +687,7 @@ int run(oxh_ctx* ctx, CdcSource& src, uint64_t n, uint32_t mn, uint32_t av, uint
     C.c_off = c_off, C.c_len = c_len, C.dig = dig, C.capacity = capacity, C.first_chunk = first_chunk;
     C.files = std::vector<FileState>(n);
     first_chunk[0] = 0;
+    const FdBudget fdb = src.holds_fds() ? fd_budget(shares) : FdBudget{};
     static const bool trace = getenv("OXH_TRACE") != nullptr;
     const double t_start = now();
     std::thread chunker(chunk_rounds, std::ref(C));
@@ -690,13 +718,15 @@ int run(oxh_ctx* ctx, CdcSource& src, uint64_t n, uint32_t mn, uint32_t av, uint
         // plan: files in order into this piece; a file that does not fit whole takes the rest of the
         // piece (if at least min_seg) and continues in the next round from `max` before its end
         uint64_t off = 0, nchunks = 0;  // (nchunks: fixed-size chunks planned this round)
-        while (cur < n && R.segs.size() < kMaxSegsPerRound) {
-            if (cur >= probed) probe_to(cur + kProbeWindow);
+        while (cur < n && R.segs.size() < fdb.segs) {
+            if (cur >= probed) probe_to(cur + fdb.window);
             FileState& F = C.files[cur];
             if (F.status.load() != OXH_OK || F.size == 0) {  // no (more) chunks: an error, or an empty file
                 // (a file whose read failed in an earlier round keeps its first output index: the
-                // stitcher drops what it emitted for it)
+                // stitcher drops what it emitted for it). Nothing more is read from it: its descriptor
+                // closes now (its earlier segments, if any, were read in rounds already uploaded).
                 R.segs.push_back({cur, 0, 0, 0, F.next_lo == 0, true});
+                if (F.segs_left == 0) src.close(cur);
                 ++cur;
                 continue;
             }
@@ -898,7 +928,7 @@ int run_sharded(oxh_ctx* const* ctxs, int nctx, const char* const* paths, const 
             auto src = source(a, m);
             S.total = 0;
             S.rc = run(ctxs[k], *src, m, mn, av, mx, lv, fixed, o, l, d, cap, S.first.data(), S.sizes.data(), S.st.data(),
-                       S.oe.data(), &S.total);
+                       S.oe.data(), &S.total, nctx);
             if (S.rc == OXH_ERR_INVALID && S.total > cap) {
                 cap = S.total;
                 S.inplace = false;  // past its region: tables of its own

@@ -548,14 +548,87 @@ def hash_file_contents_with_retry(path, total_retries: int = 5, sleep=time.sleep
                 raise
 
 
+def serde_f64(x: float) -> str:
+    """serde_json's text for an f64 field: non-finite values are `null` (serde_json's
+    serialize_f64), finite ones ryu's shortest round-trip form (ryu::Buffer::format_finite, the crate's
+    pretty.rs `format64`). With d the shortest digit string (length L, no trailing zeros) and the value
+    d x 10^k, kk = L + k (10^(kk-1) <= |x| < 10^kk):
+      0 <= k and kk <= 16    digits, k zeros, ".0"            12.0 -> "12.0", 1e15 -> "1000000000000000.0"
+      0 < kk <= 16           the point after kk digits         12.5 -> "12.5"
+      -5 < kk <= 0           "0.", -kk zeros, digits           1e-5 -> "0.00001", 0.1 -> "0.1"
+      L == 1                 d "e" (kk - 1)                    1e16 -> "1e16", 1e-6 -> "1e-6"
+      otherwise              d0 "." rest "e" (kk - 1)          1.5e16 -> "1.5e16", 1.25e-7 -> "1.25e-7"
+    (no "+" and no zero padding in the exponent; zero is "0.0" / "-0.0"). The digit string is
+    Python's repr's -- both pick the shortest string that round-trips, nearest the value."""
+    import math
+    from decimal import Decimal
+
+    x = float(x)
+    if not math.isfinite(x):
+        return "null"
+    if x == 0.0:
+        return "-0.0" if math.copysign(1.0, x) < 0 else "0.0"
+    sign = "-" if x < 0 else ""
+    _, digits, k = Decimal(repr(abs(x))).as_tuple()
+    d = "".join(map(str, digits))
+    stripped = d.rstrip("0")
+    k += len(d) - len(stripped)
+    d = stripped
+    n = len(d)
+    kk = n + k
+    if 0 <= k and kk <= 16:
+        return f"{sign}{d}{'0' * k}.0"
+    if 0 < kk <= 16:
+        return f"{sign}{d[:kk]}.{d[kk:]}"
+    if -5 < kk <= 0:
+        return f"{sign}0.{'0' * -kk}{d}"
+    if n == 1:
+        return f"{sign}{d}e{kk - 1}"
+    return f"{sign}{d[0]}.{d[1:]}e{kk - 1}"
+
+
+# GenericMetadata variants with f64 fields (model/metadata/metadata_audio.rs:11, metadata_video.rs:11):
+# serde writes them as floats even when the value is integral (12 -> "12.0")
+_F64_FIELDS = {"audio": ("num_seconds",), "video": ("num_seconds",)}
+
+
+def _serde_json(v) -> str:
+    """serde_json::to_string's compact form: struct fields in order, strings escaped as serde_json
+    does (", \\, \\b \\f \\n \\r \\t, other controls \\u00xx lowercase; non-ASCII as UTF-8)."""
+    if v is None:
+        return "null"
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, int):
+        return str(v)
+    if isinstance(v, float):
+        return serde_f64(v)
+    if isinstance(v, str):
+        return json.dumps(v, ensure_ascii=False)
+    if isinstance(v, dict):
+        return "{" + ",".join(f"{json.dumps(str(k), ensure_ascii=False)}:{_serde_json(x)}" for k, x in v.items()) + "}"
+    if isinstance(v, (list, tuple)):
+        return "[" + ",".join(_serde_json(x) for x in v) + "]"
+    raise TypeError(f"cannot serialise {type(v).__name__} as serde_json")
+
+
 def metadata_json(oxen_metadata) -> str:
-    """serde_json::to_string of the (untagged) GenericMetadata, or "null" for None.
+    """serde_json::to_string of the (untagged) GenericMetadata (model/metadata/generic_metadata.rs:8-17),
+    or "null" for None (hasher.rs:95-100).
 
     Dicts are serialised compactly in insertion order (= Rust struct field order); non-ASCII is
-    written as UTF-8 like serde_json."""
+    written as UTF-8 like serde_json; floats as serde_json's f64 (serde_f64: ryu, NaN / inf -> null),
+    and the f64 fields of MetadataAudio / MetadataVideo (num_seconds) as floats even when given an int.
+    An object with to_json() serialises itself."""
     if hasattr(oxen_metadata, "to_json"):
         return oxen_metadata.to_json()
-    return json.dumps(oxen_metadata, separators=(",", ":"), ensure_ascii=False)
+    if isinstance(oxen_metadata, dict) and len(oxen_metadata) == 1:
+        (kind, body), = oxen_metadata.items()
+        if kind in _F64_FIELDS and isinstance(body, dict):
+            body = {k: (float(x) if k in _F64_FIELDS[kind] and isinstance(x, int) and not isinstance(x, bool) else x)
+                    for k, x in body.items()}
+            oxen_metadata = {kind: body}
+    return _serde_json(oxen_metadata)
 
 
 def get_metadata_hash(oxen_metadata) -> int:

@@ -33,7 +33,7 @@ def test_built_for_gfx950(built_lib):
 
 def test_abi_version_and_format(built_lib):
     L = _capi.lib()
-    assert L.oxh_abi_version() == 4
+    assert L.oxh_abi_version() == 5
     buf = ctypes.create_string_buffer(40)
     # unpadded lowercase hex (merkle_hash.rs:73-77)
     n = L.oxh_format_hex(0x688558138047f8a, 0x2da4b9c5a75caad3 >> 4, buf)

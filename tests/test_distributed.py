@@ -116,7 +116,7 @@ def test_pipelined_gather_gloo():
     assert res == {0: True, 1: True}
 
 
-def _comm_id_worker(rank, world, port, q):
+def _comm_id_worker(rank, world, port, q, bad_rank):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -131,24 +131,30 @@ def _comm_id_worker(rank, world, port, q):
 
         comm.DigestComm.unique_id = staticmethod(no_rccl)
         comm.DigestComm.__init__ = never
+        # every rank's own check passes, or (bad_rank) one rank's device/RCCL check fails
+        comm.comm_check = lambda device: (_capi.OxenError("device index out of range (test)", _capi.OXH_ERR_INVALID)
+                                          if rank == bad_rank else None)
         try:
             comm.comm_from_process_group(rank, world, 0)
             q.put((rank, "no error"))
         except _capi.OxenError as e:
-            q.put((rank, e.code, "rank 0 could not create the comm id" in str(e)))
+            want = "rank 0 could not create the comm id" if bad_rank < 0 else f"rank {bad_rank} cannot join"
+            q.put((rank, e.code, want in str(e)))
     finally:
         dist.destroy_process_group()
 
 
-def test_comm_id_failure_raises_on_every_rank():
-    """comm_from_process_group: when rank 0 cannot create the RCCL id, every rank raises the same
-    error (none waits in the broadcast or in oxh_comm_create), so bench.py's collective fallback to
-    torch's all-gather is reached by all of them."""
+@pytest.mark.parametrize("bad_rank", [-1, 2])
+def test_comm_id_failure_raises_on_every_rank(bad_rank):
+    """comm_from_process_group: when rank 0 cannot create the RCCL id (bad_rank -1), or when one
+    rank's own oxh_comm_check fails (a bad device index or no RCCL on rank 2: ADVICE r05), every rank
+    raises the same error before any rank enters oxh_comm_create (none waits in the broadcast or in
+    RCCL's bootstrap), so bench.py's collective fallback to torch's all-gather is reached by all."""
     world = 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_comm_id_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_comm_id_worker, args=(r, world, port, q, bad_rank)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -157,4 +163,5 @@ def test_comm_id_failure_raises_on_every_rank():
     from oxen_amd import _capi
 
     got = sorted(q.get(timeout=10) for _ in range(world))
-    assert got == [(r, _capi.OXH_ERR_HIP, True) for r in range(world)]
+    code = _capi.OXH_ERR_HIP if bad_rank < 0 else _capi.OXH_ERR_INVALID
+    assert got == [(r, code, True) for r in range(world)]

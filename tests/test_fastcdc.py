@@ -712,3 +712,63 @@ def test_host_chunk_entries_empty_calls(cuda):
     finally:
         for c in ctxs:
             c.close()
+
+
+@pytest.mark.gpu
+def test_host_chunk_entries_low_fd_limit(cuda, oracle_lib, tmp_path):
+    """the host chunk entries under a low descriptor limit. 2 000 empty files (which used to
+    keep their descriptors to the end of the call), 300 small files and a few missing paths, with the
+    soft RLIMIT_NOFILE lowered to what the process holds + 200: every file is chunked (or reported
+    missing with ENOENT, like fs::read), no spurious OXH_ERR_OPEN from EMFILE -- on one context and on
+    three side by side (the _multi entries split the descriptor budget over their shares)."""
+    import errno
+    import resource
+
+    from oxen_amd import _capi, dedup
+
+    rng = np.random.default_rng(2300)
+    datas, paths = [], []
+    for i in range(2320):
+        p = tmp_path / f"e{i:05d}"
+        if i % 8 == 3 and len([d for d in datas if d is not None and len(d)]) < 300:
+            d = rng.integers(0, 256, int(rng.integers(1, 50_000)), dtype=np.uint8)
+        elif i % 500 == 7:
+            paths.append(str(p) + ".missing")
+            datas.append(None)
+            continue
+        else:
+            d = np.zeros(0, np.uint8)
+        p.write_bytes(d.tobytes())
+        datas.append(d)
+        paths.append(str(p))
+    missing = [i for i, d in enumerate(datas) if d is None]
+    ctxs = [_capi.Context(0) for _ in range(3)]
+    one = _capi.Context(0)
+    for c in [one] + ctxs:  # pipelines and reader pools made before the limit drops
+        dedup.fastcdc_host([np.zeros(10, np.uint8)], 4096, 8192, 16384, ctx=c)
+    dedup.fastcdc_host([np.zeros(10, np.uint8)], 4096, 8192, 16384, ctxs=ctxs)
+    soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+    low = len(os.listdir("/proc/self/fd")) + 200
+    if hard != resource.RLIM_INFINITY and low > hard:
+        pytest.skip("hard descriptor limit below the test's")
+    try:
+        resource.setrlimit(resource.RLIMIT_NOFILE, (low, hard))
+        for kw in ({"ctx": one}, {"ctxs": ctxs}):
+            tab = dedup.fastcdc_files(paths, 4096, 8192, 16384, **kw)
+            fix = dedup.chunk_digests_files(paths, 4096, **kw)
+            for t in (tab, fix):
+                bad = [i for i in range(len(paths)) if (i in missing) != (t.status[i] != 0)]
+                assert not bad, (kw.keys(), bad[:5], [int(t.status[i]) for i in bad[:5]])
+                assert all(t.status[i] == _capi.OXH_ERR_OPEN and t.os_error[i] == errno.ENOENT for i in missing)
+            _check_table(oracle_lib, tab, datas, 4096, 8192, 16384)
+            for i, d in enumerate(datas):
+                if d is None or not len(d):
+                    assert len(fix.file(i)) == 0
+                    continue
+                offs = np.arange(0, len(d), 4096, dtype=np.uint64)
+                lens = np.minimum(np.uint64(4096), np.uint64(len(d)) - offs)
+                assert np.array_equal(fix.file(i), oracle_lib.batch(d, offs, lens)), i
+    finally:
+        resource.setrlimit(resource.RLIMIT_NOFILE, (soft, hard))
+        for c in [one] + ctxs:
+            c.close()

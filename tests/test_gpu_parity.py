@@ -325,7 +325,7 @@ def test_hash_buffers_and_streams(ctx, oracle_lib, golden):
     assert [format(d, "x") for d in got] == [s["hex"] for s in streams]
 
 
-def test_hasher_mirror_api(ctx, golden, tmp_path):
+def test_hasher_mirror_api(ctx, golden, tmp_path, oracle_lib):
     """liboxen util::hasher names and semantics (hasher.rs:11-244) on the GPU path."""
     import io
 
@@ -342,6 +342,13 @@ def test_hasher_mirror_api(ctx, golden, tmp_path):
     c = int(r0["hex"], 16)
     assert format(hasher.get_combined_hash(hasher.get_metadata_hash(md), c), "x") == r0["combined_hash"]
     assert hasher.get_combined_hash(None, c) == c
+    # a non-text GenericMetadata (MetadataAudio, an f64 field) through the GPU path, against the oracle
+    # over serde_json's text (tests/test_host.py pins the text)
+    O = oracle_lib
+    audio = {"audio": {"num_seconds": 1e-5, "num_channels": 2, "sample_rate": 44100}}
+    js = b'{"audio":{"num_seconds":0.00001,"num_channels":2,"sample_rate":44100}}'
+    assert hasher.get_metadata_hash(audio) == O.xxh3_128_int(js)
+    assert hasher.get_combined_hash(hasher.get_metadata_hash(audio), c) == O.combined_hash(c, O.xxh3_128_int(js))
     p = tmp_path / "a.txt"
     p.write_bytes(b"File content 0")
     assert hasher.hash_file_contents(str(p)) == r0["hex"]

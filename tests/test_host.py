@@ -95,6 +95,61 @@ def test_metadata_json_matches_serde(golden):
     assert metadata_json(None) == "null"
 
 
+# serde_json's f64 text (ryu's format64), hand-derived -- parity unpinned: no reference fixture holds
+# float-bearing metadata. d = shortest digits, value = d x 10^k, kk = len(d) + k:
+#   12.5    d=125 k=-1 kk=2   -> point after 2 digits          "12.5"
+#   12.0    d=12  k=0  kk=2   -> digits + k zeros + ".0"        "12.0"
+#   1e-5    d=1   k=-5 kk=-4  -> -5 < kk <= 0: "0." 4 zeros d   "0.00001"
+#   1e-6    d=1   k=-6 kk=-5  -> one digit: "1e" (kk-1)         "1e-6"
+#   1e16    d=1   k=16 kk=17  -> kk > 16, one digit             "1e16"
+#   1e15    d=1   k=15 kk=16  -> digits + 15 zeros + ".0"       "1000000000000000.0"
+#   1.5e16  d=15  k=15 kk=17  -> d0 "." rest "e" (kk-1)         "1.5e16"
+#   NaN, inf                  -> serde_json's serialize_f64     "null"
+SERDE_F64 = [(12.5, "12.5"), (12.0, "12.0"), (1e-5, "0.00001"), (1e-6, "1e-6"), (1e16, "1e16"),
+             (1e15, "1000000000000000.0"), (1.5e16, "1.5e16"), (1.25e-7, "1.25e-7"), (0.1, "0.1"), (0.0, "0.0"),
+             (-0.0, "-0.0"), (-3.75, "-3.75"), (5e-324, "5e-324"), (1.7976931348623157e308, "1.7976931348623157e308"),
+             (9007199254740992.0, "9007199254740992.0"), (float("nan"), "null"), (float("inf"), "null"),
+             (float("-inf"), "null")]
+
+
+@pytest.mark.parametrize("x,want", SERDE_F64, ids=[w if w != "null" else repr(x) for x, w in SERDE_F64])
+def test_serde_f64(x, want):
+    from oxen_amd.hasher import serde_f64
+
+    assert serde_f64(x) == want
+
+
+def test_metadata_json_audio_video_floats():
+    """MetadataAudio / MetadataVideo (model/metadata/metadata_audio.rs:5-15, metadata_video.rs:5-15) as
+    serde_json writes them through GenericMetadata (untagged): field order, f64 num_seconds in ryu form
+    (an int given for it still prints as a float), usize fields as integers, NaN as null."""
+    from oxen_amd.hasher import metadata_json
+
+    for secs, txt in [(12.5, "12.5"), (12.0, "12.0"), (12, "12.0"), (1e-5, "0.00001"), (1e16, "1e16"),
+                      (float("nan"), "null")]:
+        assert metadata_json({"audio": {"num_seconds": secs, "num_channels": 2, "sample_rate": 44100}}) == \
+            '{"audio":{"num_seconds":%s,"num_channels":2,"sample_rate":44100}}' % txt
+        assert metadata_json({"video": {"num_seconds": secs, "width": 1920, "height": 1080}}) == \
+            '{"video":{"num_seconds":%s,"width":1920,"height":1080}}' % txt
+    # integers stay integers outside the f64 fields; strings escape like serde_json
+    assert metadata_json({"text": {"num_lines": 3, "num_chars": 9}}) == '{"text":{"num_lines":3,"num_chars":9}}'
+    assert metadata_json({"x": "a\"b\\c\n\x01\u00e9/"}) == '{"x":"a\\"b\\\\c\\n\\u0001\u00e9/"}'
+    assert metadata_json({"x": [True, None, 1.0]}) == '{"x":[true,null,1.0]}'
+
+
+def test_metadata_hash_audio_on_oracle(oracle_lib):
+    """get_metadata_hash / get_combined_hash (hasher.rs:67-100) of a non-text GenericMetadata, on the
+    oracle: XXH3-128 of the serde_json text above, then of content || metadata (LE u128s)."""
+    from oxen_amd.hasher import metadata_json
+
+    js = metadata_json({"audio": {"num_seconds": 12.5, "num_channels": 2, "sample_rate": 44100}})
+    assert js == '{"audio":{"num_seconds":12.5,"num_channels":2,"sample_rate":44100}}'
+    m = oracle_lib.xxh3_128_int(js.encode())
+    c = oracle_lib.xxh3_128_int(b"audio bytes")
+    comb = oracle_lib.combined_hash(c, m)
+    assert comb == oracle_lib.xxh3_128_int(c.to_bytes(16, "little") + m.to_bytes(16, "little"))
+
+
 @pytest.mark.parametrize("second", [False, True])
 @pytest.mark.parametrize("vnode_size", [10_000, 7])
 def test_commit_driver_host_logic(monkeypatch, oracle_lib, second, vnode_size):
