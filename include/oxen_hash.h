@@ -405,6 +405,10 @@ int oxh_format_dec(uint64_t lo, uint64_t hi, char* out);
 int oxh_fill_splitmix(void* d_buf, uint64_t nbytes, uint64_t seed, void* stream);
 /* Diagnostic: select the long-path kernel variant (0 = default). Returns the previous value. */
 int oxh_set_kernel_variant(int variant);
+/* Diagnostic counters of a context, out[0..n): [0] device allocations of the large-file piece buffers
+ * (files above a staging slot; each one synchronises the device), [1] their current bytes; further
+ * entries 0. */
+int oxh_ctx_counters(oxh_ctx* ctx, uint64_t* out, int n);
 
 #ifdef __cplusplus
 }

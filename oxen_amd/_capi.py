@@ -105,6 +105,7 @@ SIGNATURES = {
     "oxh_fastcdc_gear": (_int, [_u64p]),
     "oxh_fastcdc_masks": (_int, [_u32, _u32, _u64p, _u64p]),
     "oxh_comm_check": (_int, [_int]),
+    "oxh_ctx_counters": (_int, [_vp, _u64p, _int]),
     "oxh_comm_unique_id": (_int, [ctypes.c_char_p]),
     "oxh_comm_create": (_int, [ctypes.c_char_p, _int, _int, _int, ctypes.POINTER(_vp)]),
     "oxh_comm_info": (_int, [_vp, ctypes.POINTER(_int), ctypes.POINTER(_int), ctypes.POINTER(_int)]),
@@ -168,6 +169,12 @@ class Context:
     @property
     def stream(self) -> int:
         return lib().oxh_ctx_stream(self.handle) or 0
+
+    def counters(self) -> dict:
+        """oxh_ctx_counters: large-file piece-buffer allocations and their current bytes."""
+        out = (ctypes.c_uint64 * 2)()
+        check(lib().oxh_ctx_counters(self.handle, out, 2), "oxh_ctx_counters")
+        return {"big_allocs": int(out[0]), "big_bytes": int(out[1])}
 
     def close(self) -> None:
         if getattr(self, "handle", None):

@@ -285,6 +285,7 @@ struct oxh_ctx {
     // and two pinned bounce buffers the file is read into in pieces
     uint8_t* d_big = nullptr;
     uint64_t d_big_size = 0;
+    uint64_t d_big_allocs = 0;   // times d_big was (re)allocated (oxh_ctx_counters)
     uint8_t* h_bounce[8] = {};   // kNBounce pinned bounce buffers, used as a ring
     hipEvent_t ev_bounce[8] = {};
     bool bounce_used[8] = {};
@@ -740,22 +741,34 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
         for (int q = 0; q < n; ++q) jobs[q].res.status = OXH_ERR_NOMEM;
         return OXH_OK;
     };
-    const uint64_t need = (uint64_t)n * (2 * slot + kRes) + 4096;
+    auto bytes_for = [&](int items) { return (uint64_t)items * (2 * slot + kRes) + 4096; };
+    const uint64_t need = bytes_for(n);
     c->where.store("large_items: d_big");
     if (c->d_big_size < need) {
         // Regrow: every earlier large_items call on this context finished its work on d_big before it
         // returned (its streams are synchronised at the end), so the old buffer is idle. Plain
         // hipFree / hipMalloc: the stream-ordered allocator (hipMallocAsync / hipFreeAsync on
-        // c->stream, r04) deadlocked inside the runtime under concurrent contexts -- threads stuck
-        // in hipMallocAsync beside others in hipEventRecord / hipHostMalloc with every stream idle
-        // (tools/engine_soak.py --regrow with a device soak beside it, profiles/r05/r05s6_*).
+        // c->stream, r04) was AVOIDED after a stall under concurrent contexts (threads parked in
+        // hipMallocAsync beside others in hipEventRecord / hipHostMalloc, every stream idle;
+        // tools/engine_soak.py --regrow, profiles/r05/r05s6_*) -- not proven faulty, no reduced
+        // reproducer. hipFree synchronises the whole device, so a regrow waits on every other
+        // context's work: the buffer is sized for the most items the engine batches
+        // (big_files_at_once(), or n if more) at once, so a context pays this once per piece size,
+        // not once per new n (oxh_ctx_counters counts it; DESIGN §5 "Soak").
         if (c->d_big) {
             (void)hipFree(c->d_big);
             c->d_big = nullptr;
             c->d_big_size = 0;
         }
         void* m = nullptr;
-        const bool ok = hipMalloc(&m, need) == hipSuccess && m != nullptr;
+        uint64_t size = std::max(need, bytes_for(big_files_at_once()));
+        bool ok = hipMalloc(&m, size) == hipSuccess && m != nullptr;
+        if (!ok && size > need) {  // the full batch does not fit: just these n items
+            (void)hipGetLastError();
+            size = need;
+            ok = hipMalloc(&m, size) == hipSuccess && m != nullptr;
+        }
+        if (ok) ++c->d_big_allocs;
         if (!ok) {
             (void)hipGetLastError();
             // 2 piece buffers per file side by side did not fit: fewer files at a time (each item's
@@ -768,7 +781,7 @@ int large_items(oxh_ctx* c, LargeJob* jobs, int n) {
             return nomem();
         }
         c->d_big = (uint8_t*)m;
-        c->d_big_size = need;
+        c->d_big_size = size;
     }
     auto dbuf = [&](int q, int b) { return c->d_big + ((uint64_t)q * 2 + b) * slot; };
     uint8_t* d_res_all = c->d_big + (uint64_t)n * 2 * slot;
@@ -1092,6 +1105,13 @@ int k1_packed(const void* d_arena, const uint64_t* d_offsets, const uint64_t* d_
 extern "C" {
 
 int oxh_abi_version(void) { return OXH_ABI_VERSION; }
+
+int oxh_ctx_counters(oxh_ctx* c, uint64_t* out, int n) {
+    if (!c || (n > 0 && !out)) return fail(OXH_ERR_INVALID, "null argument");
+    const uint64_t v[2] = {c->d_big_allocs, c->d_big_size};
+    for (int i = 0; i < n; ++i) out[i] = i < 2 ? v[i] : 0;
+    return OXH_OK;
+}
 const char* oxh_last_error(void) { return g_err.c_str(); }
 
 int oxh_device_count(int* count) {

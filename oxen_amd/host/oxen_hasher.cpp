@@ -874,10 +874,7 @@ std::vector<bool> should_restore_batch(const std::vector<RestoreCheck>& files, b
         if (stat(f.working_path.c_str(), &sb) != 0) continue;
         const NodeHashes& ref = f.base ? *f.base : f.target;
         if (f.mtime_matched && (uint64_t)sb.st_size == ref.num_bytes) continue;
-        if (combined && f.file_metadata.kind == util::fs::FileMetadataHash::Error)
-            throw OxenError::basic_str(f.file_metadata.error.empty() ? "could not compute file metadata" : f.file_metadata.error,
-                                       OXH_ERR_META);
-        need.push_back(i);
+        need.push_back(i);  // (a metadata Error is raised after this file's hash, below, as restore.rs:334-339)
     }
     if (need.empty()) return out;
     const size_t m = need.size();
@@ -888,10 +885,16 @@ std::vector<bool> should_restore_batch(const std::vector<RestoreCheck>& files, b
     check(oxh_hash_files_ex(ctx, cp.data(), nullptr, m, dig.data(), sizes.data(), status.data(), oserr.data(),
                             combined ? counts.data() : nullptr, nullptr),
           "oxh_hash_files_ex");
-    for (size_t j = 0; j < m; ++j)  // u128_hash_file_contents(&working_path)? -- the first failure in order
+    // per file in order: u128_hash_file_contents(&working_path)?, then (combined) get_file_metadata(..)?
+    // (restore.rs:334-339 / :377-382) -- the first failing file's first failure is the error
+    for (size_t j = 0; j < m; ++j) {
+        const RestoreCheck& f = files[need[j]];
         if (status[j] != OXH_OK)
-            throw OxenError::basic_str(util::hasher::file_error_text(files[need[j]].working_path, status[j], oserr[j], sizes[j]),
-                                       status[j]);
+            throw OxenError::basic_str(util::hasher::file_error_text(f.working_path, status[j], oserr[j], sizes[j]), status[j]);
+        if (combined && f.file_metadata.kind == util::fs::FileMetadataHash::Error)
+            throw OxenError::basic_str(f.file_metadata.error.empty() ? "could not compute file metadata" : f.file_metadata.error,
+                                       OXH_ERR_META);
+    }
     std::vector<u128> h(m);
     for (size_t j = 0; j < m; ++j) h[j] = to_u128(dig[2 * j], dig[2 * j + 1]);
     if (combined) {  // maybe_get_metadata_hash + get_combined_hash (hasher.rs:67-100), batched

@@ -54,21 +54,26 @@ def should_restore(paths: Sequence[str], targets: Sequence[NodeHashes], bases: S
         raise _capi.OxenError("should_restore: argument lengths differ", _capi.OXH_ERR_INVALID)
     out: list[Optional[bool]] = [None] * n
     need: list[int] = []
+    stat_error: Optional[tuple[int, OxenError]] = None  # the first file whose metadata(..)? fails
     for i, p in enumerate(paths):
         if not os.path.exists(p):  # working_path.exists() (follows symlinks)
             out[i] = True
             continue
         try:
-            size = os.stat(p).st_size  # util::fs::metadata(&working_path)?
+            size = os.stat(p).st_size  # util::fs::metadata(&working_path)? (only a race after exists())
         except OSError as e:
-            raise OxenError(f"Could not get file metadata: {rust_path_debug(p)} error {rust_io_error_debug(e.errno or 0)}",
-                            _capi.OXH_ERR_IO) from None
+            # raised after the hashes of the files before it: an earlier file's hash error comes first
+            stat_error = (i, OxenError(f"Could not get file metadata: {rust_path_debug(p)} error "
+                                       f"{rust_io_error_debug(e.errno or 0)}", _capi.OXH_ERR_IO))
+            break
         ref = bases[i] if bases[i] is not None else targets[i]
         if mtime_matched[i] and size == ref.num_bytes:
             out[i] = True
             continue
         need.append(i)
     if not need:
+        if stat_error is not None:
+            raise stat_error[1]
         return [bool(x) for x in out]
     meta = [None] * n if file_metadata is None else list(file_metadata)
     text = [i for i in need if combined and isinstance(meta[i], str) and meta[i] == TEXT]
@@ -102,6 +107,8 @@ def should_restore(paths: Sequence[str], targets: Sequence[NodeHashes], bases: S
                 _, _, st2, oe2 = hash_files_with_errors_128bit([paths[i]], ctx=ctx)
                 st, oe = (st2[0], oe2[0]) if st2[0] != 0 else (st, 0)
             raise file_error(paths[i], st, oe)
+    if stat_error is not None:  # every file before it hashed cleanly
+        raise stat_error[1]
     if combined:  # get_combined_hash (hasher.rs:67-80) of every file with a metadata hash, one batch
         for i in need:
             t, b = targets[i], bases[i]

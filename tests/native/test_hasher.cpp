@@ -611,6 +611,16 @@ static void restore_checks() {
     d.working_path = dir;  // a directory: the hash's read fails (EISDIR) and the call throws
     d.target = node(newv, false);
     CHECK(throws_oxen([&] { rs::should_restore_batch({d}, false); }, "Could not read file for hashing"));
+    // the first failing FILE's error: per file the hash comes before get_file_metadata
+    // (restore.rs:334-339), so file 0's read error beats file 1's metadata error, and the other way round
+    rs::RestoreCheck bad_meta;
+    bad_meta.working_path = put("meta.txt", other);
+    bad_meta.target = node(newv, true);
+    bad_meta.file_metadata.kind = liboxen::util::fs::FileMetadataHash::Error;
+    bad_meta.file_metadata.error = "metadata failed (test)";
+    d.target = node(newv, true);
+    CHECK(throws_oxen([&] { rs::should_restore_batch({d, bad_meta}, true); }, "Could not read file for hashing"));
+    CHECK(throws_oxen([&] { rs::should_restore_batch({bad_meta, d}, true); }, "metadata failed (test)"));
     const std::string rm = std::string("rm -rf ") + dir;
     if (system(rm.c_str()) != 0) fprintf(stderr, "could not remove %s\n", dir);
 }

@@ -92,3 +92,38 @@ def test_k1l_default_pieces_file(cuda, oracle_lib, tmp_path, monkeypatch):
     assert int(status_b[0]) == 0 and int(sizes_b[0]) == size
     assert (int(out_b[0, 1]) << 64) | int(out_b[0, 0]) == want_int
     os.remove(blob)
+
+
+def test_large_item_buffer_allocations_stay_rare(cuda, oracle_lib, tmp_path, monkeypatch):
+    """the large-file piece buffers (files above a staging slot) are sized for the most
+    files the engine batches (OXH_BIG_FILES) on first use, so a context allocates them once -- each
+    allocation is a hipFree / hipMalloc that synchronises the whole device -- not once per new batch
+    size. Rising batches of 1, 2, 3, 4 and 6 large files, the device entry beside them: one allocation;
+    raising OXH_BIG_FILES to 8 takes exactly one more. Every digest equals the oracle's."""
+    from oxen_amd import _capi, hasher
+
+    monkeypatch.setenv("OXH_BIG_PIECE_MIB", "4")
+    monkeypatch.delenv("OXH_BIG_FILES", raising=False)
+    rng = np.random.default_rng(45)
+    paths, want = [], []
+    for i in range(8):
+        d = rng.integers(0, 256, (3 << 20) + 5000 + 777 * i, dtype=np.uint8)  # 3 MiB + : above a 1 MiB slot
+        p = tmp_path / f"big{i}"
+        p.write_bytes(d.tobytes())
+        paths.append(str(p))
+        w = oracle_lib.batch(d, np.zeros(1, np.uint64), np.array([len(d)], np.uint64))[0]
+        want.append((int(w[1]) << 64) | int(w[0]))
+    with _capi.Context(0, staging_bytes=1 << 20) as ctx:
+        assert ctx.counters()["big_allocs"] == 0
+        for n in (1, 2, 3, 4, 6):
+            got, sizes, status = hasher.hash_files_128bit(paths[:n], ctx=ctx)
+            assert status == [0] * n and got == want[:n], n
+        c = ctx.counters()
+        assert c["big_allocs"] == 1, c
+        monkeypatch.setenv("OXH_BIG_FILES", "8")
+        got, _, status = hasher.hash_files_128bit(paths, ctx=ctx)
+        assert status == [0] * 8 and got == want
+        c2 = ctx.counters()
+        assert c2["big_allocs"] <= 2 and c2["big_bytes"] >= c["big_bytes"], (c, c2)
+        got, _, _ = hasher.hash_files_128bit(paths[:3], ctx=ctx)
+        assert got == want[:3] and ctx.counters()["big_allocs"] == c2["big_allocs"]

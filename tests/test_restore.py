@@ -135,3 +135,35 @@ def test_should_restore_short_cuts_need_no_device(tmp_path):
         assert restore.should_restore([], [], [], [], combined=combined) == []
     with pytest.raises(_capi.OxenError, match="lengths differ"):
         restore.should_restore([str(f)], [t], [None, None], [True])
+
+
+@pytest.mark.gpu
+def test_should_restore_first_failing_file_wins(cuda, tmp_path, monkeypatch):
+    """per file the reference runs metadata(..)? then the hash (restore.rs:311, :334), so
+    the error raised is the first failing FILE's: a hash failure on file 0 beats a stat failure on
+    file 1 (the stat failure is a race after exists(), simulated here), and a stat failure on file 0
+    beats file 1's hash failure."""
+    import os
+
+    from oxen_amd import _capi, restore
+    from oxen_amd.restore import NodeHashes
+
+    d = tmp_path / "adir"
+    d.mkdir()  # exists, stats, fails its read (EISDIR)
+    f = tmp_path / "racy.txt"
+    f.write_bytes(b"hello")
+    n = NodeHashes(hash=1, num_bytes=5, combined_hash=1)
+    real_stat = os.stat
+
+    def stat(p, *a, **k):
+        if str(p) == str(f):
+            raise FileNotFoundError(2, "gone")
+        return real_stat(p, *a, **k)
+
+    import types
+
+    monkeypatch.setattr(restore, "os", types.SimpleNamespace(path=os.path, stat=stat))
+    with pytest.raises(_capi.OxenError, match="Could not read file for hashing"):
+        restore.should_restore([str(d), str(f)], [n, n], [None, None], [False, False])
+    with pytest.raises(_capi.OxenError, match="Could not get file metadata"):
+        restore.should_restore([str(f), str(d)], [n, n], [None, None], [False, False])
