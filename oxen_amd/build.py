@@ -13,10 +13,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "liboxen_hash.so")
-SOURCES = [os.path.join(CSRC, "xxh3_kernels.hip"), os.path.join(CSRC, "oxen_hash_capi.hip"), os.path.join(CSRC, "fastcdc.hip"),
-           os.path.join(CSRC, "reader_pool.cpp"), os.path.join(CSRC, "comm.cpp"), os.path.join(CSRC, "fastcdc_host.cpp")]
-DEPS = SOURCES + [os.path.join(CSRC, "xxh3_device.hpp"), os.path.join(CSRC, "fastcdc_gear.h"), os.path.join(CSRC, "pool.hpp"), os.path.join(CSRC, "scratch.hpp"),
-                  os.path.join(CSRC, "reader_pool.hpp"), os.path.join(ROOT, "include", "oxen_hash.h")]
+# the C ABI runtime (capi_internal.hpp lists its pieces), the kernels, FastCDC, the reader pool, RCCL
+SOURCES = [os.path.join(CSRC, f) for f in (
+    "xxh3_kernels.hip", "capi_dispatch.hip", "capi_context.hip", "staging.hip", "large_items.hip", "xxh3_stream.hip",
+    "engine.hip", "modified.hip", "publish.hip", "fastcdc.hip", "reader_pool.cpp", "comm.cpp", "fastcdc_host.cpp")]
+DEPS = SOURCES + [os.path.join(CSRC, h) for h in ("capi_internal.hpp", "xxh3_device.hpp", "fastcdc_gear.h", "pool.hpp",
+                                                 "scratch.hpp", "reader_pool.hpp")] + [os.path.join(ROOT, "include", "oxen_hash.h")]
 HELPER_SRC = os.path.join(CSRC, "hash_helper.cpp")
 HELPER = os.path.join(HERE, "oxh_hash_helper")  # the reader-pool helper process (oxh_pool_*)
 ARCH = "gfx950"

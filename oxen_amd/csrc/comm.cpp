@@ -23,7 +23,7 @@
 #include "../../include/oxen_hash.h"
 
 namespace oxh {
-int set_error(int code, const std::string& msg);  // oxen_hash_capi.hip
+int set_error(int code, const std::string& msg);  // capi_context.hip
 }
 
 namespace {

@@ -50,9 +50,9 @@
 
 namespace oxh {
 
-int set_error(int code, const std::string& msg);  // oxen_hash_capi.hip: oxh_last_error() text
+int set_error(int code, const std::string& msg);  // capi_context.hip: oxh_last_error() text
 int k1_packed(const void* d_arena, const uint64_t* d_offsets, const uint64_t* d_lens, uint64_t n, uint64_t* d_out,
-              uint64_t mean_len, hipStream_t st);  // oxen_hash_capi.hip
+              uint64_t mean_len, hipStream_t st);  // capi_dispatch.hip
 __global__ void xxh3_rows_fold_kernel(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t*,
                                       const uint64_t*, const uint8_t*);  // xxh3_kernels.hip (K1F)
 

@@ -44,8 +44,8 @@
 #include "pool.hpp"
 
 namespace oxh {
-int set_error(int code, const std::string& msg);            // oxen_hash_capi.hip
-int ctx_device(oxh_ctx* c);                                 // oxen_hash_capi.hip
+int set_error(int code, const std::string& msg);            // capi_context.hip
+int ctx_device(oxh_ctx* c);                                 // capi_context.hip
 std::mutex& ctx_call_mutex(oxh_ctx* c);                     // ... serialises a context's non-engine calls
 void*& ctx_cdc_state(oxh_ctx* c, void (*deleter)(void*));   // ... a slot the context frees on destroy
 int default_reader_threads();                               // ... OXH_NUM_THREADS / the CPU quota, <= 16

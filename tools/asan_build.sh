@@ -18,9 +18,10 @@ SAN="-Xarch_host -fsanitize=address -Xarch_host -fno-omit-frame-pointer"
 # the runtime as a DT_NEEDED of each library, so programs linked against them resolve its symbols
 RT=$(ls /opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so | head -1)
 RTLINK="-Wl,$RT -Wl,-rpath,$(dirname "$RT")"
+# the product library's own source list (oxen_amd/build.py SOURCES), so the two never drift apart
+SRCS=$(python3 -c 'from oxen_amd import build; print(" ".join(build.SOURCES))')
 $HIPCC --offload-arch=gfx950 -O3 -Xarch_host -g -std=c++17 -shared -fPIC -Wall $SAN -o $OUT/liboxen_hash.so \
-  oxen_amd/csrc/xxh3_kernels.hip oxen_amd/csrc/oxen_hash_capi.hip oxen_amd/csrc/fastcdc.hip oxen_amd/csrc/reader_pool.cpp \
-  oxen_amd/csrc/comm.cpp oxen_amd/csrc/fastcdc_host.cpp $RTLINK
+  $SRCS $RTLINK
 $CLANGXX -std=c++17 -O1 -g -fno-gpu-sanitize -fsanitize=address -fno-omit-frame-pointer -shared -fPIC -Wall \
   -o $OUT/liboxen_hasher.so oxen_amd/host/oxen_hasher.cpp oxen_amd/host/commit_writer.cpp \
   -L$OUT -l:liboxen_hash.so -Wl,-rpath,'$ORIGIN' $RTLINK
