@@ -226,13 +226,18 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL on ROCm); gloo only to rehearse N>1 on one GPU")
-    ap.add_argument("--gather", choices=["abi", "torch"], default="abi",
-                    help="N > 1 on RCCL: the digest gather through the C ABI (oxh_gather_digests, default) or "
-                         "torch.distributed's all-gather (the fallback when the ABI gather cannot come up)")
+    ap.add_argument("--gather", choices=["abi", "torch", "host"], default=None,
+                    help="N > 1: the digest gather through the C ABI (oxh_gather_digests; the default on nccl), "
+                         "torch.distributed's all-gather (the fallback when the ABI gather cannot come up), or "
+                         "host tables over the process group (the default on gloo). abi on gloo: the ABI gather "
+                         "with the id broadcast over gloo -- with OXH_RCCL_LIB=tests/native/libfake_rccl.so it "
+                         "rehearses the whole N > 1 step with every rank on one GPU (tests/test_bench_launch.py)")
     ap.add_argument("--dist", action="store_true",
                     help="take the N>1 path (process group, pipelined RCCL gather) even at WORLD_SIZE=1: "
                          "rehearses the multi-GPU step on a one-GPU box under torch.distributed.run")
     args = ap.parse_args()
+    if args.gather is None:
+        args.gather = "abi" if args.backend == "nccl" else "host"
     if args.gpus < 1:
         log("[bench] --gpus must be >= 1")
         sys.exit(2)
@@ -292,7 +297,13 @@ def main() -> None:
     # the call a Rust host links; rank 0's communicator id travels over the process group.
     comm = None
     gather_via = "none"
-    if multi and args.backend == "nccl":
+    if multi and args.backend != "nccl" and args.gather == "abi":
+        # the ABI gather over a gloo group (the id travels over gloo): no fallback, a failure is the run's
+        from oxen_amd.comm import comm_from_process_group
+
+        comm = comm_from_process_group(rank, world, dev.index)
+        gather_via = "oxh_gather_digests (process group: %s)" % args.backend
+    elif multi and args.backend == "nccl":
         from oxen_amd.comm import comm_from_process_group
 
         err = None

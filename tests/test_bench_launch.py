@@ -54,6 +54,27 @@ def test_bench_two_ranks_gloo_one_gpu(cuda):
     assert d["n_gpus"] == 2 and d["steps"] == 3 and d["config"]["items_per_gpu"] == 2048
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks", [2, 4, 8])
+def test_bench_ranks_abi_gather_fake_rccl(cuda, ranks):
+    """The whole N > 1 bench step as the driver's 8-GPU run takes it -- ranks started by bench.py itself,
+    comm_from_process_group (oxh_comm_check agreed, the id broadcast), shard.PipelinedGather with
+    oxh_gather_digests per step on a side stream, the max over ranks, rank 0's checks of every rank's
+    shard against the oracle -- with every rank on the one GPU of the test box and RCCL replaced by the
+    test double (tests/native/libfake_rccl.so via OXH_RCCL_LIB; the id travels over gloo)."""
+    from oxen_amd import build
+
+    r = _run(["--gpus", str(ranks), "--backend", "gloo", "--gather", "abi", "--workload", "t", "--steps", "3",
+              "--warmup", "1", "--no-cpu-baseline", "--prewarm-s", "0"],
+             env={"OXH_RCCL_LIB": build.FAKE_RCCL, "OXH_FAKE_RCCL_SLOT_BYTES": str(8 << 20)})
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, r.stdout
+    d = json.loads(line[0])
+    assert d["n_gpus"] == ranks and d["steps"] == 3
+    assert "oxh_gather_digests" in d["config"]["parallelism"], d["config"]
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
