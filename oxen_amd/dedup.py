@@ -243,6 +243,23 @@ def _fixed_count(sizes, chunk: int) -> int:
     return int(sum((int(x) + chunk - 1) // chunk for x in sizes))
 
 
+# Measured rates behind INTEGRATION.md §2 "When NOT to call the host chunk entries" (DESIGN §5,
+# profiles/r05/r05j_fixed_e2e_*, r05as_h2d_probe.json): host-resident bytes cross one PCIe link per GPU
+# first (~49 GiB/s each, the host entries at 92-93 % of the link), the reference's CPU loops hash at
+# these rates per core (16 threads: fixed-size 67.7 GiB/s, FastCDC 34.9-40.3 GiB/s).
+LINK_GIBS = 49.0
+CPU_GIBS_PER_CORE = {"fixed": 4.2, "fastcdc": 2.4}
+
+
+def host_entry_pays_off(host_cores: int, links: int, fastcdc: bool) -> bool:
+    """Whether chunk_digests_files / fastcdc_files (and _multi) beat the reference's own CPU loop for
+    host-resident files on this node: links x LINK_GIBS against host_cores x the per-core rate. A
+    routing rule for the caller (bytes already in HBM take the device entries regardless); the library
+    itself has no CPU hashing path."""
+    cpu = host_cores * CPU_GIBS_PER_CORE["fastcdc" if fastcdc else "fixed"]
+    return links * LINK_GIBS > cpu
+
+
 def chunk_digests_files(paths, chunk_size: int, ctx: Optional[_capi.Context] = None, ctxs=None) -> FixedChunkTable:
     """oxh_chunk_digests_files: XXH3-128 of every fixed-size chunk of files on disk, read by the library
     (fixedsize_multithreaded.rs:78-110), digests in host memory; per-file errors as fastcdc_files.

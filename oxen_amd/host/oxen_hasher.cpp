@@ -852,6 +852,11 @@ std::vector<std::vector<Chunk>> fixed_chunk_buffers(const std::vector<std::strin
     return r;
 }
 
+bool host_entry_pays_off(unsigned host_cores, unsigned links, bool fastcdc) {
+    const double cpu = host_cores * (fastcdc ? 2.4 : 4.2), gpu = links * 49.0;  // GiB/s
+    return gpu > cpu;
+}
+
 std::string chunk_name(u128 hash) {
     char b[48];
     oxh_format_dec((uint64_t)hash, (uint64_t)(hash >> 64), b);

@@ -328,6 +328,12 @@ std::vector<std::vector<Chunk>> fixed_chunk_buffers(const std::vector<std::strin
                                                     oxh_ctx* ctx = nullptr);
 std::vector<std::vector<Chunk>> fixed_chunk_buffers(const std::vector<std::string_view>& buffers, uint64_t chunk_size,
                                                     const std::vector<oxh_ctx*>& ctxs);
+// Whether the host chunk entries above beat the reference's own CPU loop for host-resident files on
+// this node (INTEGRATION.md §2 "When NOT to call the host chunk entries"): every byte crosses a PCIe
+// link first, so `links` GPUs move ~49 GiB/s each, against `host_cores` hashing at ~4.2 GiB/s per core
+// (fixed-size) or ~2.4 (FastCDC v2020 + XXH3), as measured on the MI355X boxes. Bytes
+// already in HBM take the device entries regardless. A routing rule for the caller, not a CPU path.
+bool host_entry_pays_off(unsigned host_cores, unsigned links, bool fastcdc);
 // u128::to_string() (fastcdchunker.rs:98, the chunk file name)
 std::string chunk_name(u128 hash);
 }  // namespace dedup

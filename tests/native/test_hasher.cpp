@@ -625,6 +625,17 @@ static void restore_checks() {
     if (system(rm.c_str()) != 0) fprintf(stderr, "could not remove %s\n", dir);
 }
 
+// liboxen::dedup::host_entry_pays_off: INTEGRATION.md §2's routing rule (the same table as dedup.py)
+static void routing_rule_checks() {
+    namespace dd = liboxen::dedup;
+    CHECK(!dd::host_entry_pays_off(16, 1, false));  // fixed-size: 67.2 GiB/s of cores > 49 of one link
+    CHECK(dd::host_entry_pays_off(16, 1, true));    // FastCDC: 38.4 < 49
+    CHECK(dd::host_entry_pays_off(8, 1, false));
+    CHECK(!dd::host_entry_pays_off(128, 8, false));
+    CHECK(dd::host_entry_pays_off(128, 8, true));
+    CHECK(!dd::host_entry_pays_off(64, 0, true));
+}
+
 int main(int argc, char** argv) {
     const std::string golden = argc > 1 ? argv[1] : "tests/golden";
     try {
@@ -638,6 +649,7 @@ int main(int argc, char** argv) {
         modified_check(golden);
         dedup_chunks(golden);
         restore_checks();
+        routing_rule_checks();
         char tmpl[] = "/tmp/oxh_native_XXXXXX";
         const char* scratch = mkdtemp(tmpl);
         if (!scratch) throw std::runtime_error("mkdtemp failed");

@@ -282,3 +282,18 @@ def test_chunk_digests_capacity_errors(cuda, tmp_path):
     rc = L.oxh_chunk_digests_host(ctx.handle, bufs, lens.ctypes.data_as(_capi._u64p), 1, 4096,
                                   dig.ctypes.data_as(_capi._u64p), 3, first.ctypes.data_as(_capi._u64p))
     assert rc == _capi.OXH_ERR_INVALID and b"need 11 entries" in L.oxh_last_error()
+
+
+def test_host_entry_routing_rule():
+    """INTEGRATION.md §2's rule as code (dedup.host_entry_pays_off; C++ liboxen::dedup::host_entry_pays_off
+    in test_hasher.cpp): on the measured 16-core box with one GPU the fixed-size host entry loses to the
+    CPU loop (67.7 vs 50.8 GiB/s) and FastCDC's wins (46.9-50.0 vs 34.9-40.3); more links or fewer cores
+    move the crossover."""
+    from oxen_amd import dedup
+
+    assert not dedup.host_entry_pays_off(16, 1, fastcdc=False)
+    assert dedup.host_entry_pays_off(16, 1, fastcdc=True)
+    assert dedup.host_entry_pays_off(8, 1, fastcdc=False)       # 33.6 < 49 GiB/s
+    assert not dedup.host_entry_pays_off(128, 8, fastcdc=False)  # 537.6 > 392
+    assert dedup.host_entry_pays_off(128, 8, fastcdc=True)       # 307.2 < 392
+    assert not dedup.host_entry_pays_off(64, 0, fastcdc=True)    # no GPU, no link
