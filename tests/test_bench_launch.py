@@ -97,6 +97,11 @@ def test_pipelined_gather_rccl_in_process(cuda, oracle_lib):
     from oxen_amd.device import DeviceArena, to_numpy_u64
     from oxen_amd.shard import PipelinedGather
 
+    from oxen_amd.comm import comm_check
+
+    assert comm_check(cuda.index or 0) is None  # RCCL loads, the device is visible
+    bad = comm_check(99)
+    assert bad is not None and bad.code == _capi.OXH_ERR_INVALID and "out of range" in str(bad)
     with DigestComm(DigestComm.unique_id(), 0, 1, cuda.index or 0) as comm:
         assert comm.info() == (0, 1, cuda.index or 0)
         rng = np.random.default_rng(11)

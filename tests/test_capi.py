@@ -105,6 +105,7 @@ def test_comm_argument_checks_without_device(built_lib):
     if not torch.cuda.is_available():
         assert L.oxh_comm_create(uid, 0, 1, 0, ctypes.byref(h)) == _capi.OXH_ERR_NODEVICE
         assert not h.value
+        assert L.oxh_comm_check(0) == _capi.OXH_ERR_NODEVICE  # checked before anything is joined
 
 
 def test_header_compiles_standalone_as_c_and_cpp(tmp_path):
