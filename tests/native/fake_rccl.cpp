@@ -12,13 +12,14 @@
 // copied device-to-host into its own slot with a directory entry {kind, peer, seq, bytes} -- then a
 // barrier, then FETCH -- every buffer this rank receives is found in the owner's directory by the
 // same matching rule RCCL uses (collectives by issue order, send/recv by per-peer order), checked
-// for size and copied host-to-device on the op's stream -- then a barrier. Each entry counts its
+// for size and copied host-to-device on the op's stream (not waited for: it lands in stream order,
+// as RCCL's kernel would) -- then a barrier. Each entry counts its
 // readers; after the second barrier every rank checks that its own entries were read exactly as
 // often as the call pattern requires (an all-gather by every rank, a gather by the root, a send by
 // its peer). Any mismatch -- unmatched send, size disagreement, wrong root -- is ncclInvalidUsage
 // with a line on stderr, so the double is stricter than the real library about call patterns.
 // Every rank must enter every group (an empty one included) and every collective, as comm.cpp does.
-// Everything is synchronous; a barrier that waits longer than OXH_FAKE_RCCL_TIMEOUT_S (default 60 s)
+// Everything else is synchronous; a barrier that waits longer than OXH_FAKE_RCCL_TIMEOUT_S (default 60 s)
 // fails with ncclSystemError instead of hanging the test.
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
@@ -226,10 +227,12 @@ ncclResult_t run(ncclComm* c, std::vector<Op>& ops) {
                 ok = false;
                 break;
             }
+            // No wait for the copy to land: like RCCL's kernel, it completes on the op's stream, so a
+            // caller that reads the table without ordering after that stream reads stale bytes. A
+            // pageable-source copy returns once the source is staged, so the slot may be reused after.
             if (o.bytes)
                 ok = check_hip(hipMemcpyAsync((uint8_t*)o.recv + dst, c->data + q * c->h->slot_bytes + e->off, o.bytes,
-                                              hipMemcpyHostToDevice, o.st), "hipMemcpyAsync H2D") &&
-                     check_hip(hipStreamSynchronize(o.st), "hipStreamSynchronize");
+                                              hipMemcpyHostToDevice, o.st), "hipMemcpyAsync H2D");
             e->reads.fetch_add(1, std::memory_order_acq_rel);
             if (!ok) break;
         }
