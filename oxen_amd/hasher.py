@@ -480,7 +480,7 @@ def text_file_nodes(paths: Sequence[str], ctx: Optional[_capi.Context] = None):
     ctx = ctx or default_context()
     digests, sizes, status, meta = hash_files_text_128bit(paths, ctx)
     ok = [i for i, st in enumerate(status) if st == 0]
-    mh = hash_streams_128bit([metadata_json(meta[i]).encode("utf-8") for i in ok], ctx)
+    mh = hash_streams_128bit([text_metadata_json(meta[i]).encode("utf-8") for i in ok], ctx)
     comb = hash_streams_128bit([digests[i].to_bytes(16, "little") + m.to_bytes(16, "little") for i, m in zip(ok, mh)], ctx)
     res: list = [None] * len(paths)
     for j, i in enumerate(ok):
@@ -612,6 +612,28 @@ def _serde_json(v) -> str:
     raise TypeError(f"cannot serialise {type(v).__name__} as serde_json")
 
 
+def _no_floats(v) -> bool:
+    """True when nothing in v is a float: json.dumps then writes exactly serde_json's text."""
+    stack = [v]
+    while stack:
+        x = stack.pop()
+        t = type(x)
+        if t is dict:
+            stack.extend(x.values())
+        elif t is list or t is tuple:
+            stack.extend(x)
+        elif isinstance(x, float):
+            return False
+    return True
+
+
+def text_metadata_json(m) -> str:
+    """metadata_json of a MetadataText (model/metadata/metadata_text.rs: {"text": {num_lines, num_chars}},
+    both usize) as serde_json writes it -- the per-file string of a text add, built directly."""
+    t = m["text"]
+    return f'{{"text":{{"num_lines":{int(t["num_lines"])},"num_chars":{int(t["num_chars"])}}}}}'
+
+
 def metadata_json(oxen_metadata) -> str:
     """serde_json::to_string of the (untagged) GenericMetadata (model/metadata/generic_metadata.rs:8-17),
     or "null" for None (hasher.rs:95-100).
@@ -622,12 +644,14 @@ def metadata_json(oxen_metadata) -> str:
     An object with to_json() serialises itself."""
     if hasattr(oxen_metadata, "to_json"):
         return oxen_metadata.to_json()
-    if isinstance(oxen_metadata, dict) and len(oxen_metadata) == 1:
+    if type(oxen_metadata) is dict and len(oxen_metadata) == 1:
         (kind, body), = oxen_metadata.items()
         if kind in _F64_FIELDS and isinstance(body, dict):
             body = {k: (float(x) if k in _F64_FIELDS[kind] and isinstance(x, int) and not isinstance(x, bool) else x)
                     for k, x in body.items()}
             oxen_metadata = {kind: body}
+    if _no_floats(oxen_metadata):  # the common case (text, image, tabular metadata): the C encoder
+        return json.dumps(oxen_metadata, separators=(",", ":"), ensure_ascii=False)
     return _serde_json(oxen_metadata)
 
 

@@ -940,6 +940,66 @@ std::vector<bool> should_restore_batch(const std::vector<RestoreCheck>& files, b
 }
 }  // namespace core::restore
 
+namespace core::branches {
+std::vector<CheckoutOutcome> classify_checkout_batch(const std::vector<CheckoutCheck>& files, bool overwrite, oxh_ctx* ctx) {
+    ctx = ctx ? ctx : util::hasher::default_context();
+    const size_t n = files.size();
+    std::vector<CheckoutOutcome> out(n, CheckoutOutcome::Restore);
+    std::vector<size_t> need;
+    std::vector<uint64_t> meta_sizes;
+    for (size_t i = 0; i < n; ++i) {
+        const CheckoutCheck& f = files[i];
+        struct stat sb;
+        // full_path.exists() is fs::metadata(..).is_ok(): a failing stat reads as "not on disk"
+        if (stat(f.working_path.c_str(), &sb) != 0) {
+            if (f.from && f.from->hash == f.target.hash)
+                out[i] = CheckoutOutcome::KeepDeleted;  // branches.rs:664-667
+            else if (f.from && !overwrite)
+                out[i] = CheckoutOutcome::Conflict;     // :668-673
+            else
+                out[i] = CheckoutOutcome::Restore;      // :678-686
+            continue;
+        }
+        const uint64_t size = (uint64_t)sb.st_size;
+        if (f.target_mtime_matched && size == f.target.num_bytes) {
+            out[i] = CheckoutOutcome::Skip;  // :703-705
+            continue;
+        }
+        if (f.from && f.from_mtime_matched && size == f.from->num_bytes) {
+            out[i] = CheckoutOutcome::Restore;  // :709-723
+            continue;
+        }
+        need.push_back(i);
+        meta_sizes.push_back(size);
+    }
+    if (need.empty()) return out;
+    const size_t m = need.size();
+    std::vector<const char*> cp(m);
+    for (size_t j = 0; j < m; ++j) cp[j] = files[need[j]].working_path.c_str();
+    std::vector<uint64_t> dig(2 * m), sizes(m);
+    std::vector<int32_t> status(m), oserr(m);
+    check(oxh_hash_files_ex(ctx, cp.data(), meta_sizes.data(), m, dig.data(), sizes.data(), status.data(), oserr.data(),
+                            nullptr, nullptr),
+          "oxh_hash_files_ex");
+    for (size_t j = 0; j < m; ++j)  // get_hash_given_metadata(&full_path, &meta)? -- the first failure in order
+        if (status[j] != OXH_OK)
+            throw OxenError::basic_str(util::hasher::file_error_text(files[need[j]].working_path, status[j], oserr[j],
+                                                                     meta_sizes[j]),
+                                       status[j]);
+    for (size_t j = 0; j < m; ++j) {  // :726-756
+        const CheckoutCheck& f = files[need[j]];
+        const u128 h = to_u128(dig[2 * j], dig[2 * j + 1]);
+        if (h == f.target.hash)
+            out[need[j]] = CheckoutOutcome::Skip;
+        else if (f.from && h == f.from->hash)
+            out[need[j]] = CheckoutOutcome::Restore;
+        else
+            out[need[j]] = overwrite ? CheckoutOutcome::Restore : CheckoutOutcome::Conflict;
+    }
+    return out;
+}
+}  // namespace core::branches
+
 namespace multigpu {
 std::vector<uint8_t> DigestGather::unique_id() {
     std::vector<uint8_t> id(OXH_COMM_ID_BYTES);

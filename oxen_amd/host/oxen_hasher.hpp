@@ -360,6 +360,30 @@ struct RestoreCheck {
 std::vector<bool> should_restore_batch(const std::vector<RestoreCheck>& files, bool combined, oxh_ctx* ctx = nullptr);
 }  // namespace core::restore
 
+// core/v_latest/branches.rs:653-757: the File arm of checkout's target-tree walk, three-way.
+namespace core::branches {
+enum class CheckoutOutcome {
+    Skip,         // the working file already is the target's version
+    Restore,      // results.files_to_restore
+    Conflict,     // results.cannot_overwrite_entries (OnConflict::Abort)
+    KeepDeleted,  // an uncommitted deletion of content both trees hold: preserved
+};
+struct CheckoutCheck {
+    std::string working_path;
+    core::restore::NodeHashes target;                // the target FileNode: content hash, num_bytes
+    std::optional<core::restore::NodeHashes> from;   // the from tree's PartialNode (hash, size), if any
+    bool target_mtime_matched = false;  // repo.mtime_matches(disk mtime, the target's mtime)
+    bool from_mtime_matched = false;    // repo.mtime_matches(disk mtime, the PartialNode's last_modified)
+};
+// Every file of the walk, in its order: missing (from holds the target's hash -> KeepDeleted; a from
+// node -> Conflict, or Restore with overwrite; none -> Restore), the target / from mtime + size short
+// cuts, then every remaining file hashed in one pass (get_hash_given_metadata with the stat's size,
+// oxh_hash_files_ex) and compared with the target's and the from node's hash. The first file in order
+// whose stat or read fails throws OxenError, as the reference's `?` does.
+std::vector<CheckoutOutcome> classify_checkout_batch(const std::vector<CheckoutCheck>& files, bool overwrite,
+                                                     oxh_ctx* ctx = nullptr);
+}  // namespace core::branches
+
 // one process per GPU, the digest table gathered once over xGMI (oxh_comm_*).
 namespace multigpu {
 class DigestGather {

@@ -1,6 +1,7 @@
 """The restore / merge "may this working file be overwritten?" checks, batched over the C ABI
 (core/v_latest/index/restore.rs:231-297 `should_restore_partial_node`, :300-405 `should_restore_file`;
-called per file by merge.rs:742-829, 1304-1398 and checkout).
+called per file by merge.rs:742-829, 1304-1398 and checkout), and checkout's own three-way
+classification of the target tree's files (core/v_latest/branches.rs:653-757, `classify_checkout`).
 
 Per file the reference decides, in order:
   * the working file does not exist                               -> true (nothing to lose)
@@ -26,7 +27,7 @@ from typing import Optional, Sequence
 from . import _capi
 from .hasher import (TEXT, OxenError, file_error, hash_files_text_128bit,
                      hash_files_with_errors_128bit, hash_streams_128bit, metadata_json, rust_io_error_debug,
-                     rust_path_debug)
+                     rust_path_debug, text_metadata_json)
 
 
 @dataclass
@@ -91,7 +92,7 @@ def should_restore(paths: Sequence[str], targets: Sequence[NodeHashes], bases: S
             content[i] = (d[j], st[j], 0)
             meta_hash[i] = None
         ok = [j for j, i in enumerate(text) if st[j] == 0]
-        for j, h in zip(ok, hash_streams_128bit([metadata_json(m[j]).encode("utf-8") for j in ok], ctx)):
+        for j, h in zip(ok, hash_streams_128bit([text_metadata_json(m[j]).encode("utf-8") for j in ok], ctx)):
             meta_hash[text[j]] = h
     if combined:
         objs = [i for i in plain if meta[i] is not None and not isinstance(meta[i], (int, str))]
@@ -130,3 +131,74 @@ def should_restore(paths: Sequence[str], targets: Sequence[NodeHashes], bases: S
         else:
             out[i] = h == want
     return [bool(x) for x in out]
+
+
+# Outcomes of checkout's File arm (core/v_latest/branches.rs:653-757, r_restore_missing_or_modified_files)
+SKIP = "skip"                  # the working file already is the target's version: nothing to do
+RESTORE = "restore"            # goes to results.files_to_restore
+CONFLICT = "conflict"          # goes to results.cannot_overwrite_entries (OnConflict::Abort)
+KEEP_DELETED = "keep_deleted"  # an uncommitted deletion of a file both trees hold unchanged: preserved
+
+
+def classify_checkout(paths: Sequence[str], targets: Sequence[NodeHashes], froms: Sequence[Optional[NodeHashes]],
+                      target_mtime_matched: Sequence[bool], from_mtime_matched: Sequence[bool],
+                      overwrite: bool = False, ctx: Optional[_capi.Context] = None) -> list[str]:
+    """The File arm of checkout's target-tree walk (branches.rs:653-757) for every file, in the walk's
+    order. targets[i]: the target FileNode's content hash and num_bytes (node.hash is the content hash,
+    merkle_tree_node.rs:147-159); froms[i]: the from tree's PartialNode at the same path (hash, size), or
+    None for a path new in the target. The two mtime verdicts are the repo's tolerance rule applied by
+    the caller (repo.mtime_matches of the disk mtime against the target's / the PartialNode's), as for
+    should_restore. overwrite = OnConflict::Overwrite (`oxen merge --abort`). Per file the reference:
+      * not on disk: from has the target's hash -> KEEP_DELETED; a from node otherwise -> CONFLICT
+        (abort) or RESTORE (overwrite); no from node -> RESTORE (new in the target);
+      * util::fs::metadata(..)? ; target mtime + size match -> SKIP; from mtime + size match -> RESTORE;
+      * get_hash_given_metadata(..)? : == target -> SKIP; == from -> RESTORE; else CONFLICT / RESTORE.
+    Every file that reaches the hash is read once, all in one GPU pass; errors raise as the reference's
+    `?` does -- the first failing file in order, its metadata before its read."""
+    n = len(paths)
+    if not (len(targets) == len(froms) == len(target_mtime_matched) == len(from_mtime_matched) == n):
+        raise _capi.OxenError("classify_checkout: argument lengths differ", _capi.OXH_ERR_INVALID)
+    out: list[Optional[str]] = [None] * n
+    need: list[int] = []
+    sizes: dict[int, int] = {}
+    stat_error: Optional[OxenError] = None
+    for i, p in enumerate(paths):
+        t, f = targets[i], froms[i]
+        if not os.path.exists(p):  # full_path.exists()
+            if f is not None and f.hash == t.hash:
+                out[i] = KEEP_DELETED
+            elif f is not None and not overwrite:
+                out[i] = CONFLICT
+            else:
+                out[i] = RESTORE
+            continue
+        try:
+            size = os.stat(p).st_size  # util::fs::metadata(&full_path)? (only a race after exists())
+        except OSError as e:
+            stat_error = OxenError(f"Could not get file metadata: {rust_path_debug(p)} error "
+                                   f"{rust_io_error_debug(e.errno or 0)}", _capi.OXH_ERR_IO)
+            break
+        if target_mtime_matched[i] and size == t.num_bytes:
+            out[i] = SKIP
+        elif f is not None and from_mtime_matched[i] and size == f.num_bytes:
+            out[i] = RESTORE
+        else:
+            need.append(i)
+            sizes[i] = size
+    if need:
+        digests, _, status, oserr = hash_files_with_errors_128bit([paths[i] for i in need],
+                                                                  meta_sizes=[sizes[i] for i in need], ctx=ctx)
+        for j, i in enumerate(need):  # in walk order: the first failing file is the error
+            if status[j] != 0:
+                raise file_error(paths[i], status[j], oserr[j], sizes[i])
+        for j, i in enumerate(need):
+            h, t, f = digests[j], targets[i], froms[i]
+            if h == t.hash:
+                out[i] = SKIP
+            elif f is not None and h == f.hash:
+                out[i] = RESTORE
+            else:
+                out[i] = RESTORE if overwrite else CONFLICT
+    if stat_error is not None:  # every file before it classified without an error
+        raise stat_error
+    return [str(x) for x in out]

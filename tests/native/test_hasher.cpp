@@ -625,6 +625,65 @@ static void restore_checks() {
     if (system(rm.c_str()) != 0) fprintf(stderr, "could not remove %s\n", dir);
 }
 
+// core::branches::classify_checkout_batch (branches.rs:653-757) against the File arm's rules spelled out here
+static void checkout_checks() {
+    namespace br = liboxen::core::branches;
+    namespace rs = liboxen::core::restore;
+    using O = br::CheckoutOutcome;
+    char tmpl[] = "/tmp/oxh_checkout_XXXXXX";
+    const char* dir = mkdtemp(tmpl);
+    CHECK(dir != nullptr);
+    if (!dir) return;
+    auto put = [&](const std::string& name, const std::string& data) {
+        const std::string p = std::string(dir) + "/" + name;
+        if (FILE* f = fopen(p.c_str(), "wb")) {
+            fwrite(data.data(), 1, data.size(), f);
+            fclose(f);
+        }
+        return p;
+    };
+    auto node = [](const std::string& d) {
+        rs::NodeHashes h;
+        h.hash = hasher::hash_buffer_128bit(d);
+        h.num_bytes = d.size();
+        return h;
+    };
+    const std::string tgt = "target version\n", frm = "from version\n", other = "edited elsewhere\n";
+    for (bool overwrite : {false, true}) {
+        std::vector<br::CheckoutCheck> v;
+        std::vector<O> want;
+        auto add = [&](const std::string& path, const std::string* from, bool t_ok, bool f_ok, O expect) {
+            br::CheckoutCheck c;
+            c.working_path = path;
+            c.target = node(tgt);
+            if (from) c.from = node(*from);
+            c.target_mtime_matched = t_ok;
+            c.from_mtime_matched = f_ok;
+            v.push_back(c);
+            want.push_back(expect);
+        };
+        const std::string missing = std::string(dir) + "/missing";
+        const std::string p_t = put("t.txt", tgt), p_f = put("f.txt", frm), p_o = put("o.txt", other);
+        add(missing, nullptr, false, false, O::Restore);                        // new in the target
+        add(missing, &tgt, false, false, O::KeepDeleted);                      // deleted, unchanged in both
+        add(missing, &frm, false, false, overwrite ? O::Restore : O::Conflict);  // deleted after a change
+        add(p_t, &frm, false, false, O::Skip);                                 // already the target
+        add(p_f, &frm, false, false, O::Restore);                              // unchanged since from
+        add(p_o, &frm, false, false, overwrite ? O::Restore : O::Conflict);    // diverged from both
+        add(p_o, nullptr, false, false, overwrite ? O::Restore : O::Conflict);
+        add(put("same_size_t.txt", std::string(tgt.size(), 'z')), &frm, true, false, O::Skip);  // short cuts: no read
+        add(put("same_size_f.txt", std::string(frm.size(), 'z')), &frm, false, true, O::Restore);
+        add(p_o + "/x", &frm, false, false, overwrite ? O::Restore : O::Conflict);  // ENOTDIR: not on disk
+        CHECK(br::classify_checkout_batch(v, overwrite) == want);
+    }
+    br::CheckoutCheck d;
+    d.working_path = dir;  // a directory: the read fails (EISDIR) and the call throws
+    d.target = node(tgt);
+    CHECK(throws_oxen([&] { br::classify_checkout_batch({d}, false); }, "Could not read file for hashing"));
+    const std::string rm = std::string("rm -rf ") + dir;
+    if (system(rm.c_str()) != 0) fprintf(stderr, "could not remove %s\n", dir);
+}
+
 // liboxen::dedup::host_entry_pays_off: INTEGRATION.md §2's routing rule (the same table as dedup.py)
 static void routing_rule_checks() {
     namespace dd = liboxen::dedup;
@@ -649,6 +708,7 @@ int main(int argc, char** argv) {
         modified_check(golden);
         dedup_chunks(golden);
         restore_checks();
+        checkout_checks();
         routing_rule_checks();
         char tmpl[] = "/tmp/oxh_native_XXXXXX";
         const char* scratch = mkdtemp(tmpl);

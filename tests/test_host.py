@@ -93,6 +93,11 @@ def test_metadata_json_matches_serde(golden):
     r0 = golden("text_repo.json")["files"][0]
     assert metadata_json({"text": {"num_lines": 1, "num_chars": 14}}) == r0["metadata_json"]
     assert metadata_json(None) == "null"
+    from oxen_amd.hasher import text_metadata_json
+
+    for lines, chars in ((1, 14), (0, 0), (123456, 7890123)):
+        md = {"text": {"num_lines": lines, "num_chars": chars}}
+        assert text_metadata_json(md) == metadata_json(md)
 
 
 # serde_json's f64 text (ryu's format64), hand-derived -- parity unpinned: no reference fixture holds

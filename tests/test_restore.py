@@ -167,3 +167,115 @@ def test_should_restore_first_failing_file_wins(cuda, tmp_path, monkeypatch):
         restore.should_restore([str(d), str(f)], [n, n], [None, None], [False, False])
     with pytest.raises(_capi.OxenError, match="Could not get file metadata"):
         restore.should_restore([str(f), str(d)], [n, n], [None, None], [False, False])
+
+
+# ---------------------------------------------------------------- checkout (branches.rs:653-757)
+def _checkout_reference(oracle_lib, path, target, frm, t_ok, f_ok, overwrite):
+    """branches.rs:653-757 (the File arm of r_restore_missing_or_modified_files) for one file, restated."""
+    from oxen_amd import restore as R
+
+    if not os.path.exists(path):
+        if frm is not None:
+            if frm.hash == target.hash:
+                return R.KEEP_DELETED
+            if not overwrite:
+                return R.CONFLICT
+        return R.RESTORE
+    size = os.stat(path).st_size
+    if t_ok and size == target.num_bytes:
+        return R.SKIP
+    if frm is not None and f_ok and size == frm.num_bytes:
+        return R.RESTORE
+    h = oracle_lib.xxh3_128_int(open(path, "rb").read())
+    if h == target.hash:
+        return R.SKIP
+    if frm is not None and h == frm.hash:
+        return R.RESTORE
+    return R.RESTORE if overwrite else R.CONFLICT
+
+
+def _checkout_case(oracle_lib, tmp_path):
+    from oxen_amd.restore import NodeHashes
+
+    rng = np.random.default_rng(17)
+    contents = [b"alpha\n", b"", b"y" * 70_000, bytes(rng.integers(0, 256, 5000, dtype=np.uint8))]
+
+    def node(data):
+        return NodeHashes(hash=oracle_lib.xxh3_128_int(data), num_bytes=len(data))
+
+    paths, targets, froms, t_ok, f_ok = [], [], [], [], []
+    k = 0
+    for ci, base in enumerate(contents):
+        tgt, frm_data, other = base + b"target\n", base + b"from!\n", base + b"other edit\n"
+        for working in ("target", "from", "other", "missing", "same"):
+            for has_from in (False, True):
+                for tm, fm in ((False, False), (True, False), (False, True)):
+                    p = tmp_path / f"c{k}.bin"
+                    k += 1
+                    data = {"target": tgt, "from": frm_data, "other": other, "same": None, "missing": None}[working]
+                    if data is not None:
+                        p.write_bytes(data)
+                    paths.append(str(p))
+                    targets.append(node(tgt))
+                    # "same": deleted, and the from tree holds the target's content (the deletion is kept)
+                    froms.append((node(tgt) if working == "same" else node(frm_data)) if has_from else None)
+                    t_ok.append(tm)
+                    f_ok.append(fm)
+    return paths, targets, froms, t_ok, f_ok
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("overwrite", [False, True], ids=["abort", "overwrite"])
+def test_classify_checkout_matches_the_reference(cuda, oracle_lib, tmp_path, overwrite):
+    """Every branch of checkout's File arm: missing (new in the target, deleted with the from tree's own
+    content, deleted after a change), the target's and the from node's mtime + size short cuts (taken
+    even when the bytes differ), the hash equal to the target's, to the from node's, or neither -- under
+    OnConflict::Abort and ::Overwrite; all hashes of one call in one GPU pass."""
+    from oxen_amd import restore
+
+    paths, targets, froms, t_ok, f_ok = _checkout_case(oracle_lib, tmp_path)
+    got = restore.classify_checkout(paths, targets, froms, t_ok, f_ok, overwrite=overwrite)
+    want = [_checkout_reference(oracle_lib, p, t, f, a, b, overwrite)
+            for p, t, f, a, b in zip(paths, targets, froms, t_ok, f_ok)]
+    assert got == want
+    assert set(want) == ({restore.SKIP, restore.RESTORE, restore.KEEP_DELETED} |
+                         (set() if overwrite else {restore.CONFLICT}))
+
+
+@pytest.mark.gpu
+def test_classify_checkout_first_failing_file_wins(cuda, tmp_path):
+    """A working path that cannot be read (a directory: EISDIR) fails the call with hasher.rs's text,
+    the first failing file in walk order; the short cuts before it read nothing."""
+    from oxen_amd import _capi, restore
+    from oxen_amd.restore import NodeHashes
+
+    d = tmp_path / "adir"
+    d.mkdir()
+    f = tmp_path / "f.txt"
+    f.write_bytes(b"hello")
+    n = NodeHashes(hash=1, num_bytes=5)
+    assert restore.classify_checkout([str(f)], [n], [None], [True], [False]) == [restore.SKIP]
+    with pytest.raises(_capi.OxenError, match="Could not read file for hashing"):
+        restore.classify_checkout([str(f), str(d)], [n, NodeHashes(hash=2, num_bytes=1)], [None, None],
+                                  [False, False], [False, False])
+
+
+def test_classify_checkout_short_cuts_need_no_device(tmp_path):
+    """Missing files and the two mtime + size short cuts decide without reading anything (no GPU call:
+    this runs on the CPU); argument lengths are checked first."""
+    from oxen_amd import _capi, restore
+    from oxen_amd.restore import NodeHashes
+
+    f = tmp_path / "five.txt"
+    f.write_bytes(b"12345")
+    t = NodeHashes(hash=1, num_bytes=5)
+    same = NodeHashes(hash=1, num_bytes=9)
+    diff = NodeHashes(hash=2, num_bytes=5)
+    missing = str(tmp_path / "gone")
+    got = restore.classify_checkout([missing, missing, missing, str(f), str(f)], [t] * 5,
+                                    [None, same, diff, None, diff], [False, False, False, True, False],
+                                    [False, False, False, False, True])
+    assert got == [restore.RESTORE, restore.KEEP_DELETED, restore.CONFLICT, restore.SKIP, restore.RESTORE]
+    assert restore.classify_checkout([missing], [t], [diff], [False], [False], overwrite=True) == [restore.RESTORE]
+    with pytest.raises(_capi.OxenError, match="lengths differ"):
+        restore.classify_checkout([missing], [t], [None, None], [False], [False])
