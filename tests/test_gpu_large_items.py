@@ -12,7 +12,8 @@ GIB = 1 << 30
 @pytest.mark.parametrize("lens", [
     [4097, GIB + 4097, 3],           # 1 GiB + 4 097 B starting at byte 4 097 (not dword-aligned)
     [13, 2 * GIB + 12_345, 1000],    # above 2 GiB (two re-bases), start at byte 13
-], ids=["1GiB+4097_misaligned", "2GiB+12345_misaligned"])
+    [7, 4 * GIB + 777, 5],           # above 2^32 bytes (four re-bases; any 32-bit offset wraps here)
+], ids=["1GiB+4097_misaligned", "2GiB+12345_misaligned", "4GiB+777_misaligned"])
 def test_k1_items_over_a_descriptor_window(cuda, oracle_lib, lens):
     import torch
 
@@ -34,14 +35,15 @@ def test_k1_items_over_a_descriptor_window(cuda, oracle_lib, lens):
 def test_k1l_default_pieces_device(cuda, oracle_lib, monkeypatch):
     """K1L as it ships -- OXH_BIG_PIECE_MIB unset (1 GiB pieces) -- over buffers
     larger than one piece: 2 GiB + 4 097 B at a misaligned start (two full pieces and a last piece of
-    4 097 B) and 1 GiB - 1 B (one piece), through oxh_xxh3_128_large_batch_device."""
+    4 097 B), 1 GiB - 1 B (one piece) and 4 GiB + 333 B (above 2^32), through
+    oxh_xxh3_128_large_batch_device."""
     import torch
 
     from oxen_amd.device import fill_splitmix, large_digests_device
 
     monkeypatch.delenv("OXH_BIG_PIECE_MIB", raising=False)
-    sizes = [2 * GIB + 4097, GIB - 1]
-    starts = [5, 0]
+    sizes = [2 * GIB + 4097, GIB - 1, 4 * GIB + 333]  # the last one above 2^32 bytes, five pieces
+    starts = [5, 0, 3]
     bufs, views = [], []
     for i, (n, s) in enumerate(zip(sizes, starts)):
         b = torch.empty(n + 64, dtype=torch.uint8, device=cuda)
