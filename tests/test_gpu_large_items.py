@@ -129,3 +129,38 @@ def test_large_item_buffer_allocations_stay_rare(cuda, oracle_lib, tmp_path, mon
         assert c2["big_allocs"] <= 2 and c2["big_bytes"] >= c["big_bytes"], (c, c2)
         got, _, _ = hasher.hash_files_128bit(paths[:3], ctx=ctx)
         assert got == want[:3] and ctx.counters()["big_allocs"] == c2["big_allocs"]
+
+
+def test_file_paths_above_4_gib(cuda, oracle_lib, tmp_path, monkeypatch):
+    """A file above 2^32 bytes through the file entries as they ship: oxh_hash_files (the large-file
+    pipeline, five 1 GiB pieces) and oxh_chunk_digests_files (the host chunk pipeline, 1 MiB chunks, the
+    piece boundaries and the 2^32 offset inside the file) -- sparse, with written regions at the start,
+    around 2^32 and at the end; whole-file digest and every chunk digest against the oracle."""
+    import os
+
+    from oxen_amd import dedup, hasher
+    from oxen_amd.workloads import splitmix_bytes
+
+    monkeypatch.delenv("OXH_BIG_PIECE_MIB", raising=False)
+    monkeypatch.delenv("OXH_CDC_PIECE_MIB", raising=False)
+    size = 4 * GIB + 4097
+    p = tmp_path / "huge.bin"
+    with open(p, "wb") as fh:
+        fh.truncate(size)
+        for off in (0, 4 * GIB - 2000, 4 * GIB + 77, size - 3000):
+            fh.seek(off)
+            fh.write(splitmix_bytes(off, 1, 4096).tobytes()[: size - off])
+    out, sizes, status = oracle_lib.hash_files([str(p)], threads=8)
+    want = (int(out[0, 1]) << 64) | int(out[0, 0])
+    assert int(status[0]) == 0 and int(sizes[0]) == size
+    d, sz, st = hasher.hash_files_128bit([str(p)])
+    assert st == [0] and sz == [size] and d == [want]
+    chunk = 1 << 20
+    tab = dedup.chunk_digests_files([str(p)], chunk)
+    assert list(tab.status) == [0] and int(tab.first[1]) == (size + chunk - 1) // chunk
+    data = np.memmap(str(p), dtype=np.uint8, mode="r")
+    offs = np.arange(0, size, chunk, dtype=np.uint64)
+    lens = np.minimum(np.uint64(chunk), np.uint64(size) - offs)
+    assert np.array_equal(tab.file(0), oracle_lib.batch(data, offs, lens, 8))
+    del data
+    os.remove(p)
