@@ -345,6 +345,36 @@ def test_fastcdc_gib_files_fully_checked(cuda, oracle_lib, avg, cdc_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("avg", [8192, 65536])
+def test_fastcdc_item_above_4_gib_fully_checked(cuda, oracle_lib, avg, cdc_path):
+    """One device-resident item of 4 GiB + 12 345 B (positions inside the item above 2^32, as C5's
+    8 GiB files have them; the host entries never hand the device more than a piece) and a small item
+    after it in the arena: every boundary and every digest of both against the C oracle."""
+    import torch
+
+    from oxen_amd.device import fastcdc_device, fill_splitmix, to_numpy_u64
+
+    sizes = [(4 << 30) + 12_345, 77_777]
+    offs = np.array([0, ((sizes[0] + 4095) // 4096) * 4096], dtype=np.uint64)
+    arena = torch.empty(int(offs[1]) + sizes[1] + 4096, dtype=torch.uint8, device=cuda)
+    fill_splitmix(arena, 4343)
+    lens = np.array(sizes, dtype=np.uint64)
+    c_off, c_len, dig, first = fastcdc_device(arena, offs, lens, 4096, avg, 2 * avg)
+    got_off, got_len = to_numpy_u64(c_off), to_numpy_u64(c_len)
+    got_dig = to_numpy_u64(dig).reshape(-1, 2)
+    for i in range(2):
+        host = arena[int(offs[i]):int(offs[i]) + sizes[i]].cpu().numpy()
+        want = F.chunks(host, 4096, avg, 2 * avg)
+        a, b = int(first[i]), int(first[i + 1])
+        assert b - a == len(want), (i, b - a, len(want))
+        assert np.array_equal(got_off[a:b] - offs[i], want[:, 0]) and np.array_equal(got_len[a:b], want[:, 1]), i
+        assert np.array_equal(oracle_lib.batch(host, want[:, 0], want[:, 1], threads=8), got_dig[a:b]), i
+        del host
+    del arena, c_off, c_len, dig
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
 def test_fastcdc_walk_truncated_window_cuts(cuda, oracle_lib, monkeypatch):
     """The walk (W) never tests a chunk's first 47 hashed positions, where cut_gear's hash has not yet
     seen a full 48-byte window; X re-walks exactly the chunks where one of them matches. With
