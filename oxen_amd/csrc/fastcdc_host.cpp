@@ -252,7 +252,10 @@ struct CdcSource {
 };
 
 // fs::read(input_file) (fastcdchunker.rs:75): File::open, then the whole file. A directory opens and
-// fails its read with EISDIR, as read_to_end does; the size is the open file's fstat.
+// fails its read with EISDIR, as read_to_end does; the size is the open file's fstat. Files open
+// with O_NONBLOCK, so a FIFO cannot park a pool thread in open(2) waiting for a writer (where fs::read
+// would wait, and then read whatever arrives); like the file engine, anything that is not a regular
+// file or a directory is refused as unreadable (EINVAL) -- the chunk pipeline preads.
 struct FileSrc final : CdcSource {
     const char* const* paths;
     std::vector<int> fds;
@@ -263,7 +266,7 @@ struct FileSrc final : CdcSource {
     }
     int open(uint64_t i, uint64_t& size, int& oserr) override {
         size = 0;
-        const int fd = ::open(paths[i], O_RDONLY | O_CLOEXEC);
+        const int fd = ::open(paths[i], O_RDONLY | O_CLOEXEC | O_NONBLOCK);
         if (fd < 0) {
             oserr = errno;
             return OXH_ERR_OPEN;
@@ -274,8 +277,8 @@ struct FileSrc final : CdcSource {
             ::close(fd);
             return OXH_ERR_IO;
         }
-        if (S_ISDIR(sb.st_mode)) {
-            oserr = EISDIR;
+        if (!S_ISREG(sb.st_mode)) {
+            oserr = S_ISDIR(sb.st_mode) ? EISDIR : EINVAL;
             ::close(fd);
             return OXH_ERR_IO;
         }

@@ -802,3 +802,35 @@ def test_host_chunk_entries_low_fd_limit(cuda, oracle_lib, tmp_path):
         resource.setrlimit(resource.RLIMIT_NOFILE, (soft, hard))
         for c in [one] + ctxs:
             c.close()
+
+
+@pytest.mark.gpu
+def test_file_entries_refuse_a_fifo_without_blocking(cuda, oracle_lib, tmp_path):
+    """A FIFO among the paths (no writer): open(2) without O_NONBLOCK would park a reader in the call
+    forever (fs::read would wait there too). The host chunk entries and the file engine open it
+    non-blocking and refuse it as unreadable -- OXH_ERR_IO with EINVAL -- while the files around it are
+    chunked / hashed exactly."""
+    import errno
+    import os
+
+    from oxen_amd import _capi, dedup, hasher
+
+    rng = np.random.default_rng(99)
+    datas = [rng.integers(0, 256, 70_000, dtype=np.uint8), None, rng.integers(0, 256, 5_000, dtype=np.uint8)]
+    paths = []
+    for i, d in enumerate(datas):
+        p = tmp_path / f"p{i}"
+        if d is None:
+            os.mkfifo(p)
+        else:
+            p.write_bytes(d.tobytes())
+        paths.append(str(p))
+    tab = dedup.fastcdc_files(paths, 4096, 8192, 16384)
+    assert list(tab.status) == [0, _capi.OXH_ERR_IO, 0] and int(tab.os_error[1]) == errno.EINVAL
+    _check_table(oracle_lib, tab, datas, 4096, 8192, 16384)
+    fix = dedup.chunk_digests_files(paths, 4096)
+    assert list(fix.status) == [0, _capi.OXH_ERR_IO, 0] and int(fix.os_error[1]) == errno.EINVAL
+    assert len(fix.file(1)) == 0
+    d, _, st, oe = hasher.hash_files_with_errors_128bit(paths)
+    assert st == [0, _capi.OXH_ERR_IO, 0] and oe[1] == errno.EINVAL
+    assert d[0] == oracle_lib.xxh3_128_int(datas[0].tobytes()) and d[2] == oracle_lib.xxh3_128_int(datas[2].tobytes())

@@ -2,6 +2,7 @@
 
 Bit-exact digests are the bar for every case: this is integer/byte work.
 """
+import ctypes
 import os
 
 import numpy as np
@@ -1116,3 +1117,45 @@ def test_engine_back_to_back_small_requests(oracle_lib, tmp_path, cuda):
         for _ in range(300):
             d, _, st = hasher.hash_files_128bit(paths, c)
             assert d == want
+
+
+def test_staging_slot_boundaries(oracle_lib, tmp_path, cuda):
+    """Items at the staging slot's edges on every host entry: exactly a slot (staged), a slot + 1 (the
+    oversize path), a slot - 1, and runs whose 256-B placement overflows the slot by one alignment step
+    (the batch must close there) -- oxh_hash_buffers, oxh_hash_streams (span and per-item forms) and
+    oxh_hash_files, all against the oracle."""
+    from oxen_amd import _capi, hasher
+    from oxen_amd.workloads import splitmix_bytes
+
+    S = 1 << 20
+    sizes = [S, S + 1, S - 1, 0, 241, S - 300, 300, 1, S // 2 + 1, S // 2, 240, S - 256, 256, 255, S]
+    bufs = [splitmix_bytes(900 + i, 0, s).tobytes() for i, s in enumerate(sizes)]
+    want = [oracle_lib.xxh3_128_int(b) for b in bufs]
+    paths = []
+    for i, b in enumerate(bufs):
+        p = tmp_path / f"edge{i}"
+        p.write_bytes(b)
+        paths.append(str(p))
+    arena = b"".join(bufs)
+    offs = np.cumsum([0] + sizes[:-1]).astype(np.uint64)
+    with _capi.Context(0, staging_bytes=S) as c:
+        assert hasher.hash_buffers_128bit(bufs, c) == want
+        assert hasher.hash_streams_128bit(bufs, c) == want  # forward arena: the span form
+        # a scattered arena (items out of order) takes the per-item form
+        order = list(range(len(bufs)))[::-1]
+        scattered = b"".join(bufs[i] for i in order)
+        s_offs = np.zeros(len(bufs), dtype=np.uint64)
+        pos = 0
+        for i in order:
+            s_offs[i] = pos
+            pos += sizes[i]
+        out = np.zeros((len(bufs), 2), dtype=np.uint64)
+        lens = np.array(sizes, dtype=np.uint64)
+        src = np.frombuffer(scattered, dtype=np.uint8)
+        _capi.check(_capi.lib().oxh_hash_streams(c.handle, ctypes.c_void_p(src.ctypes.data),
+                                                 s_offs.ctypes.data_as(_capi._u64p), lens.ctypes.data_as(_capi._u64p),
+                                                 len(bufs), out.ctypes.data_as(_capi._u64p)), "oxh_hash_streams")
+        assert [(int(hi) << 64) | int(lo) for lo, hi in out] == want
+        d, got_sizes, st = hasher.hash_files_128bit(paths, c)
+        assert st == [0] * len(paths) and d == want and got_sizes == sizes
+    assert len(arena) == int(offs[-1]) + sizes[-1]
