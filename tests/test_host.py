@@ -114,7 +114,10 @@ SERDE_F64 = [(12.5, "12.5"), (12.0, "12.0"), (1e-5, "0.00001"), (1e-6, "1e-6"), 
              (1e15, "1000000000000000.0"), (1.5e16, "1.5e16"), (1.25e-7, "1.25e-7"), (0.1, "0.1"), (0.0, "0.0"),
              (-0.0, "-0.0"), (-3.75, "-3.75"), (5e-324, "5e-324"), (1.7976931348623157e308, "1.7976931348623157e308"),
              (9007199254740992.0, "9007199254740992.0"), (float("nan"), "null"), (float("inf"), "null"),
-             (float("-inf"), "null")]
+             (float("-inf"), "null"),
+             # serde_json's own `test_write_f64` cases (tests/test.rs of the crate, not vendored here)
+             (3.0, "3.0"), (3.1, "3.1"), (-1.5, "-1.5"), (0.5, "0.5"),
+             (-1.7976931348623157e308, "-1.7976931348623157e308"), (2.220446049250313e-16, "2.220446049250313e-16")]
 
 
 @pytest.mark.parametrize("x,want", SERDE_F64, ids=[w if w != "null" else repr(x) for x, w in SERDE_F64])
