@@ -19,6 +19,7 @@ import json
 import os
 import subprocess
 import sys
+import time
 
 import numpy as np
 import pytest
@@ -82,9 +83,10 @@ def test_abi_gather_multi_rank(cuda, oracle_lib, tmp_path, world, variant):
             procs.append(subprocess.Popen([sys.executable, "-u", WORKER, str(r), str(world), tmp], env=env,
                                           stdout=log, stderr=subprocess.STDOUT))
         codes = []
+        deadline = time.monotonic() + 150  # one deadline for the whole job, not one per rank
         for p in procs:
             try:
-                codes.append(p.wait(timeout=150))
+                codes.append(p.wait(timeout=max(1.0, deadline - time.monotonic())))
             except subprocess.TimeoutExpired:
                 codes.append("timeout")
     finally:
