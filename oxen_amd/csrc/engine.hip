@@ -690,6 +690,7 @@ void run_stream(oxh_ctx* c) {
 
 // The context's engine thread: one run per burst of requests.
 void engine_main(oxh_ctx* c) {
+    oxh::runtime_thread_timer_slack();  // pool.hpp: the engine's 20 us polls are not stretched to 70
     std::unique_lock<std::mutex> lk(c->qmu);
     for (;;) {
         c->qcv.wait(lk, [&] { return c->stop || !c->queue.empty(); });

@@ -3,6 +3,7 @@
 #include <dirent.h>
 #include <sched.h>
 #include <stdlib.h>
+#include <sys/prctl.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -39,6 +40,20 @@ inline void make_fd_table_private() {
         closedir(d);
         for (int fd : fds) close(fd);
     }
+}
+
+// The file engine's thread polls its slots' events in 20 us timed waits while a slot is in flight;
+// Linux stretches every such wait by the thread's timer slack, 50 us by default, so a one-file request
+// paid 50-70 us oversleeps end to end (tools/latency_probe.py). The engine thread runs with a slack of
+// OXH_TIMER_SLACK_NS (default 1000 ns; 0 keeps the kernel's default). The pools' threads (readers that
+// wait 2-5 us for a slot, copiers) and callers' threads keep theirs: tighter reader waits would spin
+// the 16 readers against each other on a CPU-bound walk.
+inline void runtime_thread_timer_slack() {
+    static const long ns = [] {
+        const char* e = getenv("OXH_TIMER_SLACK_NS");
+        return e ? atol(e) : 1000L;
+    }();
+    if (ns > 0) (void)prctl(PR_SET_TIMERSLACK, (unsigned long)ns, 0, 0, 0);
 }
 
 class Pool {

@@ -49,6 +49,13 @@ int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_
 // Wait for slot s's digests. Polls (a slot is at most a few hundred MiB: milliseconds of work) and,
 // after OXH_WAIT_LIMIT_S seconds (default 60), reports which stage never finished instead of
 // blocking forever.
+// OXH_SPIN_US: how long a caller waiting on a staged batch spins before it sleeps (default 200; 0 =
+// sleep after 64 polls, the r02-r05 form)
+double spin_us() {
+    static const double v = getenv("OXH_SPIN_US") ? atof(getenv("OXH_SPIN_US")) : 200.0;
+    return v;
+}
+
 int wait_slot(oxh_ctx* c, int s, const Pending& p) {
     static const double limit = getenv("OXH_WAIT_LIMIT_S") ? atof(getenv("OXH_WAIT_LIMIT_S")) : 60.0;
     const auto t0 = std::chrono::steady_clock::now();
@@ -56,7 +63,12 @@ int wait_slot(oxh_ctx* c, int s, const Pending& p) {
         const hipError_t q = hipEventQuery(c->ev_done[s]);
         if (q == hipSuccess) return OXH_OK;
         if (q != hipErrorNotReady) return fail(OXH_ERR_HIP, std::string("slot event: ") + hipGetErrorString(q));
-        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        // a small batch is back within tens of us: spin (yielding) for the first spin_us(), then sleep
+        // in 20 us steps (a caller's own thread keeps its timer slack, so a sleep costs ~70 us)
+        if (spin > 64 && std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e6 > spin_us())
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+        else
+            std::this_thread::yield();
         if ((spin & 1023) == 0 &&
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
             const uint64_t M = c->max_items;
