@@ -159,11 +159,17 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
             off += hlen[j];
         }
         STEP("fill s=%d items=%zu", s, batch.size());
-        const int ntasks = (int)std::min<size_t>(batch.size(), (size_t)c->pool->size() * 4);
-        c->pool->parallel_for(ntasks, [&](int t) {
+        // a small batch is copied on this thread: handing 1 MiB or less to the pool costs more in
+        // wake-ups than the copy (tools/latency_probe.py, one 4 KiB buffer)
+        const int ntasks = off <= (1u << 20) ? 1 : (int)std::min<size_t>(batch.size(), (size_t)c->pool->size() * 4);
+        auto fill = [&](int t) {
             for (size_t j = (size_t)t; j < batch.size(); j += (size_t)ntasks)
                 if (hlen[j]) memcpy(c->h_stage[s] + hoff[j], src(batch[j]), hlen[j]);
-        });
+        };
+        if (ntasks == 1)
+            fill(0);
+        else
+            c->pool->parallel_for(ntasks, fill);
         const double t2 = Trace::now();
         tr.fill += t2 - t1;
         if (int rc = submit_slot(c, s, off, batch.size(), short_only_lane && all_short,
