@@ -49,6 +49,8 @@ COMMIT_CLI_SRC = os.path.join(ROOT, "tests", "native", "commit_tree_cli.cpp")
 COMMIT_CLI = os.path.join(ROOT, "tests", "native", "commit_tree_cli")
 FAKE_HELPER_SRC = os.path.join(ROOT, "tests", "native", "fake_pool_helper.cpp")
 FAKE_HELPER = os.path.join(ROOT, "tests", "native", "fake_pool_helper")  # tests only: the pool without a GPU
+C_CONSUMER_SRC = os.path.join(ROOT, "tests", "native", "abi_c_consumer.c")
+C_CONSUMER = os.path.join(ROOT, "tests", "native", "abi_c_consumer")  # tests only: a plain C99 caller of the ABI
 FAKE_RCCL_SRC = os.path.join(ROOT, "tests", "native", "fake_rccl.cpp")
 # tests only: an "RCCL" for N processes on one GPU (OXH_RCCL_LIB), with and without ncclGather
 FAKE_RCCL = os.path.join(ROOT, "tests", "native", "libfake_rccl.so")
@@ -77,6 +79,9 @@ def build_host(force: bool = False, verbose: bool = False) -> str:
           f"-L{HERE}", "-l:liboxen_hasher.so", "-l:liboxen_hash.so", "-Wl,-rpath,$ORIGIN/../../oxen_amd"]),
         (FAKE_HELPER, [FAKE_HELPER_SRC, os.path.join(CSRC, "reader_pool.hpp")],
          ["g++", "-std=c++17", "-O2", "-Wall", "-o", FAKE_HELPER + ".tmp", FAKE_HELPER_SRC]),
+        (C_CONSUMER, [C_CONSUMER_SRC, hdr, LIB],
+         ["gcc", "-std=c99", "-O2", "-Wall", "-Wextra", "-pedantic", "-Werror", "-o", C_CONSUMER + ".tmp", C_CONSUMER_SRC,
+          f"-L{HERE}", "-l:liboxen_hash.so", "-Wl,-rpath,$ORIGIN/../../oxen_amd"]),
         (COMMIT_CLI, [COMMIT_CLI_SRC, COMMIT_HDR, HOST_HDR, HOST_LIB],
          ["g++", "-std=c++17", "-O2", "-Wall", "-o", COMMIT_CLI + ".tmp", COMMIT_CLI_SRC,
           f"-L{HERE}", "-l:liboxen_hasher.so", "-l:liboxen_hash.so", "-Wl,-rpath,$ORIGIN/../../oxen_amd"]),

@@ -118,3 +118,32 @@ def test_header_compiles_standalone_as_c_and_cpp(tmp_path):
         r = subprocess.run(["gcc" if lang == "c" else "g++", std, "-Wall", "-Wextra", "-pedantic", "-Werror",
                             "-fsyntax-only", "-x", lang, hdr], capture_output=True, text=True)
         assert r.returncode == 0, (lang, r.stderr)
+
+
+def _c_consumer(*args):
+    from oxen_amd import build
+
+    build.build_host()
+    return subprocess.run([build.C_CONSUMER, *args], capture_output=True, text=True, timeout=120)
+
+
+def test_plain_c_consumer_without_device(built_lib):
+    """tests/native/abi_c_consumer.c: the ABI from plain C99 (gcc -std=c99 -pedantic -Werror), as a cgo /
+    bindgen caller uses it -- version, formatting, argument errors, and OXH_ERR_NODEVICE from context
+    creation and the comm check when no GPU is visible (no CPU fallback)."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("the no-device branch needs a host without a GPU")
+    r = _c_consumer()
+    assert r.returncode == 0, r.stderr
+    assert "all checks passed (no device)" in r.stdout
+
+
+@pytest.mark.gpu
+def test_plain_c_consumer_on_gpu(cuda):
+    """The same C99 program on the GPU box: the reference's known answer and the SURVEY §8c vectors
+    through oxh_hash_buffers and oxh_hash_streams, formatted as MerkleHash Display does."""
+    r = _c_consumer("gpu")
+    assert r.returncode == 0, r.stderr
+    assert "all checks passed (gpu)" in r.stdout
