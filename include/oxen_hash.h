@@ -406,8 +406,9 @@ int oxh_fill_splitmix(void* d_buf, uint64_t nbytes, uint64_t seed, void* stream)
 /* Diagnostic: select the long-path kernel variant (0 = default). Returns the previous value. */
 int oxh_set_kernel_variant(int variant);
 /* Diagnostic counters of a context, out[0..n): [0] device allocations of the large-file piece buffers
- * (files above a staging slot; each one synchronises the device), [1] their current bytes; further
- * entries 0. */
+ * (files above a staging slot; each one synchronises the device), [1] their current bytes, [2] file
+ * requests served on the caller's thread (small requests on an idle context), [3] file-engine runs;
+ * further entries 0. */
 int oxh_ctx_counters(oxh_ctx* ctx, uint64_t* out, int n);
 
 #ifdef __cplusplus

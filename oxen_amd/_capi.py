@@ -171,10 +171,12 @@ class Context:
         return lib().oxh_ctx_stream(self.handle) or 0
 
     def counters(self) -> dict:
-        """oxh_ctx_counters: large-file piece-buffer allocations and their current bytes."""
-        out = (ctypes.c_uint64 * 2)()
-        check(lib().oxh_ctx_counters(self.handle, out, 2), "oxh_ctx_counters")
-        return {"big_allocs": int(out[0]), "big_bytes": int(out[1])}
+        """oxh_ctx_counters: large-file piece-buffer allocations and their current bytes, file requests
+        served on the caller's thread, file-engine runs."""
+        out = (ctypes.c_uint64 * 4)()
+        check(lib().oxh_ctx_counters(self.handle, out, 4), "oxh_ctx_counters")
+        return {"big_allocs": int(out[0]), "big_bytes": int(out[1]), "direct_requests": int(out[2]),
+                "engine_runs": int(out[3])}
 
     def close(self) -> None:
         if getattr(self, "handle", None):

@@ -62,8 +62,8 @@ extern "C" {
 
 int oxh_ctx_counters(oxh_ctx* c, uint64_t* out, int n) {
     if (!c || (n > 0 && !out)) return fail(OXH_ERR_INVALID, "null argument");
-    const uint64_t v[2] = {c->d_big_allocs, c->d_big_size};
-    for (int i = 0; i < n; ++i) out[i] = i < 2 ? v[i] : 0;
+    const uint64_t v[4] = {c->d_big_allocs, c->d_big_size, c->n_direct.load(), c->n_runs.load()};
+    for (int i = 0; i < n; ++i) out[i] = i < 4 ? v[i] : 0;
     return OXH_OK;
 }
 
@@ -101,6 +101,9 @@ int oxh_ctx_create(int device, uint64_t staging_bytes, oxh_ctx** out) {
         if (hipMalloc(&c->d_cnt[s], c->max_items * 16) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "device counts");
         if (hipHostMalloc(&c->h_utf8[s], c->max_items * 4, hipHostMallocDefault) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "pinned utf8");
         if (hipMalloc(&c->d_utf8[s], c->max_items * 4) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "device utf8");
+        if (hipHostMalloc(&c->h_klen[s], c->max_items * 8, hipHostMallocDefault) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "pinned wave lens");
+        if (hipMalloc(&c->d_klen[s], c->max_items * 8) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "device wave lens");
+        if (hipMalloc(&c->d_sums[s], ((c->stage_bytes >> 10) + 1) * 64) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "device block sums");
         if (hipEventCreateWithFlags(&c->ev_copied[s], hipEventDisableTiming) != hipSuccess) return cleanup(OXH_ERR_HIP, "event");
         if (hipEventCreateWithFlags(&c->ev_done[s], hipEventDisableTiming) != hipSuccess) return cleanup(OXH_ERR_HIP, "event");
     }
@@ -150,6 +153,9 @@ int oxh_ctx_destroy(oxh_ctx* c) {
         if (c->d_cnt[s]) (void)hipFree(c->d_cnt[s]);
         if (c->h_utf8[s]) (void)hipHostFree(c->h_utf8[s]);
         if (c->d_utf8[s]) (void)hipFree(c->d_utf8[s]);
+        if (c->h_klen[s]) (void)hipHostFree(c->h_klen[s]);
+        if (c->d_klen[s]) (void)hipFree(c->d_klen[s]);
+        if (c->d_sums[s]) (void)hipFree(c->d_sums[s]);
         if (c->ev_copied[s]) (void)hipEventDestroy(c->ev_copied[s]);
         if (c->ev_done[s]) (void)hipEventDestroy(c->ev_done[s]);
     }

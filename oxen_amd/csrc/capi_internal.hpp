@@ -137,6 +137,11 @@ struct oxh_ctx {
     uint64_t* d_cnt[oxh::capi::NSLOT] = {};
     int32_t* h_utf8[oxh::capi::NSLOT] = {};  // is_utf8 of each item's first 4 KiB (util/fs.rs:652-668)
     int32_t* d_utf8[oxh::capi::NSLOT] = {};
+    // a slot's large items on K1L (submit_slot): the lens the K1 wave launch sees (those items zeroed),
+    // and their block sums (8 u64 per KiB: at most a sixteenth of the slot)
+    uint64_t* h_klen[oxh::capi::NSLOT] = {};
+    uint64_t* d_klen[oxh::capi::NSLOT] = {};
+    uint64_t* d_sums[oxh::capi::NSLOT] = {};
     // streaming file engine (engine.hip): file calls queue requests here; the engine thread runs
     // them, and requests arriving while it runs join the live pipeline
     std::mutex qmu;
@@ -150,6 +155,7 @@ struct oxh_ctx {
     uint8_t* d_big = nullptr;
     uint64_t d_big_size = 0;
     uint64_t d_big_allocs = 0;   // times d_big was (re)allocated (oxh_ctx_counters)
+    std::atomic<uint64_t> n_direct{0}, n_runs{0};  // file requests on the caller's thread / engine runs
     uint8_t* h_bounce[8] = {};   // kNBounce pinned bounce buffers, used as a ring
     hipEvent_t ev_bounce[8] = {};
     bool bounce_used[8] = {};
@@ -224,6 +230,9 @@ int drain_slot(oxh_ctx* c, int s, Pending& p, uint64_t* out);
 // Unused dynamic LDS on top of the kernel's 32 KiB makes every chain workgroup need more than half a
 // CU's 160 KiB: one chain per CU.
 constexpr size_t kChainLdsPad = 50 * 1024;
+// Items of a staged batch at least this long (the kChainJobs largest) take K1L instead of a K1 wave
+// (submit_slot). OXH_SLOT_CHAINS=0: every item on a wave (the r01-r06 form, for A/B).
+constexpr uint64_t kSlotChainBytes = 1ull << 20;
 constexpr uint64_t kBounce = 64ull << 20, kBigRead = 4ull << 20;
 constexpr int kNBounce = 8;  // bounce buffers in the ring: up to 7 windows read while earlier H2Ds drain
 

@@ -49,6 +49,31 @@ struct SlotRun {  // a submitted slot
     bool text = false, utf8 = false;
 };
 
+// A file of at least kSplitBytes in a slot is read in kPartBytes parts by several readers: one pread
+// stream from the page cache copies ~5-10 GB/s, so a slot holding one 200 MiB file waited ~30 ms on
+// its reader. The parts together read [0, L + 1), one byte past the expected size, as read_expected does.
+// OXH_SPLIT_READS=0: one pread per file (the r01-r06 form, for A/B).
+constexpr uint64_t kPartBytes = 4ull << 20, kSplitBytes = 8ull << 20;
+inline bool split_reads() {
+    static const bool on = !(getenv("OXH_SPLIT_READS") && atoi(getenv("OXH_SPLIT_READS")) == 0);
+    return on;
+}
+
+struct PartFile {  // one split file, shared by its parts: the reader that finishes the last one completes it
+    FileRequest* r = nullptr;
+    uint64_t i = 0, j = 0, L = 0;
+    int fd = -1, s = 0;
+    uint8_t* dst = nullptr;
+    std::atomic<int> left{0};
+    std::atomic<int> err{0};            // errno of a failed pread (the first one recorded)
+    std::atomic<bool> failed{false};
+    std::atomic<bool> resized{false};   // fewer or more than L bytes: its size changed since the stat
+};
+struct PartTask {
+    PartFile* f = nullptr;
+    uint64_t lo = 0, hi = 0;  // file bytes [lo, hi) into f->dst + lo
+};
+
 }  // namespace oxh::capi
 
 // One file call (oxh_hash_files / _text / _text_utf8 / oxh_add_files / fsck). Lives on its caller's
@@ -91,6 +116,8 @@ struct FileStream {
     std::vector<FileRequest*> reqs;      // joined requests; nullptr once complete (under c->qmu)
     size_t cur_req = 0;                  // under c->qmu
     std::atomic<bool> want_text{false}, want_utf8{false};
+    std::deque<PartTask> parts;          // parts of split files not yet claimed (under c->qmu)
+    std::atomic<uint64_t> n_parts{0};    // parts.size(), read without the lock by waiting readers
     std::atomic<int> claimed_out{0};     // requests with every file claimed, not yet complete
     std::mutex omu;
     std::vector<std::pair<FileRequest*, uint64_t>> oversize;
@@ -108,9 +135,8 @@ struct FileStream {
 
 inline void pause_us(int us) { std::this_thread::sleep_for(std::chrono::microseconds(us)); }
 
-// Request r is complete: zero the outputs of failed items (add.rs:533-544 skips them), report sizes
-// and statuses, retire it from the run and wake its caller.
-void finish_request(FileStream& fs, FileRequest* r) {
+// Zero the outputs of r's failed items (add.rs:533-544 skips them), report sizes and statuses.
+void write_outputs(FileRequest* r) {
     for (uint64_t i = 0; i < r->n; ++i) {
         if (r->st[i] != OXH_OK) {
             r->out[2 * i] = r->out[2 * i + 1] = 0;
@@ -121,6 +147,11 @@ void finish_request(FileStream& fs, FileRequest* r) {
         if (r->status) r->status[i] = r->st[i];
         if (r->os_err) r->os_err[i] = r->st[i] == OXH_OK ? 0 : r->eno[i];
     }
+}
+
+// Request r is complete: write its outputs, retire it from the run and wake its caller.
+void finish_request(FileStream& fs, FileRequest* r) {
+    write_outputs(r);
     {
         std::lock_guard<std::mutex> g(fs.c->qmu);
         fs.reqs[r->idx] = nullptr;
@@ -147,19 +178,46 @@ inline int unreadable_errno(int fd, struct stat& sb) {
     return S_ISDIR(sb.st_mode) ? EISDIR : EINVAL;
 }
 
+// pread a file expected to hold L bytes into dst, asking for one byte more (a file that grew since its
+// size was taken shows as a longer count): the count read, or -1 with the read's errno in e
+inline int64_t read_expected(int fd, uint8_t* dst, uint64_t L, int& e) {
+    const uint64_t want = L + 1;
+    uint64_t got = 0;
+    while (got < want) {
+        const ssize_t k = pread(fd, dst + got, want - got, (off_t)got);
+        if (k < 0) {
+            e = errno;
+            return -1;
+        }
+        if (k == 0) break;  // EOF
+        got += (uint64_t)k;
+        // a short read of a regular file ends at its EOF: once the expected L bytes are in,
+        // that settles the size without the extra pread that would return 0
+        if (got >= L && (uint64_t)k < want - (got - (uint64_t)k)) break;
+    }
+    return (int64_t)got;
+}
+
 // k more items of r are fully written; the thread that accounts the last one completes r.
 inline void account(FileStream& fs, FileRequest* r, uint64_t k) {
     if (k && r->remaining.fetch_sub(k, std::memory_order_acq_rel) == k) finish_request(fs, r);
 }
 
-// Next files to read: [i0, i1) of request *r. Moves queued requests into the run; an idle reader
-// sleeps until a request arrives or the engine closes the run. False = stop.
-bool claim(FileStream& fs, FileRequest*& r, uint64_t& i0, uint64_t& i1) {
+// Next work: a part of a split file (pt.f set), else files [i0, i1) of request *r. Moves queued
+// requests into the run; an idle reader sleeps until a request or a part arrives or the engine closes
+// the run. False = stop.
+bool claim(FileStream& fs, FileRequest*& r, uint64_t& i0, uint64_t& i1, PartTask& pt) {
     constexpr uint64_t kClaim = 8;
     oxh_ctx* c = fs.c;
     std::unique_lock<std::mutex> lk(c->qmu);
     for (;;) {
         if (fs.abort.load(std::memory_order_relaxed) || fs.closing) return false;
+        if (!fs.parts.empty()) {
+            pt = fs.parts.front();
+            fs.parts.pop_front();
+            fs.n_parts.fetch_sub(1);
+            return true;
+        }
         for (; fs.cur_req < fs.reqs.size(); ++fs.cur_req) {
             FileRequest* q = fs.reqs[fs.cur_req];
             if (q && q->next < q->n) {
@@ -183,17 +241,21 @@ bool claim(FileStream& fs, FileRequest*& r, uint64_t& i0, uint64_t& i1) {
             continue;
         }
         if (fs.idle.fetch_add(1) + 1 == fs.nreaders) fs.wake();  // the engine may flush or close now
-        c->qcv.wait(lk, [&] { return fs.abort.load() || fs.closing || !c->queue.empty(); });
+        c->qcv.wait(lk, [&] { return fs.abort.load() || fs.closing || !c->queue.empty() || !fs.parts.empty(); });
         fs.idle.fetch_sub(1);
     }
 }
+
+// A reader waiting for a slot reads queued parts meanwhile: the slot it waits for may be held by a
+// split file whose parts only readers can finish.
+bool help_with_a_part(FileStream& fs);
 
 // Open slot t for filling (generation + 1, empty, unsealed) once the engine has freed it.
 bool open_slot(FileStream& fs, int t) {
     SlotFill& nx = fs.slot[t];
     while (nx.state.load(std::memory_order_acquire) != 0) {
         if (fs.abort.load(std::memory_order_relaxed)) return false;
-        pause_us(5);
+        if (!help_with_a_part(fs)) pause_us(5);
     }
     const uint64_t gen = (nx.word.load(std::memory_order_relaxed) >> kGenShift) + 1;
     nx.done.store(0, std::memory_order_relaxed);
@@ -219,7 +281,7 @@ int reserve(FileStream& fs, FileRequest* r, uint64_t i, uint64_t L, uint64_t roo
             // waiting on `cur` alone would then never end
             while (fs.cur.load(std::memory_order_acquire) == s && sl.word.load(std::memory_order_acquire) == w &&
                    !fs.abort.load(std::memory_order_relaxed))
-                pause_us(2);
+                if (!help_with_a_part(fs)) pause_us(2);
             continue;
         }
         const uint64_t o = w_bytes(w), j = w_items(w);
@@ -240,12 +302,80 @@ int reserve(FileStream& fs, FileRequest* r, uint64_t i, uint64_t L, uint64_t roo
     }
 }
 
+// Item j of slot s is fully written: the last writer of a sealed slot wakes the engine.
+inline void slot_item_done(FileStream& fs, int s) {
+    const uint64_t d = fs.slot[s].done.fetch_add(1, std::memory_order_acq_rel) + 1;
+    const uint64_t w = fs.slot[s].word.load(std::memory_order_acquire);
+    if ((w & kSealedBit) && d == w_items(w)) fs.wake();
+}
+
+// The file in slot s, item j is not the size its stat / its caller gave: the engine re-reads it.
+inline void item_resized(FileStream& fs, FileRequest* r, uint64_t i, int s, uint64_t j) {
+    fs.c->rq[s][j] = nullptr;  // drain skips this slot entry
+    {
+        std::lock_guard<std::mutex> g(fs.omu);
+        fs.changed.push_back({r, i});
+    }
+    fs.n_changed.fetch_add(1);
+    fs.wake();
+}
+
+// Read one part of a split file; the reader that finishes its file's last part completes the item.
+void run_part(FileStream& fs, const PartTask& t) {
+    PartFile* f = t.f;
+    const uint64_t n = t.hi - t.lo;
+    const bool last = t.hi == f->L + 1;
+    uint64_t got = 0;
+    while (got < n && !f->failed.load(std::memory_order_relaxed)) {
+        const ssize_t k = pread(f->fd, f->dst + t.lo + got, n - got, (off_t)(t.lo + got));
+        if (k < 0) {
+            int zero = 0;
+            f->err.compare_exchange_strong(zero, errno);
+            f->failed.store(true);
+            break;
+        }
+        if (k == 0) break;  // EOF
+        got += (uint64_t)k;
+        // the last part asks for one byte past L: a short read once L is reached is the EOF
+        if (last && t.lo + got >= f->L && (uint64_t)k < n - (got - (uint64_t)k)) break;
+    }
+    // a part that ends before L, or the last one reaching L + 1: the file changed size
+    if (!f->failed.load() && (last ? t.lo + got != f->L : got != n)) f->resized.store(true);
+    if (f->left.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
+    close(f->fd);
+    if (f->failed.load()) item_failed(f->r, f->i, OXH_ERR_IO, f->err.load());
+    else if (f->resized.load()) item_resized(fs, f->r, f->i, f->s, f->j);
+    const int s = f->s;
+    delete f;
+    slot_item_done(fs, s);
+}
+
+bool help_with_a_part(FileStream& fs) {
+    if (fs.n_parts.load(std::memory_order_acquire) == 0) return false;
+    PartTask t;
+    {
+        std::lock_guard<std::mutex> g(fs.c->qmu);
+        if (fs.parts.empty()) return false;
+        t = fs.parts.front();
+        fs.parts.pop_front();
+        fs.n_parts.fetch_sub(1);
+    }
+    run_part(fs, t);
+    return true;
+}
+
 void reader_loop(FileStream& fs) {
     oxh_ctx* c = fs.c;
     FileRequest* r = nullptr;
     uint64_t i0 = 0, i1 = 0;
     bool stop = false;
-    while (!stop && claim(fs, r, i0, i1)) {
+    PartTask pt;
+    while (!stop && claim(fs, r, i0, i1, pt)) {
+        if (pt.f) {
+            run_part(fs, pt);
+            pt = PartTask{};
+            continue;
+        }
         uint64_t failed = 0;  // items of this claim that never reach a slot
         for (uint64_t i = i0; i < i1; ++i) {
             struct stat sb;
@@ -285,35 +415,27 @@ void reader_loop(FileStream& fs) {
                 stop = true;  // aborted: the engine fails every open request
                 break;
             }
-            uint8_t* dst = c->h_stage[s] + off;
-            const uint64_t want = L + 1;
-            uint64_t got = 0;
-            while (got < want) {
-                const ssize_t k = pread(fd, dst + got, want - got, (off_t)got);
-                if (k < 0) {
-                    item_failed(r, i, OXH_ERR_IO, errno);
-                    break;
-                }
-                if (k == 0) break;  // EOF
-                got += (uint64_t)k;
-                // a short read of a regular file ends at its EOF: once the expected L bytes are in,
-                // that settles the size without the extra pread that would return 0
-                if (got >= L && (uint64_t)k < want - (got - (uint64_t)k)) break;
-            }
-            close(fd);
-            if (r->st[i] == OXH_OK && got != L) {  // the file is not the size the stat / the caller saw
-                c->rq[s][j] = nullptr;                     // drain skips this slot entry
+            if (L >= kSplitBytes && fs.nreaders > 1 && split_reads()) {  // parts for the other readers; part 0 here
+                auto* f = new PartFile;
+                f->r = r, f->i = i, f->j = j, f->L = L, f->fd = fd, f->s = s, f->dst = c->h_stage[s] + off;
+                const uint64_t nparts = (L + kPartBytes) / kPartBytes;  // over [0, L + 1)
+                f->left.store((int)nparts);
                 {
-                    std::lock_guard<std::mutex> g(fs.omu);
-                    fs.changed.push_back({r, i});
+                    std::lock_guard<std::mutex> g(c->qmu);
+                    for (uint64_t k = 1; k < nparts; ++k)
+                        fs.parts.push_back({f, k * kPartBytes, std::min(L + 1, (k + 1) * kPartBytes)});
+                    fs.n_parts.fetch_add(nparts - 1);
                 }
-                fs.n_changed.fetch_add(1);
-                fs.wake();
+                c->qcv.notify_all();
+                run_part(fs, {f, 0, kPartBytes});
+                continue;
             }
-            // the last writer of a sealed slot wakes the engine
-            const uint64_t d = fs.slot[s].done.fetch_add(1, std::memory_order_acq_rel) + 1;
-            const uint64_t w = fs.slot[s].word.load(std::memory_order_acquire);
-            if ((w & kSealedBit) && d == w_items(w)) fs.wake();
+            int e = 0;
+            const int64_t got = read_expected(fd, c->h_stage[s] + off, L, e);
+            close(fd);
+            if (got < 0) item_failed(r, i, OXH_ERR_IO, e);
+            if (got >= 0 && (uint64_t)got != L) item_resized(fs, r, i, s, j);  // not the size the stat / the caller saw
+            slot_item_done(fs, s);
         }
         if (!stop) account(fs, r, failed);
     }
@@ -504,6 +626,7 @@ int refresh_file(FileStream& fs, FileRequest* r, uint64_t i) {
 void run_stream(oxh_ctx* c) {
     FileStream fs;
     fs.c = c;
+    c->n_runs.fetch_add(1, std::memory_order_relaxed);
     {
         std::lock_guard<std::mutex> g(c->qmu);
         c->live = &fs;
@@ -664,6 +787,16 @@ void run_stream(oxh_ctx* c) {
             c->qcv.notify_all();
         }
         readers.wait();
+        {  // parts no reader took (the run aborted): their files' descriptors and state
+            std::vector<PartFile*> left;
+            for (const PartTask& t : fs.parts)
+                if (std::find(left.begin(), left.end(), t.f) == left.end()) left.push_back(t.f);
+            fs.parts.clear();
+            for (PartFile* f : left) {
+                close(f->fd);
+                delete f;
+            }
+        }
         (void)hipStreamSynchronize(c->stream);
         (void)hipStreamSynchronize(c->copy_stream);
         std::vector<FileRequest*> open;
@@ -740,6 +873,130 @@ void dump_engine(oxh_ctx* c, const FileRequest& r) {
     }
 }
 
+// Small requests on an idle context: the caller's own thread does what an engine run would do for them
+// -- open + fstat (or the caller's size), pread into staging slot 0, one submit, wait -- with none of a
+// run's hand-offs (engine wake-up, reader-pool start, the readers' idle handshake, the engine's 20 us
+// drain poll, the caller's wake-up), which cost ~60 of a one-file call's ~100 us (DESIGN §5 "Per-call
+// latency"). This is the shape of the per-file callers (hash_file_contents from restore, checkout, the
+// metadata CLI). Requests of more files, or more bytes, or arriving while a run is live keep the engine,
+// where concurrent requests share slots and reads run in parallel. The outputs are the engine's: the
+// same reads (read_expected), statuses, errnos and kernels; a file whose size changed between its stat
+// and its read hands the whole request back to the engine, whose refresh path re-reads it.
+// OXH_DIRECT_FILES=0 turns it off (A/B, and the tests that compare both forms).
+constexpr uint64_t kDirectFiles = 8, kDirectBytes = 2ull << 20;
+
+// OXH_OK / an error: the request is done. kDirectDeclined: the engine runs it (r is as it was).
+constexpr int kDirectDeclined = -1;
+
+int direct_files(oxh_ctx* c, FileRequest& r) {
+    const uint64_t n = r.n;
+    if (n > kDirectFiles || n > c->max_items) return kDirectDeclined;
+    const char* env = getenv("OXH_DIRECT_FILES");
+    if (env && atoi(env) == 0) return kDirectDeclined;
+    {
+        std::lock_guard<std::mutex> g(c->qmu);
+        if (c->live || !c->queue.empty()) return kDirectDeclined;
+    }
+    // the slots are the holder's (an engine run, a buffer call, the large-item path): never wait for one
+    std::unique_lock<std::mutex> lk(c->mu, std::try_to_lock);
+    if (!lk.owns_lock()) return kDirectDeclined;
+    int fds[kDirectFiles];
+    auto decline = [&](uint64_t upto) {
+        for (uint64_t i = 0; i < upto; ++i)
+            if (fds[i] >= 0) close(fds[i]);
+        r.lens.assign(n, 0);
+        r.st.assign(n, OXH_OK);
+        r.eno.assign(n, 0);
+        return kDirectDeclined;
+    };
+    // 1. open + fstat, as reader_loop does
+    uint64_t room = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        fds[i] = -1;
+        struct stat sb;
+        const int fd = r.paths[i] ? open(r.paths[i], O_RDONLY | O_CLOEXEC | O_NONBLOCK) : -1;
+        if (fd < 0) {
+            item_failed(&r, i, OXH_ERR_OPEN, r.paths[i] ? errno : EINVAL);
+            continue;
+        }
+        const bool meta = r.meta != nullptr && r.meta[i] < c->stage_bytes;
+        if (!meta && (fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode))) {
+            item_failed(&r, i, OXH_ERR_IO, unreadable_errno(fd, sb));
+            close(fd);
+            continue;
+        }
+        fds[i] = fd;
+        r.lens[i] = meta ? r.meta[i] : (uint64_t)sb.st_size;
+        room += align_up(r.lens[i] + 1);
+        if (r.lens[i] >= c->stage_bytes || room > kDirectBytes || room > c->stage_bytes) return decline(i + 1);
+    }
+    const int prev_dev = [] {
+        int d = 0;
+        (void)hipGetDevice(&d);
+        return d;
+    }();
+    if (hipSetDevice(c->device) != hipSuccess) {
+        decline(n);
+        return fail(OXH_ERR_HIP, "hipSetDevice failed");
+    }
+    struct RestoreDevice {  // the caller's thread keeps its current device
+        int d;
+        ~RestoreDevice() { (void)hipSetDevice(d); }
+    } restore{prev_dev};
+    // 2. read into slot 0 at the engine's placement (256-B aligned, one spare byte per item)
+    const int s = 0;
+    const uint64_t M = c->max_items;
+    uint64_t* hoff = c->h_desc[s];
+    uint64_t* hlen = c->h_desc[s] + M;
+    uint64_t idx[kDirectFiles];
+    uint64_t off = 0, cnt = 0, bytes = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (fds[i] < 0) continue;
+        const uint64_t L = r.lens[i];
+        int e = 0;
+        const int64_t got = read_expected(fds[i], c->h_stage[s] + off, L, e);
+        close(fds[i]);
+        fds[i] = -1;
+        if (got < 0) {
+            item_failed(&r, i, OXH_ERR_IO, e);
+            continue;
+        }
+        if ((uint64_t)got != L) return decline(n);  // its size changed: the engine's refresh path
+        hoff[cnt] = off;
+        hlen[cnt] = L;
+        idx[cnt++] = i;
+        bytes = off + L;
+        off += align_up(L + 1);
+    }
+    // 3. one batch: H2D, K1 / K1T (+ is_utf8), D2H -- the engine's submit
+    if (cnt) {
+        c->where.store("direct: submit_slot");
+        const bool text = r.counts != nullptr, utf8 = r.utf8 != nullptr;
+        if (int rc = submit_slot(c, s, bytes, cnt, false, bytes / cnt <= kShortItemBytes, text, utf8)) return rc;
+        Pending p;
+        p.busy = true;
+        p.ids.assign(idx, idx + cnt);
+        c->where.store("direct: wait_slot");
+        if (int rc = wait_slot(c, s, p)) return rc;
+        c->where.store("direct: done");
+        for (uint64_t j = 0; j < cnt; ++j) {
+            const uint64_t i = idx[j];
+            r.out[2 * i] = c->h_out[s][2 * j];
+            r.out[2 * i + 1] = c->h_out[s][2 * j + 1];
+            if (text) {
+                r.counts[2 * i] = c->h_cnt[s][2 * j];
+                r.counts[2 * i + 1] = c->h_cnt[s][2 * j + 1];
+            }
+            if (utf8) r.utf8[i] = c->h_utf8[s][j];
+            if (r.sink) r.sink->put(i, c->h_stage[s] + hoff[j], hlen[j], r.out[2 * i], r.out[2 * i + 1]);
+        }
+        if (r.sink) r.sink->commit();
+    }
+    write_outputs(&r);
+    c->n_direct.fetch_add(1, std::memory_order_relaxed);
+    return OXH_OK;
+}
+
 int hash_files_impl(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* out, uint64_t* sizes, int32_t* status,
                     uint64_t* counts, ItemSink* sink, int32_t* utf8, const uint64_t* meta, int32_t* os_error) {
     if (!c || (n && (!paths || !out))) return fail(OXH_ERR_INVALID, "bad arguments");
@@ -759,6 +1016,7 @@ int hash_files_impl(oxh_ctx* c, const char* const* paths, uint64_t n, uint64_t* 
     r.st.assign(n, OXH_OK);
     r.eno.assign(n, 0);
     r.remaining.store(n);
+    if (const int d = direct_files(c, r); d != kDirectDeclined) return d;
     {
         std::lock_guard<std::mutex> g(c->qmu);
         c->queue.push_back(&r);

@@ -8,10 +8,35 @@ using namespace oxh::capi;
 
 namespace oxh::capi {
 
+// The batch's large items for K1L, at most kChainJobs (the largest): one K1 wave reads ~10 GB/s, so a
+// batch holding a few large files waited on their waves -- a 200 MiB file ~20 ms against ~4 ms to copy
+// it over PCIe, and one 1 MiB file ~100 us of a single-file call. K1L's block sums run chip-wide and
+// its serial chain costs ~17 ns per KiB. Plain digests only: K1T's text counts stay
+// on the wave.
+static uint64_t slot_chain_items(const uint64_t* hlen, uint64_t cnt, uint64_t* big) {
+    static const bool on = !(getenv("OXH_SLOT_CHAINS") && atoi(getenv("OXH_SLOT_CHAINS")) == 0);
+    uint64_t nbig = 0;
+    if (!on) return 0;
+    for (uint64_t j = 0; j < cnt; ++j) {
+        if (hlen[j] < kSlotChainBytes) continue;
+        if (nbig < (uint64_t)oxh::kChainJobs) {
+            big[nbig++] = j;
+            continue;
+        }
+        uint64_t m = 0;  // the smallest kept item gives way to a larger one
+        for (uint64_t q = 1; q < nbig; ++q)
+            if (hlen[big[q]] < hlen[big[m]]) m = q;
+        if (hlen[j] > hlen[big[m]]) big[m] = j;
+    }
+    return nbig;
+}
+
 // One staged batch: items [0, cnt) already in h_stage[s] at h_desc offsets; launch and queue D2H.
 int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_only, bool short_items, bool text,
                 bool utf8) {
     const uint64_t M = c->max_items;
+    uint64_t big[oxh::kChainJobs];
+    const uint64_t nbig = text || any_short_only ? 0 : slot_chain_items(c->h_desc[s] + M, cnt, big);
     STEP("submit s=%d bytes=%llu cnt=%llu lane=%d short=%d", s, (unsigned long long)bytes, (unsigned long long)cnt,
          (int)any_short_only, (int)short_items);
     c->where.store("submit_slot: H2D stage");
@@ -19,6 +44,13 @@ int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_
     c->where.store("submit_slot: H2D desc");
     HIP_TRY(hipMemcpyAsync(c->d_desc[s], c->h_desc[s], cnt * 8, hipMemcpyHostToDevice, c->copy_stream));
     HIP_TRY(hipMemcpyAsync(c->d_desc[s] + M, c->h_desc[s] + M, cnt * 8, hipMemcpyHostToDevice, c->copy_stream));
+    const uint64_t* d_wave_lens = c->d_desc[s] + M;
+    if (nbig) {  // the wave launch sees the K1L items as empty
+        memcpy(c->h_klen[s], c->h_desc[s] + M, cnt * 8);
+        for (uint64_t q = 0; q < nbig; ++q) c->h_klen[s][big[q]] = 0;
+        HIP_TRY(hipMemcpyAsync(c->d_klen[s], c->h_klen[s], cnt * 8, hipMemcpyHostToDevice, c->copy_stream));
+        d_wave_lens = c->d_klen[s];
+    }
     c->where.store("submit_slot: record / wait");
     HIP_TRY(hipEventRecord(c->ev_copied[s], c->copy_stream));
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[s], 0));
@@ -27,9 +59,29 @@ int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_
     int rc = text ? launch_text(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->d_cnt[s], c->stream,
                                 short_items)
              : any_short_only ? launch_lane(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->stream)
-                              : launch_wave(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->stream,
+                              : launch_wave(c->d_stage[s], c->d_desc[s], d_wave_lens, cnt, c->d_out[s], c->stream,
                                             short_items ? ItemShape::Short : ItemShape::Long);
     if (rc) return rc;
+    if (nbig) {  // K1L: each item's block sums chip-wide, then one launch of their chains (after the
+                 // wave kernel on the same stream, so the chains' digests are the ones that stay)
+        oxh::ChainBatch batch;
+        uint64_t soff = 0;
+        for (uint64_t q = 0; q < nbig; ++q) {
+            const uint64_t j = big[q], L = c->h_desc[s][M + j], nb = (L - 1) >> 10;
+            const uint8_t* p = c->d_stage[s] + c->h_desc[s][j];
+            uint64_t* sums = c->d_sums[s] + soff;
+            soff += nb * 8;
+            const uint64_t blocks = ((nb + 3) / 4 + 3) / 4;
+            if ((reinterpret_cast<uintptr_t>(p) & 15) == 0)
+                hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, c->stream, p, nb, sums);
+            else
+                hipLaunchKernelGGL(oxh::xxh3_blocksum_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, c->stream, p, nb, sums);
+            HIP_TRY(hipGetLastError());
+            batch.job[q] = {p, L, sums, c->d_out[s] + 2 * j, L, nullptr, 0};
+        }
+        hipLaunchKernelGGL(oxh::xxh3_chain_kernel, dim3((unsigned)nbig), dim3(64), kChainLdsPad, c->stream, batch);
+        HIP_TRY(hipGetLastError());
+    }
     STEP("launched s=%d", s);
     c->where.store("submit_slot: D2H");
     HIP_TRY(hipMemcpyAsync(c->h_out[s], c->d_out[s], cnt * 16, hipMemcpyDeviceToHost, c->stream));

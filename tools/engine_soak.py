@@ -25,6 +25,9 @@ device-resident callers in other processes) run.
 --mutate: a mutator thread atomically replaces files of a hot tenth of the corpus (sizes across the
 1 MiB slot too) while the requests run; a digest must then be one of the file's versions (no torn
 read: the engine's re-read on a size change, read to EOF) with that version's counts and is_utf8.
+--split: about 0.5 % of the corpus 8-24 MiB (read in 4 MiB parts by several readers, engine.hip
+run_part), a third context with 32 MiB slots (split files compete for slots), and the mutator's sizes
+include 10 MiB.
 Prints one JSON line: per-kind counts, items checked, failures (the first few described). Exit 1 on any
 mismatch.
 """
@@ -55,6 +58,8 @@ def main():
                          "one of that file's versions, with that version's text counts and is_utf8")
     ap.add_argument("--regrow", action="store_true",
                     help="a thread keeps creating contexts whose large-file piece buffers regrow (1, 2, 4 files side by side)")
+    ap.add_argument("--split", action="store_true",
+                    help="files of 8-24 MiB (split reads), a 32 MiB-slot context, 10 MiB mutations")
     a = ap.parse_args()
 
     import numpy as np
@@ -79,6 +84,8 @@ def main():
             r = rng.random()
             n = 0 if r < 0.02 else rng.randint(1, 240) if r < 0.2 else rng.randint(241, 300_000) if r < 0.99 \
                 else rng.randint(1_200_000, 3_000_000)
+            if a.split and rng.random() < 0.005:
+                n = rng.randint(8 << 20, 24 << 20)
             if i % 3 == 0:
                 data = b"".join(rng.choice(words) for _ in range(n // 4 + 1))[:n]
             else:
@@ -98,6 +105,8 @@ def main():
                 return hist[p].get(d)
 
         ctxs = [_capi.Context(0, staging_bytes=1 << 20), _capi.Context(0)]
+        if a.split:
+            ctxs.append(_capi.Context(0, staging_bytes=32 << 20))
         lock = threading.Lock()
         counts = {k: 0 for k in ("files", "text", "add", "buffers", "stream", "meta", "streams", "modified", "utf8", "pool",
                                  "cdc", "fixed")}
@@ -291,7 +300,7 @@ def main():
             hot_list = sorted(hot)
             while time.time() < deadline and not fails:
                 p = r.choice(hot_list)
-                n = r.choice((0, 100, 5000, 60_000, 300_000, 1_500_000))
+                n = r.choice((0, 100, 5000, 60_000, 300_000, 1_500_000) + ((10 << 20,) if a.split else ()))
                 data = r.randbytes(n) if r.random() < 0.5 else b"".join(r.choice(words) for _ in range(n // 4 + 1))[:n]
                 d = oracle.xxh3_128_int(data)
                 with lock:

@@ -84,14 +84,18 @@ def main():
         res["batch64_cpu_1thread_us"] = med_us(lambda: oracle.hash_files(batch, threads=1), a.calls)
         buf = rng.integers(0, 256, 4096, dtype=np.uint8).tobytes()
         res["buffer_4k_us"] = med_us(lambda: hasher.hash_buffers_128bit([buf], ctx), a.calls)
-        da = DeviceArena.splitmix([4096], seed=3, device="cuda")
+        buf1m = open(files["1m"], "rb").read()
+        res["buffer_1m_us"] = med_us(lambda: hasher.hash_buffers_128bit([buf1m], ctx), a.calls)
+        res["read_1m_us"] = med_us(lambda: open(files["1m"], "rb").read(), a.calls)
         out = torch.empty((1, 2), dtype=torch.int64, device="cuda")
+        for name, size in (("4k", 4096), ("1m", 1 << 20)):
+            da = DeviceArena.splitmix([size], seed=3, device="cuda")
 
-        def dev():
-            da.hash(out)
-            torch.cuda.synchronize()
+            def dev():
+                da.hash(out)
+                torch.cuda.synchronize()
 
-        res["device_item_4k_launch_sync_us"] = med_us(dev, a.calls)
+            res[f"device_item_{name}_launch_sync_us"] = med_us(dev, a.calls)
         # digests agree
         got = hasher.u128_hash_file_contents(files["4k"])
         o, _, _ = oracle.hash_files([files["4k"]], threads=1)
