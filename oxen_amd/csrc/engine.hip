@@ -52,6 +52,9 @@ struct SlotRun {  // a submitted slot
 // A file of at least kSplitBytes in a slot is read in kPartBytes parts by several readers: one pread
 // stream from the page cache copies ~5-10 GB/s, so a slot holding one 200 MiB file waited ~30 ms on
 // its reader. The parts together read [0, L + 1), one byte past the expected size, as read_expected does.
+// Readers have file-descriptor tables of their own (pool.hpp), so each part opens the path itself and
+// checks that it names the file the first reader opened (device + inode); a file replaced meanwhile is
+// re-read whole by the engine, as one whose size changed.
 // OXH_SPLIT_READS=0: one pread per file (the r01-r06 form, for A/B).
 constexpr uint64_t kPartBytes = 4ull << 20, kSplitBytes = 8ull << 20;
 inline bool split_reads() {
@@ -62,7 +65,9 @@ inline bool split_reads() {
 struct PartFile {  // one split file, shared by its parts: the reader that finishes the last one completes it
     FileRequest* r = nullptr;
     uint64_t i = 0, j = 0, L = 0;
-    int fd = -1, s = 0;
+    dev_t dev = 0;
+    ino_t ino = 0;
+    int s = 0;
     uint8_t* dst = nullptr;
     std::atomic<int> left{0};
     std::atomic<int> err{0};            // errno of a failed pread (the first one recorded)
@@ -320,14 +325,25 @@ inline void item_resized(FileStream& fs, FileRequest* r, uint64_t i, int s, uint
     fs.wake();
 }
 
-// Read one part of a split file; the reader that finishes its file's last part completes the item.
-void run_part(FileStream& fs, const PartTask& t) {
+// Read one part of a split file (through `own_fd`, the first reader's descriptor, or a descriptor of
+// its own); the reader that finishes the file's last part completes the item.
+void run_part(FileStream& fs, const PartTask& t, int own_fd = -1) {
     PartFile* f = t.f;
     const uint64_t n = t.hi - t.lo;
     const bool last = t.hi == f->L + 1;
     uint64_t got = 0;
-    while (got < n && !f->failed.load(std::memory_order_relaxed)) {
-        const ssize_t k = pread(f->fd, f->dst + t.lo + got, n - got, (off_t)(t.lo + got));
+    int fd = own_fd;
+    if (fd < 0) {
+        fd = open(f->r->paths[f->i], O_RDONLY | O_CLOEXEC | O_NONBLOCK);
+        struct stat sb;
+        if (fd >= 0 && (fstat(fd, &sb) != 0 || sb.st_dev != f->dev || sb.st_ino != f->ino)) {
+            close(fd);
+            fd = -1;
+        }
+        if (fd < 0) f->resized.store(true);  // gone or replaced since the first open: the engine re-reads it
+    }
+    while (fd >= 0 && got < n && !f->failed.load(std::memory_order_relaxed)) {
+        const ssize_t k = pread(fd, f->dst + t.lo + got, n - got, (off_t)(t.lo + got));
         if (k < 0) {
             int zero = 0;
             f->err.compare_exchange_strong(zero, errno);
@@ -340,9 +356,9 @@ void run_part(FileStream& fs, const PartTask& t) {
         if (last && t.lo + got >= f->L && (uint64_t)k < n - (got - (uint64_t)k)) break;
     }
     // a part that ends before L, or the last one reaching L + 1: the file changed size
-    if (!f->failed.load() && (last ? t.lo + got != f->L : got != n)) f->resized.store(true);
+    if (fd >= 0 && !f->failed.load() && (last ? t.lo + got != f->L : got != n)) f->resized.store(true);
+    if (fd >= 0 && fd != own_fd) close(fd);
     if (f->left.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
-    close(f->fd);
     if (f->failed.load()) item_failed(f->r, f->i, OXH_ERR_IO, f->err.load());
     else if (f->resized.load()) item_resized(fs, f->r, f->i, f->s, f->j);
     const int s = f->s;
@@ -415,9 +431,12 @@ void reader_loop(FileStream& fs) {
                 stop = true;  // aborted: the engine fails every open request
                 break;
             }
-            if (L >= kSplitBytes && fs.nreaders > 1 && split_reads()) {  // parts for the other readers; part 0 here
+            struct stat fsb;
+            if (L >= kSplitBytes && fs.nreaders > 1 && split_reads() && fstat(fd, &fsb) == 0) {  // parts for the
+                // other readers; part 0 here
                 auto* f = new PartFile;
-                f->r = r, f->i = i, f->j = j, f->L = L, f->fd = fd, f->s = s, f->dst = c->h_stage[s] + off;
+                f->r = r, f->i = i, f->j = j, f->L = L, f->s = s, f->dst = c->h_stage[s] + off;
+                f->dev = fsb.st_dev, f->ino = fsb.st_ino;
                 const uint64_t nparts = (L + kPartBytes) / kPartBytes;  // over [0, L + 1)
                 f->left.store((int)nparts);
                 {
@@ -427,7 +446,8 @@ void reader_loop(FileStream& fs) {
                     fs.n_parts.fetch_add(nparts - 1);
                 }
                 c->qcv.notify_all();
-                run_part(fs, {f, 0, kPartBytes});
+                run_part(fs, {f, 0, kPartBytes}, fd);
+                close(fd);
                 continue;
             }
             int e = 0;
@@ -792,10 +812,7 @@ void run_stream(oxh_ctx* c) {
             for (const PartTask& t : fs.parts)
                 if (std::find(left.begin(), left.end(), t.f) == left.end()) left.push_back(t.f);
             fs.parts.clear();
-            for (PartFile* f : left) {
-                close(f->fd);
-                delete f;
-            }
+            for (PartFile* f : left) delete f;
         }
         (void)hipStreamSynchronize(c->stream);
         (void)hipStreamSynchronize(c->copy_stream);
