@@ -103,7 +103,8 @@ int oxh_ctx_create(int device, uint64_t staging_bytes, oxh_ctx** out) {
         if (hipMalloc(&c->d_utf8[s], c->max_items * 4) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "device utf8");
         if (hipHostMalloc(&c->h_klen[s], c->max_items * 8, hipHostMallocDefault) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "pinned wave lens");
         if (hipMalloc(&c->d_klen[s], c->max_items * 8) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "device wave lens");
-        if (hipMalloc(&c->d_sums[s], ((c->stage_bytes >> 10) + 1) * 64) != hipSuccess) return cleanup(OXH_ERR_NOMEM, "device block sums");
+        if (hipMalloc(&c->d_sums[s], (slot_sums_words(c->stage_bytes) + kSlotCountRaw) * 8) != hipSuccess)
+            return cleanup(OXH_ERR_NOMEM, "device block sums");
         if (hipEventCreateWithFlags(&c->ev_copied[s], hipEventDisableTiming) != hipSuccess) return cleanup(OXH_ERR_HIP, "event");
         if (hipEventCreateWithFlags(&c->ev_done[s], hipEventDisableTiming) != hipSuccess) return cleanup(OXH_ERR_HIP, "event");
     }

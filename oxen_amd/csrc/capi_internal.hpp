@@ -57,6 +57,7 @@ __global__ void fill_splitmix_kernel(uint64_t*, uint64_t, uint64_t);
 template <int VARIANT>
 __global__ void xxh3_text_wave_kernel(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, uint64_t*, uint64_t*);
 __global__ void text_count_kernel(const uint8_t*, uint64_t, unsigned long long*);
+__global__ void text_count_finish_kernel(const unsigned long long*, CountFix, uint64_t*);
 __global__ void utf8_prefix_kernel(const uint8_t*, const uint64_t*, const uint64_t*, uint64_t, int32_t*);
 __global__ void fill_splitmix_tail_kernel(uint8_t*, uint64_t, uint64_t, uint64_t);
 }  // namespace oxh
@@ -138,7 +139,8 @@ struct oxh_ctx {
     int32_t* h_utf8[oxh::capi::NSLOT] = {};  // is_utf8 of each item's first 4 KiB (util/fs.rs:652-668)
     int32_t* d_utf8[oxh::capi::NSLOT] = {};
     // a slot's large items on K1L (submit_slot): the lens the K1 wave launch sees (those items zeroed),
-    // and their block sums (8 u64 per KiB: at most a sixteenth of the slot)
+    // and their block sums (8 u64 per KiB: at most a sixteenth of the slot), then kSlotCountRaw u64 of
+    // raw text counts (K1T batches)
     uint64_t* h_klen[oxh::capi::NSLOT] = {};
     uint64_t* d_klen[oxh::capi::NSLOT] = {};
     uint64_t* d_sums[oxh::capi::NSLOT] = {};
@@ -233,6 +235,8 @@ constexpr size_t kChainLdsPad = 50 * 1024;
 // Items of a staged batch at least this long (the kChainJobs largest) take K1L instead of a K1 wave
 // (submit_slot). OXH_SLOT_CHAINS=0: every item on a wave (the r01-r06 form, for A/B).
 constexpr uint64_t kSlotChainBytes = 1ull << 20;
+constexpr uint64_t kSlotCountRaw = 2 * oxh::kChainJobs;
+inline uint64_t slot_sums_words(uint64_t stage_bytes) { return ((stage_bytes >> 10) + 1) * 8; }
 constexpr uint64_t kBounce = 64ull << 20, kBigRead = 4ull << 20;
 constexpr int kNBounce = 8;  // bounce buffers in the ring: up to 7 windows read while earlier H2Ds drain
 

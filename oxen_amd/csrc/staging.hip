@@ -11,8 +11,8 @@ namespace oxh::capi {
 // The batch's large items for K1L, at most kChainJobs (the largest): one K1 wave reads ~10 GB/s, so a
 // batch holding a few large files waited on their waves -- a 200 MiB file ~20 ms against ~4 ms to copy
 // it over PCIe, and one 1 MiB file ~100 us of a single-file call. K1L's block sums run chip-wide and
-// its serial chain costs ~17 ns per KiB. Plain digests only: K1T's text counts stay
-// on the wave.
+// its serial chain costs ~17 ns per KiB. In a K1T batch their text counts come from
+// text_count_kernel (chip-wide) instead of the wave.
 static uint64_t slot_chain_items(const uint64_t* hlen, uint64_t cnt, uint64_t* big) {
     static const bool on = !(getenv("OXH_SLOT_CHAINS") && atoi(getenv("OXH_SLOT_CHAINS")) == 0);
     uint64_t nbig = 0;
@@ -36,7 +36,7 @@ int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_
                 bool utf8) {
     const uint64_t M = c->max_items;
     uint64_t big[oxh::kChainJobs];
-    const uint64_t nbig = text || any_short_only ? 0 : slot_chain_items(c->h_desc[s] + M, cnt, big);
+    const uint64_t nbig = any_short_only ? 0 : slot_chain_items(c->h_desc[s] + M, cnt, big);
     STEP("submit s=%d bytes=%llu cnt=%llu lane=%d short=%d", s, (unsigned long long)bytes, (unsigned long long)cnt,
          (int)any_short_only, (int)short_items);
     c->where.store("submit_slot: H2D stage");
@@ -56,7 +56,7 @@ int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[s], 0));
     STEP("copies queued s=%d", s);
     c->where.store("submit_slot: launch");
-    int rc = text ? launch_text(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->d_cnt[s], c->stream,
+    int rc = text ? launch_text(c->d_stage[s], c->d_desc[s], d_wave_lens, cnt, c->d_out[s], c->d_cnt[s], c->stream,
                                 short_items)
              : any_short_only ? launch_lane(c->d_stage[s], c->d_desc[s], c->d_desc[s] + M, cnt, c->d_out[s], c->stream)
                               : launch_wave(c->d_stage[s], c->d_desc[s], d_wave_lens, cnt, c->d_out[s], c->stream,
@@ -81,6 +81,22 @@ int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_
         }
         hipLaunchKernelGGL(oxh::xxh3_chain_kernel, dim3((unsigned)nbig), dim3(64), kChainLdsPad, c->stream, batch);
         HIP_TRY(hipGetLastError());
+        if (text) {  // their counts: chip-wide sums, then MetadataText's form over the wave's (1, 0)
+            unsigned long long* raw = (unsigned long long*)(c->d_sums[s] + slot_sums_words(c->stage_bytes));
+            HIP_TRY(hipMemsetAsync(raw, 0, nbig * 16, c->stream));
+            oxh::CountFix fix{};
+            fix.n = (int)nbig;
+            for (uint64_t q = 0; q < nbig; ++q) {
+                const uint64_t j = big[q], L = c->h_desc[s][M + j];
+                fix.j[q] = j, fix.len[q] = L;
+                const unsigned grid = (unsigned)std::min<uint64_t>(2048, (L / 16 + 255) / 256 + 1);
+                hipLaunchKernelGGL(oxh::text_count_kernel, dim3(grid), dim3(256), 0, c->stream, c->d_stage[s] + c->h_desc[s][j],
+                                   L, raw + 2 * q);
+                HIP_TRY(hipGetLastError());
+            }
+            hipLaunchKernelGGL(oxh::text_count_finish_kernel, dim3(1), dim3(64), 0, c->stream, raw, fix, c->d_cnt[s]);
+            HIP_TRY(hipGetLastError());
+        }
     }
     STEP("launched s=%d", s);
     c->where.store("submit_slot: D2H");

@@ -100,6 +100,13 @@ constexpr int kChainJobs = 32;
 struct ChainBatch {
     ChainJob job[kChainJobs];
 };
+// The text counts of up to kChainJobs large items of a staged batch (text_count_kernel's raw newline and
+// continuation-byte sums, raw[2q], raw[2q + 1]) written in MetadataText's form to counts[2 j[q]] and
+// counts[2 j[q] + 1]: num_lines = 1 + newlines, num_chars = len - continuation bytes.
+struct CountFix {
+    uint64_t j[kChainJobs], len[kChainJobs];
+    int n;
+};
 
 // The 24 aligned secret words, for lane-dependent (runtime) indexing on the device.
 static __constant__ uint64_t kSecW[24] = {

@@ -1109,6 +1109,15 @@ __global__ __launch_bounds__(256) void text_count_kernel(const uint8_t* __restri
     }
 }
 
+__global__ void text_count_finish_kernel(const unsigned long long* __restrict__ raw, CountFix fix,
+                                        uint64_t* __restrict__ counts) {
+    const int q = threadIdx.x;
+    if (q < fix.n) {
+        counts[2 * fix.j[q]] = 1 + raw[2 * q];
+        counts[2 * fix.j[q] + 1] = fix.len[q] - raw[2 * q + 1];
+    }
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;

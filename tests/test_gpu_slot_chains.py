@@ -6,8 +6,8 @@ those items as empty and the chains overwrite their digests.
 Every digest here is checked against the oracle (the published XXH3-128, oracle/xxh3_oracle.c):
 lengths around the 1 MiB threshold and the 1 KiB block edges, more large items in one slot than one
 chain launch takes, items just below a slot, unaligned items in a stream arena, and every staged
-entry (the file engine, the small-request path, host buffers, streams, the fused add); a large text
-file (K1T, which stays on the wave) beside them.
+entry (the file engine, the small-request path, host buffers, streams, the fused add); in K1T
+batches the large items' text counts come from text_count_kernel, checked against a direct count.
 """
 import numpy as np
 import pytest
@@ -86,17 +86,35 @@ def test_items_just_below_a_slot(cuda, oracle_lib, tmp_path):
         assert hasher.hash_buffers_128bit(blobs, c) == want
 
 
+def _counts(b):
+    """MetadataText of bytes (repositories/metadata/text.rs:12-20): 1 + newlines, and the bytes that
+    are not UTF-8 continuation bytes (bytecount::num_chars)."""
+    a = np.frombuffer(b, dtype=np.uint8)
+    return {"text": {"num_lines": 1 + b.count(b"\n"), "num_chars": len(b) - int(((a & 0xC0) == 0x80).sum())}}
+
+
 def test_text_request_with_large_files(ctx, oracle_lib, tmp_path):
-    """K1T (digest + text counts in one wave) is not split: a 3 MiB text file and a 2 MiB binary one,
-    digests against the oracle, counts against a direct count."""
+    """K1T batches too: large items take K1L for the digest and text_count_kernel for the counts, the
+    rest K1T's wave. Text of 1 MiB +- a byte, ragged tails, multi-byte characters across 16-B loads,
+    random bytes, a 20 MiB text file read in parts; digests against the oracle, counts against a direct
+    count of the bytes, is_utf8 against the oracle's sniff."""
     from oxen_amd import hasher
 
-    text = ("row,é,中\n" * 300_000).encode()
-    blobs = [text, _blobs([2 * MIB + 3], 75)[0], b"a\nb"]
+    line = "row,é,中,\U0001f600\n".encode()
+    rnd = _blobs([2 * MIB + 3, MIB + 9], 75)
+    blobs = [(line * (MIB // len(line) + 2))[:n] for n in (MIB - 1, MIB, MIB + 1, 3 * MIB + 13)]
+    blobs += [rnd[0], b"a\nb", rnd[1], (line * (20 * MIB // len(line) + 1))[: 20 * MIB + 5], b""]
     paths = _write(tmp_path, blobs)
     d, _, st, meta = hasher.hash_files_text_128bit(paths, ctx=ctx)
     assert not any(st) and d == [oracle_lib.xxh3_128_int(b) for b in blobs]
-    assert meta[0] == {"text": {"num_lines": text.count(b"\n") + 1, "num_chars": len(text.decode())}}
+    assert meta == [_counts(b) for b in blobs]
+    d, _, st, meta, u8 = hasher.hash_files_text_utf8_128bit(paths, ctx=ctx)
+    assert not any(st) and d == [oracle_lib.xxh3_128_int(b) for b in blobs]
+    assert meta == [_counts(b) for b in blobs]
+    assert u8 == [oracle_lib.is_utf8_prefix(b[:4096]) for b in blobs]
+    for p, b in zip(paths, blobs):  # one file per call: the small-request path (up to 2 MiB)
+        _, _, st, m = hasher.hash_files_text_128bit([p], ctx=ctx)
+        assert st == [0] and m == [_counts(b)]
 
 
 # Files of 8 MiB and more in a slot are read in 4 MiB parts by several readers (engine.hip run_part);
