@@ -31,6 +31,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <array>
 #include <deque>
 #include <functional>
 #include <memory>

@@ -228,16 +228,24 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
         }
         STEP("fill s=%d items=%zu", s, batch.size());
         // a small batch is copied on this thread: handing 1 MiB or less to the pool costs more in
-        // wake-ups than the copy (tools/latency_probe.py, one 4 KiB buffer)
-        const int ntasks = off <= (1u << 20) ? 1 : (int)std::min<size_t>(batch.size(), (size_t)c->pool->size() * 4);
-        auto fill = [&](int t) {
-            for (size_t j = (size_t)t; j < batch.size(); j += (size_t)ntasks)
+        // wake-ups than the copy (tools/latency_probe.py, one 4 KiB buffer). Otherwise the pool copies
+        // pieces of at most 4 MiB, so one large buffer is not one thread's memcpy (~10 GB/s)
+        if (off <= (1u << 20)) {
+            for (size_t j = 0; j < batch.size(); ++j)
                 if (hlen[j]) memcpy(c->h_stage[s] + hoff[j], src(batch[j]), hlen[j]);
-        };
-        if (ntasks == 1)
-            fill(0);
-        else
-            c->pool->parallel_for(ntasks, fill);
+        } else {
+            constexpr uint64_t kPiece = 4ull << 20;
+            std::vector<std::array<uint64_t, 3>> pieces;  // (j, lo, hi) of item j's bytes
+            for (size_t j = 0; j < batch.size(); ++j)
+                for (uint64_t lo = 0; lo < hlen[j]; lo += kPiece) pieces.push_back({j, lo, std::min(hlen[j], lo + kPiece)});
+            const int ntasks = (int)std::min<size_t>(pieces.size(), (size_t)c->pool->size() * 4);
+            c->pool->parallel_for(ntasks, [&](int t) {
+                for (size_t k = (size_t)t; k < pieces.size(); k += (size_t)ntasks) {
+                    const auto& pc = pieces[k];
+                    memcpy(c->h_stage[s] + hoff[pc[0]] + pc[1], src(batch[pc[0]]) + pc[1], pc[2] - pc[1]);
+                }
+            });
+        }
         const double t2 = Trace::now();
         tr.fill += t2 - t1;
         if (int rc = submit_slot(c, s, off, batch.size(), short_only_lane && all_short,
