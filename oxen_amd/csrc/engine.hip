@@ -3,6 +3,8 @@
 // pipeline over every queued request. See capi_internal.hpp for the pieces.
 #include "capi_internal.hpp"
 
+#include <sys/syscall.h>
+
 using namespace oxh::capi;
 
 // ---------------------------------------------------------------- streaming file engine
@@ -52,9 +54,11 @@ struct SlotRun {  // a submitted slot
 // A file of at least kSplitBytes in a slot is read in kPartBytes parts by several readers: one pread
 // stream from the page cache copies ~5-10 GB/s, so a slot holding one 200 MiB file waited ~30 ms on
 // its reader. The parts together read [0, L + 1), one byte past the expected size, as read_expected does.
-// Readers have file-descriptor tables of their own (pool.hpp), so each part opens the path itself and
-// checks that it names the file the first reader opened (device + inode); a file replaced meanwhile is
-// re-read whole by the engine, as one whose size changed.
+// Readers have file-descriptor tables of their own (pool.hpp), so a part reopens the first reader's
+// open file through /proc/self/task/<tid>/fd/<fd>: the same inode even if the path was replaced or
+// unlinked since, as the reference's one File handle reads it (hasher.rs:126-148). The first reader
+// keeps its descriptor until every part has opened its own (reading parts meanwhile). Without /proc a
+// part opens the path and checks device + inode; a replaced file is then re-read whole by the engine.
 // OXH_SPLIT_READS=0: one pread per file (the r01-r06 form, for A/B).
 constexpr uint64_t kPartBytes = 4ull << 20, kSplitBytes = 8ull << 20;
 inline bool split_reads() {
@@ -69,6 +73,9 @@ struct PartFile {  // one split file, shared by its parts: the reader that finis
     ino_t ino = 0;
     int s = 0;
     uint8_t* dst = nullptr;
+    char link[64] = {};                 // /proc/self/task/<first reader's tid>/fd/<its descriptor>
+    std::atomic<int> opened{0};         // parts (other than part 0) that have opened their descriptor
+    std::atomic<int> refs{2};           // the completing reader and the first reader: the last one deletes
     std::atomic<int> left{0};
     std::atomic<int> err{0};            // errno of a failed pread (the first one recorded)
     std::atomic<bool> failed{false};
@@ -334,7 +341,9 @@ void run_part(FileStream& fs, const PartTask& t, int own_fd = -1) {
     uint64_t got = 0;
     int fd = own_fd;
     if (fd < 0) {
-        fd = open(f->r->paths[f->i], O_RDONLY | O_CLOEXEC | O_NONBLOCK);
+        fd = open(f->link, O_RDONLY | O_CLOEXEC | O_NONBLOCK);
+        f->opened.fetch_add(1, std::memory_order_acq_rel);  // the first reader may close its descriptor now
+        if (fd < 0) fd = open(f->r->paths[f->i], O_RDONLY | O_CLOEXEC | O_NONBLOCK);  // no /proc
         struct stat sb;
         if (fd >= 0 && (fstat(fd, &sb) != 0 || sb.st_dev != f->dev || sb.st_ino != f->ino)) {
             close(fd);
@@ -362,7 +371,7 @@ void run_part(FileStream& fs, const PartTask& t, int own_fd = -1) {
     if (f->failed.load()) item_failed(f->r, f->i, OXH_ERR_IO, f->err.load());
     else if (f->resized.load()) item_resized(fs, f->r, f->i, f->s, f->j);
     const int s = f->s;
-    delete f;
+    if (f->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) delete f;
     slot_item_done(fs, s);
 }
 
@@ -437,6 +446,7 @@ void reader_loop(FileStream& fs) {
                 auto* f = new PartFile;
                 f->r = r, f->i = i, f->j = j, f->L = L, f->s = s, f->dst = c->h_stage[s] + off;
                 f->dev = fsb.st_dev, f->ino = fsb.st_ino;
+                snprintf(f->link, sizeof f->link, "/proc/self/task/%ld/fd/%d", (long)syscall(SYS_gettid), fd);
                 const uint64_t nparts = (L + kPartBytes) / kPartBytes;  // over [0, L + 1)
                 f->left.store((int)nparts);
                 {
@@ -447,7 +457,12 @@ void reader_loop(FileStream& fs) {
                 }
                 c->qcv.notify_all();
                 run_part(fs, {f, 0, kPartBytes}, fd);
+                // the descriptor stays open until every other part has reopened it (this reader reads
+                // queued parts meanwhile, its own among them, so the wait always ends)
+                while (f->opened.load(std::memory_order_acquire) < (int)nparts - 1 && !fs.abort.load(std::memory_order_relaxed))
+                    if (!help_with_a_part(fs)) pause_us(2);
                 close(fd);
+                if (f->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) delete f;
                 continue;
             }
             int e = 0;

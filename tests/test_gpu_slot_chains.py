@@ -169,3 +169,44 @@ def test_split_reads_small_slots(cuda, oracle_lib, tmp_path):
         for _ in range(2):
             d, got, st = hasher.hash_files_128bit(paths, ctx=c)
             assert d == want and got == sizes and not any(st)
+
+
+def test_split_reads_under_replacement(ctx, oracle_lib, tmp_path):
+    """A 20 MiB file replaced (new content, temp + rename) and briefly removed while it is hashed again
+    and again: every answer is one whole version of the file (the parts read the inode the first reader
+    opened) or, when the path did not exist at the open, OXH_ERR_OPEN with ENOENT."""
+    import errno
+    import os
+    import threading
+
+    from oxen_amd import _capi, hasher
+
+    p = tmp_path / "hot.bin"
+    versions = _blobs([20 * MIB + 11, 20 * MIB - 5, 12 * MIB, 9 * MIB + 1], 80)
+    digests = {oracle_lib.xxh3_128_int(v) for v in versions}
+    p.write_bytes(versions[0])
+    stop = threading.Event()
+
+    def mutate():
+        k = 0
+        while not stop.is_set():
+            k += 1
+            tmp = tmp_path / "hot.tmp"
+            tmp.write_bytes(versions[k % len(versions)])
+            if k % 5 == 0:
+                os.remove(p)
+            os.replace(tmp, p)
+
+    th = threading.Thread(target=mutate)
+    th.start()
+    seen = set()
+    try:
+        for _ in range(60):
+            d, _, st, oserr = hasher.hash_files_with_errors_128bit([str(p)] * 9, ctx=ctx)  # 9: the engine
+            for dg, s, e in zip(d, st, oserr):
+                assert (s == 0 and dg in digests) or (s == _capi.OXH_ERR_OPEN and e == errno.ENOENT), (s, e)
+                seen.add(dg)
+    finally:
+        stop.set()
+        th.join()
+    assert len(seen - {None}) >= 2  # the test did race the replacements
