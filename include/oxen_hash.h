@@ -132,7 +132,10 @@ int oxh_hash_buffers(oxh_ctx* ctx, const uint8_t* const* bufs, const uint64_t* l
  * files of the call are unaffected; digest 0 on error). Files are read to EOF: one whose size
  * differs from its stat (or, below, from the caller's size) is re-read, so the digest covers what
  * the read returned, like read_to_end (hasher.rs:126-148).
- * `sizes` and `status` may be NULL. oxh_hash_files_ex also returns the errno of each failure. */
+ * A call of at most 8 files and 2 MiB on a context with no file request in flight runs on the caller's
+ * thread (the same reads and kernels, no engine hand-offs; the thread's current HIP device is restored
+ * before return); other calls are requests to the context's engine thread. Either way the results are
+ * the same. `sizes` and `status` may be NULL. oxh_hash_files_ex also returns the errno of each failure. */
 int oxh_hash_files(oxh_ctx* ctx, const char* const* paths, uint64_t n, uint64_t* out,
                    uint64_t* sizes, int32_t* status);
 
