@@ -1004,7 +1004,10 @@ int direct_files(oxh_ctx* c, FileRequest& r) {
     if (cnt) {
         c->where.store("direct: submit_slot");
         const bool text = r.counts != nullptr, utf8 = r.utf8 != nullptr;
-        if (int rc = submit_slot(c, s, bytes, cnt, false, bytes / cnt <= kShortItemBytes, text, utf8)) return rc;
+        bool packed = false;
+        if (int rc = submit_packed(c, s, bytes, cnt, bytes / cnt <= kShortItemBytes, text, utf8, packed)) return rc;
+        if (!packed)
+            if (int rc = submit_slot(c, s, bytes, cnt, false, bytes / cnt <= kShortItemBytes, text, utf8)) return rc;
         Pending p;
         p.busy = true;
         p.ids.assign(idx, idx + cnt);

@@ -114,6 +114,42 @@ int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_
     return OXH_OK;
 }
 
+// One small batch of the caller's thread (engine.hip direct_files), items below kSlotChainBytes: their
+// descriptors go into the slot right after their bytes, so ONE H2D on the compute stream carries both
+// (no copy-stream hop, no event between the streams), then K1 / K1T (+ is_utf8), D2H and the done
+// event. Each host-to-device copy costs ~5 us of a small call's ~40 us round trip. False: it does not
+// fit (the caller takes submit_slot). OXH_DIRECT_PACKED=0: always submit_slot.
+int submit_packed(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool short_items, bool text, bool utf8, bool& done) {
+    static const bool on = !(getenv("OXH_DIRECT_PACKED") && atoi(getenv("OXH_DIRECT_PACKED")) == 0);
+    const uint64_t M = c->max_items, doff = align_up(bytes);
+    done = false;
+    if (!on || doff + 16 * cnt > c->stage_bytes) return OXH_OK;
+    for (uint64_t j = 0; j < cnt; ++j)
+        if (c->h_desc[s][M + j] >= kSlotChainBytes) return OXH_OK;
+    uint64_t* hd = reinterpret_cast<uint64_t*>(c->h_stage[s] + doff);
+    memcpy(hd, c->h_desc[s], cnt * 8);
+    memcpy(hd + cnt, c->h_desc[s] + M, cnt * 8);
+    const uint64_t* d_offs = reinterpret_cast<const uint64_t*>(c->d_stage[s] + doff);
+    const uint64_t* d_lens = d_offs + cnt;
+    c->where.store("submit_packed: H2D");
+    HIP_TRY(hipMemcpyAsync(c->d_stage[s], c->h_stage[s], doff + 16 * cnt, hipMemcpyHostToDevice, c->stream));
+    int rc = text ? launch_text(c->d_stage[s], d_offs, d_lens, cnt, c->d_out[s], c->d_cnt[s], c->stream, short_items)
+                  : launch_wave(c->d_stage[s], d_offs, d_lens, cnt, c->d_out[s], c->stream,
+                                short_items ? ItemShape::Short : ItemShape::Long);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(c->h_out[s], c->d_out[s], cnt * 16, hipMemcpyDeviceToHost, c->stream));
+    if (text) HIP_TRY(hipMemcpyAsync(c->h_cnt[s], c->d_cnt[s], cnt * 16, hipMemcpyDeviceToHost, c->stream));
+    if (utf8) {
+        hipLaunchKernelGGL(oxh::utf8_prefix_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, c->stream, c->d_stage[s],
+                           d_offs, d_lens, cnt, c->d_utf8[s]);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(c->h_utf8[s], c->d_utf8[s], cnt * 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_TRY(hipEventRecord(c->ev_done[s], c->stream));
+    done = true;
+    return OXH_OK;
+}
+
 // Wait for slot s's digests. Polls (a slot is at most a few hundred MiB: milliseconds of work) and,
 // after OXH_WAIT_LIMIT_S seconds (default 60), reports which stage never finished instead of
 // blocking forever.
@@ -248,9 +284,13 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
         }
         const double t2 = Trace::now();
         tr.fill += t2 - t1;
-        if (int rc = submit_slot(c, s, off, batch.size(), short_only_lane && all_short,
-                                 off / std::max<uint64_t>(1, batch.size()) <= kShortItemBytes, false))
-            return rc;
+        // a call that is one small batch: descriptors packed after the bytes, one H2D (submit_packed)
+        bool packed = false;
+        const bool short_items = off / std::max<uint64_t>(1, batch.size()) <= kShortItemBytes;
+        if (off <= (1u << 20) && i == n && tr.batches == 0 && !(short_only_lane && all_short))
+            if (int rc = submit_packed(c, s, off, batch.size(), short_items, false, false, packed)) return rc;
+        if (!packed)
+            if (int rc = submit_slot(c, s, off, batch.size(), short_only_lane && all_short, short_items, false)) return rc;
         tr.submit += Trace::now() - t2;
         tr.batches++;
         pend[s].busy = true;
