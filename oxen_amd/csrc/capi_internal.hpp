@@ -225,7 +225,8 @@ int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_
                 bool utf8 = false);
 // A small batch of items below kSlotChainBytes with its descriptors packed after its bytes: one H2D on the
 // compute stream (engine.hip direct_files). `done` false: not taken (does not fit, or disabled).
-int submit_packed(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool short_items, bool text, bool utf8, bool& done);
+int submit_packed(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool short_items, bool text, bool utf8, bool& done,
+                  bool lane = false);
 // Wait for slot s's digests (bounded by OXH_WAIT_LIMIT_S, which reports the stalled stage).
 int wait_slot(oxh_ctx* c, int s, const Pending& p);
 // Scatter slot s's digests to the caller's table (host-buffer batches: oxh_hash_buffers/_streams).

@@ -119,7 +119,8 @@ int submit_slot(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool any_short_
 // (no copy-stream hop, no event between the streams), then K1 / K1T (+ is_utf8), D2H and the done
 // event. Each host-to-device copy costs ~5 us of a small call's ~40 us round trip. False: it does not
 // fit (the caller takes submit_slot). OXH_DIRECT_PACKED=0: always submit_slot.
-int submit_packed(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool short_items, bool text, bool utf8, bool& done) {
+int submit_packed(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool short_items, bool text, bool utf8, bool& done,
+                  bool lane) {
     static const bool on = !(getenv("OXH_DIRECT_PACKED") && atoi(getenv("OXH_DIRECT_PACKED")) == 0);
     const uint64_t M = c->max_items, doff = align_up(bytes);
     done = false;
@@ -133,9 +134,10 @@ int submit_packed(oxh_ctx* c, int s, uint64_t bytes, uint64_t cnt, bool short_it
     const uint64_t* d_lens = d_offs + cnt;
     c->where.store("submit_packed: H2D");
     HIP_TRY(hipMemcpyAsync(c->d_stage[s], c->h_stage[s], doff + 16 * cnt, hipMemcpyHostToDevice, c->stream));
-    int rc = text ? launch_text(c->d_stage[s], d_offs, d_lens, cnt, c->d_out[s], c->d_cnt[s], c->stream, short_items)
-                  : launch_wave(c->d_stage[s], d_offs, d_lens, cnt, c->d_out[s], c->stream,
-                                short_items ? ItemShape::Short : ItemShape::Long);
+    int rc = text   ? launch_text(c->d_stage[s], d_offs, d_lens, cnt, c->d_out[s], c->d_cnt[s], c->stream, short_items)
+             : lane ? launch_lane(c->d_stage[s], d_offs, d_lens, cnt, c->d_out[s], c->stream)
+                    : launch_wave(c->d_stage[s], d_offs, d_lens, cnt, c->d_out[s], c->stream,
+                                  short_items ? ItemShape::Short : ItemShape::Long);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(c->h_out[s], c->d_out[s], cnt * 16, hipMemcpyDeviceToHost, c->stream));
     if (text) HIP_TRY(hipMemcpyAsync(c->h_cnt[s], c->d_cnt[s], cnt * 16, hipMemcpyDeviceToHost, c->stream));
@@ -287,8 +289,9 @@ static int hash_host_items(oxh_ctx* c, uint64_t n, const uint64_t* lens,
         // a call that is one small batch: descriptors packed after the bytes, one H2D (submit_packed)
         bool packed = false;
         const bool short_items = off / std::max<uint64_t>(1, batch.size()) <= kShortItemBytes;
-        if (off <= (1u << 20) && i == n && tr.batches == 0 && !(short_only_lane && all_short))
-            if (int rc = submit_packed(c, s, off, batch.size(), short_items, false, false, packed)) return rc;
+        if (off <= (1u << 20) && i == n && tr.batches == 0)
+            if (int rc = submit_packed(c, s, off, batch.size(), short_items, false, false, packed, short_only_lane && all_short))
+                return rc;
         if (!packed)
             if (int rc = submit_slot(c, s, off, batch.size(), short_only_lane && all_short, short_items, false)) return rc;
         tr.submit += Trace::now() - t2;
@@ -377,9 +380,13 @@ static int hash_stream_spans(oxh_ctx* c, const uint8_t* streams, const uint64_t*
         }
         const double t2 = Trace::now();
         tr.fill += t2 - t1;
-        if (int rc = submit_slot(c, s, span, batch.size(), all_short, span / std::max<uint64_t>(1, batch.size()) <= kShortItemBytes,
-                                 false))
-            return rc;
+        // a call that is one small span: descriptors packed after the bytes, one H2D (submit_packed)
+        bool packed = false;
+        const bool short_items = span / std::max<uint64_t>(1, batch.size()) <= kShortItemBytes;
+        if (span <= (1u << 20) && k == n && tr.batches == 0)
+            if (int rc = submit_packed(c, s, span, batch.size(), short_items, false, false, packed, all_short)) return rc;
+        if (!packed)
+            if (int rc = submit_slot(c, s, span, batch.size(), all_short, short_items, false)) return rc;
         tr.submit += Trace::now() - t2;
         tr.batches++;
         pend[s].busy = true;

@@ -84,6 +84,8 @@ def main():
         res["batch64_cpu_1thread_us"] = med_us(lambda: oracle.hash_files(batch, threads=1), a.calls)
         buf = rng.integers(0, 256, 4096, dtype=np.uint8).tobytes()
         res["buffer_4k_us"] = med_us(lambda: hasher.hash_buffers_128bit([buf], ctx), a.calls)
+        streams = [bytes(rng.integers(0, 256, int(rng.integers(5, 200)), dtype=np.uint8)) for _ in range(50)]
+        res["streams_50_short_us"] = med_us(lambda: hasher.hash_streams_128bit(streams, ctx), a.calls)
         buf1m = open(files["1m"], "rb").read()
         res["buffer_1m_us"] = med_us(lambda: hasher.hash_buffers_128bit([buf1m], ctx), a.calls)
         res["read_1m_us"] = med_us(lambda: open(files["1m"], "rb").read(), a.calls)
